@@ -1,0 +1,96 @@
+/*
+ * lz4mt_hip.h — MI355X extensions to the lz4mt C ABI (liblz4mt_amd.so).
+ *
+ * Three layers, all plain C types (pointers, sizes, an opaque stream):
+ *
+ * 1. Block operators with exactly the reference's plugin signatures
+ *    (typedefs Lz4MtCompress / Lz4MtCompressBound / Lz4MtDecompress,
+ *    reference src/lz4mt.h:41-58).  Assign them to ctx.compress /
+ *    ctx.compressBound / ctx.decompress and the reference-shaped host
+ *    scheduler (lz4mtCompress in PARALLEL/SEQUENTIAL mode) runs every block
+ *    on the GPU.  Host pointers; each call stages through device memory.
+ *    They replace LZ4_compress_limitedOutput / LZ4_compressBound /
+ *    LZ4_decompress_safe as wired in reference src/main.cpp:749-751,767-785.
+ *
+ * 2. Device-resident frame engine: one call compresses or decompresses a
+ *    whole lz4mt frame whose input and output already live in HBM
+ *    (the performance path; used by lz4mtCompress/lz4mtDecompress in
+ *    LZ4MT_MODE_DEVICE and by bench.py).
+ *
+ * 3. Utilities: synthetic input generator, XXH32, device info.
+ *
+ * Streams are hipStream_t passed as void* (NULL = default stream).
+ * Every function fails loudly (returns LZ4MT_RESULT_ERROR / a negative
+ * value) when no HIP device is present; nothing falls back to the CPU.
+ */
+#ifndef LZ4MT_AMD_LZ4MT_HIP_H
+#define LZ4MT_AMD_LZ4MT_HIP_H
+
+#include "lz4mt.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- 1. block operators (reference plugin signatures) ------------------ */
+/* LZ4_compress_limitedOutput semantics (lz4 1.9.3, acceleration 1):
+ * returns the compressed size, or 0 when it does not fit maxOutputSize.
+ * compressionLevel >= 3 (HC) is not provided on the GPU: returns 0, so the
+ * block is stored raw (a valid frame, but not LZ4-HC bytes). */
+int lz4mtHipCompressBlock(const char* src, char* dst, int isize, int maxOutputSize, int compressionLevel);
+/* LZ4_compressBound. */
+int lz4mtHipCompressBound(int isize);
+/* LZ4_decompress_safe semantics: decoded size, or a negative value. */
+int lz4mtHipDecompressBlock(const char* src, char* dst, int isize, int maxOutputSize);
+
+/* ---- 2. device-resident frame engine ----------------------------------- */
+/* Upper bound of a frame for srcSize input bytes under `sd`. */
+uint64_t lz4mtHipFrameBound(uint64_t srcSize, const Lz4MtStreamDescriptor* sd);
+/* Scratch bytes lz4mtHipCompressFrame needs for srcSize (slots + tables). */
+uint64_t lz4mtHipCompressWorkspaceSize(uint64_t srcSize, const Lz4MtStreamDescriptor* sd);
+/* Compresses d_src[0..srcSize) into one frame at d_frame (device memory).
+ * d_workspace may be NULL (the library then allocates and frees scratch).
+ * *frameSize (host) receives the frame length; the call synchronises the
+ * stream once at the end to read it.  Block independence is required
+ * (blockIndependence = 0 returns BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET). */
+Lz4MtResult lz4mtHipCompressFrame(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
+                                  uint64_t* frameSize, const Lz4MtStreamDescriptor* sd,
+                                  void* d_workspace, uint64_t workspaceSize, void* stream);
+/* Asynchronous variant: *d_frameSize is device memory, nothing is
+ * synchronised (the stream carries the dependency). */
+Lz4MtResult lz4mtHipCompressFrameAsync(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
+                                       uint64_t* d_frameSize, const Lz4MtStreamDescriptor* sd,
+                                       void* d_workspace, uint64_t workspaceSize, void* stream);
+
+/* Parses the frame header at d_frame (one small device->host copy) and
+ * reports its descriptor, header length and an upper bound of the decoded
+ * size (blocks x blockMax, from a device walk of the block size words). */
+Lz4MtResult lz4mtHipFrameInfo(const void* d_frame, uint64_t frameSize, Lz4MtStreamDescriptor* sd,
+                              uint64_t* decodedBound, uint64_t* nBlocks, void* stream);
+/* Decompresses every frame in d_frame[0..frameSize) (concatenated frames
+ * and skippable frames included) into d_out.  outCap must hold
+ * (blocks x blockMax) bytes of the last frame (see lz4mtHipFrameInfo).
+ * *outSize receives the decoded length; `sd` the last frame's descriptor.
+ * Result codes follow lz4mtDecompress (reference src/lz4mt.cpp:938-1011). */
+Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t frameSize, void* d_out, uint64_t outCap,
+                                    uint64_t* outSize, Lz4MtStreamDescriptor* sd, void* stream);
+
+/* ---- 3. utilities ------------------------------------------------------- */
+/* SURVEY.md App. F generator, bit-identical to the CPU oracle. */
+int lz4mtHipGenSynthetic(void* d_dst, uint64_t n, uint64_t seed, void* stream);
+/* XXH32 (seed 0) of device memory; synchronises the stream. */
+uint32_t lz4mtHipXxh32(const void* d_src, uint64_t len, void* stream);
+/* Number of HIP devices visible (0 = none: every compute entry point errors). */
+int lz4mtHipDeviceCount(void);
+
+/* Per-stage device timings (ms, hipEvents) of the last frame call on this
+ * thread: [0] encode/decode kernel, [1] checksum kernel(s), [2] scan +
+ * assemble / walk + verify, [3] whole call.  Enabled by
+ * lz4mtHipSetTiming(1) (adds event records, no synchronisation). */
+void lz4mtHipSetTiming(int enable);
+int lz4mtHipGetTimings(float* ms4);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

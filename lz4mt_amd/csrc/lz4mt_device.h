@@ -1,0 +1,64 @@
+// lz4mt_device.h — shared declarations between the HIP kernels
+// (lz4mt_kernels.hip) and the host engine (lz4mt_engine.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lz4mt {
+
+// LZ4 1.9.3 constants.
+constexpr int kMinMatch = 4;
+constexpr int kLastLiterals = 5;
+constexpr int kMfLimit = 12;
+constexpr int kMinLength = 13;
+constexpr uint32_t kDistMax = 65535;
+constexpr int kLimit64K = 65547;
+
+// Decoder status codes beyond LZ4_decompress_safe's own negative values.
+constexpr int kDecodeOutputTooSmall = INT32_MIN;   // physical slot smaller than the decoded block
+
+// Per-block record of a parsed frame (device-resident, one per block).
+struct BlockRec {
+    uint64_t offset;     // payload offset inside the frame
+    uint32_t bits;       // size word: stored size | 0x80000000 if raw
+    uint32_t checksum;   // block XXH32 read from the frame (if FLG.4)
+};
+
+// Frame-walk summary written by the walk kernel.
+struct WalkInfo {
+    uint64_t endPos;     // position just after the EOS word
+    uint32_t nBlocks;
+    int32_t  result;     // Lz4MtResult code (0 = OK)
+};
+
+// ---- kernel launchers (lz4mt_kernels.hip) ----
+hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                         uint8_t* slots, uint64_t slotStride, uint32_t capOverride, int32_t* csize,
+                         hipStream_t st);
+hipError_t launch_decode(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax,
+                         uint8_t* out, uint64_t outCap, int32_t* dsize, hipStream_t st);
+hipError_t launch_xxh32_blocks(const uint8_t* base, const uint64_t* offs, const uint32_t* lens, uint32_t nBlocks,
+                               uint32_t* digest, hipStream_t st);
+hipError_t launch_xxh32_stored(const uint8_t* src, const uint8_t* slots, uint64_t srcSize, uint32_t blockSize,
+                               uint32_t nBlocks, const int32_t* csize, uint32_t* digest, hipStream_t st);
+hipError_t launch_xxh32_frame_blocks(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t* digest,
+                                     hipStream_t st);
+hipError_t launch_xxh32_stream(const uint8_t* p, uint64_t len, uint32_t* digest, hipStream_t st);
+hipError_t launch_frame_scan(const int32_t* csize, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                             int blockChecksum, uint64_t* recOff, hipStream_t st);
+hipError_t launch_frame_assemble(const uint8_t* src, const uint8_t* slots, uint64_t srcSize, uint32_t blockSize,
+                                 uint32_t nBlocks, const int32_t* csize, const uint32_t* bsum,
+                                 const uint64_t* recOff, int blockChecksum, uint8_t* frame, uint32_t hdrLen,
+                                 hipStream_t st);
+hipError_t launch_frame_finalize(uint8_t* frame, const uint8_t* hdr, uint32_t hdrLen, const uint64_t* recOff,
+                                 uint32_t nBlocks, const uint32_t* streamSum, uint64_t* frameSize,
+                                 hipStream_t st);
+hipError_t launch_frame_walk(const uint8_t* frame, uint64_t frameSize, uint64_t bodyPos, uint32_t blockMax,
+                             int blockChecksum, uint32_t maxBlocks, BlockRec* recs, WalkInfo* info,
+                             hipStream_t st);
+hipError_t launch_block_verify(const BlockRec* recs, uint32_t nBlocks, const uint32_t* digest, const int32_t* dsize,
+                               uint32_t blockMax, int blockChecksum, int32_t* status, hipStream_t st);
+hipError_t launch_gen_synthetic(uint8_t* dst, uint64_t n, uint64_t seed, hipStream_t st);
+
+}  // namespace lz4mt

@@ -1,0 +1,528 @@
+// lz4mt_engine.hip — host side of the device engine: the lz4mt_hip.h C ABI.
+//
+// Compress path (device-resident frame, one lz4mt frame per call):
+//   k_encode (wave per block, slots of blockMax) -> k_xxh32_stored (if FLG.4)
+//   -> k_frame_scan (record offsets) -> k_frame_assemble (scatter into the
+//   frame) -> [k_xxh32_stream if FLG.2] -> k_frame_finalize (header, EOS,
+//   content checksum).  Replaces lz4mt's compress() scheduler and ordered
+//   write chain (reference src/lz4mt.cpp:372-457, 898-935).
+// Decompress path: host parses the header (one small D2H copy), k_frame_walk
+//   builds the block table, k_decode (wave per block) -> k_xxh32_frame_blocks
+//   + k_block_verify -> [k_xxh32_stream].  Replaces decompress() and
+//   lz4mtDecompress (src/lz4mt.cpp:593-734, 938-1011).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "../../include/lz4mt_hip.h"
+#include "lz4mt_device.h"
+#include "lz4mt_host.h"
+
+using namespace lz4mt;
+
+namespace {
+
+#define HIPCHK(x)                                   \
+    do {                                            \
+        if ((x) != hipSuccess) return LZ4MT_RESULT_ERROR; \
+    } while (0)
+
+inline uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+bool have_device() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return false;
+    return n > 0;
+}
+
+// ---- optional per-stage timing (thread-local hipEvents) -------------------
+struct Timing {
+    bool enabled = false;
+    bool valid = false;
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    void mark(int i, hipStream_t st) {
+        if (!enabled) return;
+        if (!ev[i]) hipEventCreate(&ev[i]);
+        hipEventRecord(ev[i], st);
+        if (i == 4) valid = true;
+    }
+};
+thread_local Timing g_timing;
+
+// ---- workspace layout for one compressed frame ----------------------------
+struct CompressWs {
+    uint8_t* slots;
+    int32_t* csize;
+    uint32_t* bsum;
+    uint64_t* recOff;
+    uint32_t* ssum;
+    uint64_t* fsize;
+    uint64_t bytes;
+};
+
+CompressWs carve_compress(uint8_t* base, uint64_t nb, uint64_t bm) {
+    CompressWs w{};
+    uint64_t o = 0;
+    auto take = [&](uint64_t n) { uint8_t* p = base ? base + o : nullptr; o = align_up(o + n, 256); return p; };
+    w.slots = take(nb * bm + 64);
+    w.csize = reinterpret_cast<int32_t*>(take((nb + 1) * 4));
+    w.bsum = reinterpret_cast<uint32_t*>(take((nb + 1) * 4));
+    w.recOff = reinterpret_cast<uint64_t*>(take((nb + 1) * 8));
+    w.ssum = reinterpret_cast<uint32_t*>(take(16));
+    w.fsize = reinterpret_cast<uint64_t*>(take(16));
+    w.bytes = o;
+    return w;
+}
+
+// ---- thread-local scratch for the block operators -------------------------
+struct BlockScratch {
+    hipStream_t st = nullptr;
+    uint8_t* dIn = nullptr;
+    uint8_t* dOut = nullptr;
+    uint64_t capIn = 0, capOut = 0;
+    int32_t* dRes = nullptr;
+    BlockRec* dRec = nullptr;
+    bool init() {
+        if (st) return true;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
+        if (hipMalloc(&dRes, 256) != hipSuccess) return false;
+        if (hipMalloc(&dRec, 256) != hipSuccess) return false;
+        return true;
+    }
+    bool ensure(uint64_t in, uint64_t out) {
+        if (in + 64 > capIn) {
+            if (dIn) hipFree(dIn);
+            capIn = std::max<uint64_t>(align_up(in + 64, 1 << 20), 1 << 20);
+            if (hipMalloc(&dIn, capIn) != hipSuccess) { dIn = nullptr; capIn = 0; return false; }
+        }
+        if (out + 64 > capOut) {
+            if (dOut) hipFree(dOut);
+            capOut = std::max<uint64_t>(align_up(out + 64, 1 << 20), 1 << 20);
+            if (hipMalloc(&dOut, capOut) != hipSuccess) { dOut = nullptr; capOut = 0; return false; }
+        }
+        return true;
+    }
+};
+thread_local BlockScratch g_blk;
+
+}  // namespace
+
+// ===========================================================================
+// internal C++ API shared with the host frame engine (lz4mt_frame.cpp)
+// ===========================================================================
+namespace lz4mt {
+
+// Compresses nb blocks (block b = src[b*bm, ...), last block short) into a
+// frame BODY (records only) at `body`; total body size written to
+// d_bodySize.  Used by the frame call and by the batched DEVICE mode.
+Lz4MtResult device_compress_body(const uint8_t* src, uint64_t n, uint32_t bm, int blockChecksum, uint8_t* ws,
+                                 uint8_t* body, uint32_t hdrLen, hipStream_t st, uint64_t** d_recOffOut) {
+    const uint64_t nb = (n + bm - 1) / bm;
+    CompressWs w = carve_compress(ws, nb, bm);
+    g_timing.mark(0, st);
+    HIPCHK(launch_encode(src, n, bm, (uint32_t)nb, w.slots, bm, 0xFFFFFFFFu, w.csize, st));
+    g_timing.mark(1, st);
+    if (blockChecksum) HIPCHK(launch_xxh32_stored(src, w.slots, n, bm, (uint32_t)nb, w.csize, w.bsum, st));
+    g_timing.mark(2, st);
+    HIPCHK(launch_frame_scan(w.csize, n, bm, (uint32_t)nb, blockChecksum, w.recOff, st));
+    HIPCHK(launch_frame_assemble(src, w.slots, n, bm, (uint32_t)nb, w.csize, w.bsum, w.recOff, blockChecksum, body,
+                                 hdrLen, st));
+    if (d_recOffOut) *d_recOffOut = w.recOff;
+    return LZ4MT_RESULT_OK;
+}
+
+uint64_t compress_ws_bytes(uint64_t n, uint32_t bm) { return carve_compress(nullptr, (n + bm - 1) / bm, bm).bytes; }
+
+}  // namespace lz4mt
+
+// ===========================================================================
+// 1. block operators
+// ===========================================================================
+extern "C" int lz4mtHipCompressBound(int isize) {
+    return ((unsigned)isize > 0x7E000000u) ? 0 : isize + isize / 255 + 16;
+}
+
+extern "C" int lz4mtHipCompressBlock(const char* src, char* dst, int isize, int maxOutputSize, int compressionLevel) {
+    if (compressionLevel >= 3) return 0;   // no GPU LZ4-HC: caller stores the block raw
+    if (isize < 0 || (unsigned)isize > 0x7E000000u) return 0;
+    if (maxOutputSize < 0) maxOutputSize = 0;
+    if (!have_device() || !g_blk.init()) return -1;
+    const int bound = lz4mtHipCompressBound(isize);
+    const uint64_t outMax = (uint64_t)std::min(maxOutputSize, bound) + 16;
+    if (!g_blk.ensure((uint64_t)isize, outMax)) return -1;
+    if (isize && hipMemcpyAsync(g_blk.dIn, src, (size_t)isize, hipMemcpyHostToDevice, g_blk.st) != hipSuccess) return -1;
+    if (launch_encode(g_blk.dIn, (uint64_t)isize, (uint32_t)std::max(isize, 1), 1, g_blk.dOut, 0,
+                      (uint32_t)maxOutputSize, g_blk.dRes, g_blk.st) != hipSuccess)
+        return -1;
+    int32_t r = 0;
+    if (hipMemcpyAsync(&r, g_blk.dRes, 4, hipMemcpyDeviceToHost, g_blk.st) != hipSuccess) return -1;
+    if (hipStreamSynchronize(g_blk.st) != hipSuccess) return -1;
+    if (r > 0) {
+        if (hipMemcpyAsync(dst, g_blk.dOut, (size_t)r, hipMemcpyDeviceToHost, g_blk.st) != hipSuccess) return -1;
+        if (hipStreamSynchronize(g_blk.st) != hipSuccess) return -1;
+    }
+    return r;
+}
+
+extern "C" int lz4mtHipDecompressBlock(const char* src, char* dst, int isize, int maxOutputSize) {
+    if (isize < 0 || maxOutputSize < 0) return -1;
+    if (!have_device() || !g_blk.init()) return -1;
+    if (!g_blk.ensure((uint64_t)isize, (uint64_t)maxOutputSize)) return -1;
+    if (isize && hipMemcpyAsync(g_blk.dIn, src, (size_t)isize, hipMemcpyHostToDevice, g_blk.st) != hipSuccess) return -1;
+    BlockRec rec{0, (uint32_t)isize, 0};
+    if (hipMemcpyAsync(g_blk.dRec, &rec, sizeof(rec), hipMemcpyHostToDevice, g_blk.st) != hipSuccess) return -1;
+    if (launch_decode(g_blk.dIn, g_blk.dRec, 1, (uint32_t)maxOutputSize, g_blk.dOut, (uint64_t)maxOutputSize,
+                      g_blk.dRes, g_blk.st) != hipSuccess)
+        return -1;
+    int32_t r = 0;
+    if (hipMemcpyAsync(&r, g_blk.dRes, 4, hipMemcpyDeviceToHost, g_blk.st) != hipSuccess) return -1;
+    if (hipStreamSynchronize(g_blk.st) != hipSuccess) return -1;
+    if (r > 0) {
+        if (hipMemcpyAsync(dst, g_blk.dOut, (size_t)r, hipMemcpyDeviceToHost, g_blk.st) != hipSuccess) return -1;
+        if (hipStreamSynchronize(g_blk.st) != hipSuccess) return -1;
+    }
+    return r == kDecodeOutputTooSmall ? -1 : r;
+}
+
+// ===========================================================================
+// 2. device-resident frame engine
+// ===========================================================================
+extern "C" uint64_t lz4mtHipFrameBound(uint64_t srcSize, const Lz4MtStreamDescriptor* sd) {
+    const int id = sd ? sd->bd.blockMaximumSize : 7;
+    const uint64_t bm = (id >= 4 && id <= 7) ? (uint64_t)block_max_bytes(id) : (4u << 20);
+    const uint64_t nb = (srcSize + bm - 1) / bm;
+    return (uint64_t)kMaxHeader + srcSize + nb * 8 + 8;
+}
+
+extern "C" uint64_t lz4mtHipCompressWorkspaceSize(uint64_t srcSize, const Lz4MtStreamDescriptor* sd) {
+    const int id = sd ? sd->bd.blockMaximumSize : 7;
+    const uint32_t bm = (id >= 4 && id <= 7) ? (uint32_t)block_max_bytes(id) : (4u << 20);
+    return compress_ws_bytes(srcSize, bm);
+}
+
+static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
+                                       uint64_t* d_frameSize, const Lz4MtStreamDescriptor* sd, void* d_ws,
+                                       uint64_t wsSize, hipStream_t st, void** ownedWs) {
+    if (!sd || !d_frame || (!d_src && srcSize)) return LZ4MT_RESULT_BAD_ARG;
+    const Lz4MtResult v = validate_sd(sd);
+    if (v != LZ4MT_RESULT_OK) return v;
+    if (!sd->flg.blockIndependence) return LZ4MT_RESULT_BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET;
+    if (!have_device()) return LZ4MT_RESULT_ERROR;
+    if (frameCap < lz4mtHipFrameBound(srcSize, sd)) return LZ4MT_RESULT_BAD_ARG;
+    const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
+    const uint64_t need = compress_ws_bytes(srcSize, bm);
+    uint8_t* ws = static_cast<uint8_t*>(d_ws);
+    if (!ws || wsSize < need) {
+        if (hipMalloc(reinterpret_cast<void**>(&ws), need) != hipSuccess) return LZ4MT_RESULT_ERROR;
+        *ownedWs = ws;
+    }
+    uint8_t hdr[kMaxHeader];
+    const int hdrLen = build_header(sd, hdr);
+    uint64_t* recOff = nullptr;
+    const Lz4MtResult r = device_compress_body(static_cast<const uint8_t*>(d_src), srcSize, bm, sd->flg.blockChecksum,
+                                               ws, static_cast<uint8_t*>(d_frame), (uint32_t)hdrLen, st, &recOff);
+    if (r != LZ4MT_RESULT_OK) return r;
+    CompressWs w = carve_compress(ws, (srcSize + bm - 1) / bm, bm);
+    if (sd->flg.streamChecksum)
+        HIPCHK(launch_xxh32_stream(static_cast<const uint8_t*>(d_src), srcSize, w.ssum, st));
+    g_timing.mark(3, st);
+    HIPCHK(launch_frame_finalize(static_cast<uint8_t*>(d_frame), hdr, (uint32_t)hdrLen, recOff,
+                                 (uint32_t)((srcSize + bm - 1) / bm), sd->flg.streamChecksum ? w.ssum : nullptr,
+                                 d_frameSize ? d_frameSize : w.fsize, st));
+    g_timing.mark(4, st);
+    return LZ4MT_RESULT_OK;
+}
+
+extern "C" Lz4MtResult lz4mtHipCompressFrameAsync(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
+                                                  uint64_t* d_frameSize, const Lz4MtStreamDescriptor* sd,
+                                                  void* d_workspace, uint64_t workspaceSize, void* stream) {
+    void* owned = nullptr;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    const Lz4MtResult r =
+        compress_frame_impl(d_src, srcSize, d_frame, frameCap, d_frameSize, sd, d_workspace, workspaceSize, st, &owned);
+    if (owned) {  // library-owned scratch: must outlive the kernels
+        hipStreamSynchronize(st);
+        hipFree(owned);
+    }
+    return r;
+}
+
+extern "C" Lz4MtResult lz4mtHipCompressFrame(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
+                                             uint64_t* frameSize, const Lz4MtStreamDescriptor* sd, void* d_workspace,
+                                             uint64_t workspaceSize, void* stream) {
+    void* owned = nullptr;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    uint64_t* dfs = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&dfs), 16) != hipSuccess) return LZ4MT_RESULT_ERROR;
+    Lz4MtResult r = compress_frame_impl(d_src, srcSize, d_frame, frameCap, dfs, sd, d_workspace, workspaceSize, st, &owned);
+    if (r == LZ4MT_RESULT_OK) {
+        uint64_t fs = 0;
+        if (hipMemcpyAsync(&fs, dfs, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            r = LZ4MT_RESULT_ERROR;
+        if (frameSize) *frameSize = fs;
+    } else {
+        hipStreamSynchronize(st);
+    }
+    if (owned) hipFree(owned);
+    hipFree(dfs);
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// decompress
+// ---------------------------------------------------------------------------
+namespace {
+
+struct DecodeBuffers {
+    BlockRec* recs = nullptr;
+    uint32_t* digest = nullptr;
+    int32_t* dsize = nullptr;
+    int32_t* status = nullptr;
+    WalkInfo* info = nullptr;
+    uint32_t* ssum = nullptr;
+    uint64_t cap = 0;
+    ~DecodeBuffers() { release(); }
+    void release() {
+        hipFree(recs); hipFree(digest); hipFree(dsize); hipFree(status); hipFree(info); hipFree(ssum);
+        recs = nullptr; digest = nullptr; dsize = nullptr; status = nullptr; info = nullptr; ssum = nullptr; cap = 0;
+    }
+    bool ensure(uint64_t nb) {
+        if (info && nb <= cap) return true;
+        release();
+        cap = std::max<uint64_t>(nb, 64);
+        return hipMalloc(reinterpret_cast<void**>(&recs), cap * sizeof(BlockRec)) == hipSuccess &&
+               hipMalloc(reinterpret_cast<void**>(&digest), cap * 4) == hipSuccess &&
+               hipMalloc(reinterpret_cast<void**>(&dsize), cap * 4) == hipSuccess &&
+               hipMalloc(reinterpret_cast<void**>(&status), cap * 4) == hipSuccess &&
+               hipMalloc(reinterpret_cast<void**>(&info), sizeof(WalkInfo)) == hipSuccess &&
+               hipMalloc(reinterpret_cast<void**>(&ssum), 16) == hipSuccess;
+    }
+};
+
+// Walks one frame body; retries with a larger block table if needed.
+Lz4MtResult walk_frame(const uint8_t* frame, uint64_t frameSize, uint64_t bodyPos, uint32_t bm, int bck,
+                       DecodeBuffers& B, WalkInfo& wi, hipStream_t st) {
+    uint64_t guess = std::min<uint64_t>((frameSize - bodyPos) / 4 + 1, (frameSize - bodyPos) / 1024 + 4096);
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        if (!B.ensure(guess)) return LZ4MT_RESULT_ERROR;
+        HIPCHK(launch_frame_walk(frame, frameSize, bodyPos, bm, bck, (uint32_t)B.cap, B.recs, B.info, st));
+        HIPCHK(hipMemcpyAsync(&wi, B.info, sizeof(wi), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (!(wi.result == 1 && wi.nBlocks == B.cap)) return LZ4MT_RESULT_OK;
+        guess = (frameSize - bodyPos) / 4 + 1;
+    }
+    return LZ4MT_RESULT_OK;
+}
+
+}  // namespace
+
+extern "C" Lz4MtResult lz4mtHipFrameInfo(const void* d_frame, uint64_t frameSize, Lz4MtStreamDescriptor* sd,
+                                         uint64_t* decodedBound, uint64_t* nBlocks, void* stream) {
+    if (!d_frame || !sd) return LZ4MT_RESULT_BAD_ARG;
+    if (!have_device()) return LZ4MT_RESULT_ERROR;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint8_t* f = static_cast<const uint8_t*>(d_frame);
+    uint64_t pos = 0;
+    for (;;) {  // skip skippable frames
+        uint8_t h[kMaxHeader + 8] = {0};
+        const uint64_t avail = std::min<uint64_t>(sizeof(h), frameSize - pos);
+        HIPCHK(hipMemcpyAsync(h, f + pos, avail, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (avail < 4) return LZ4MT_RESULT_INVALID_HEADER;
+        const uint32_t magic = get32(h);
+        if (magic >= kSkippableMin && magic <= kSkippableMax) {
+            if (avail < 8) return LZ4MT_RESULT_INVALID_HEADER_SKIPPABLE_SIZE_UNREADABLE;
+            pos += 8 + (uint64_t)get32(h + 4);
+            if (pos >= frameSize) return LZ4MT_RESULT_INVALID_MAGIC_NUMBER;
+            continue;
+        }
+        if (magic != kMagic) return LZ4MT_RESULT_INVALID_MAGIC_NUMBER;
+        int hb = 0;
+        const Lz4MtResult r = parse_header(h + 4, avail - 4, sd, &hb);
+        if (r != LZ4MT_RESULT_OK) return r;
+        if (!sd->flg.blockIndependence) return LZ4MT_RESULT_BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET;
+        const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
+        DecodeBuffers B;
+        WalkInfo wi{};
+        const Lz4MtResult wr = walk_frame(f, frameSize, pos + 4 + hb, bm, sd->flg.blockChecksum, B, wi, st);
+        if (wr != LZ4MT_RESULT_OK) return wr;
+        if (decodedBound) *decodedBound = (uint64_t)wi.nBlocks * bm;
+        if (nBlocks) *nBlocks = wi.nBlocks;
+        return wi.result ? (Lz4MtResult)wi.result : LZ4MT_RESULT_OK;
+    }
+}
+
+extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t frameSize, void* d_out, uint64_t outCap,
+                                               uint64_t* outSize, Lz4MtStreamDescriptor* sd, void* stream) {
+    if (!d_frame || !sd || (!d_out && outCap)) return LZ4MT_RESULT_BAD_ARG;
+    if (!have_device()) return LZ4MT_RESULT_ERROR;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint8_t* f = static_cast<const uint8_t*>(d_frame);
+    uint8_t* out = static_cast<uint8_t*>(d_out);
+    uint64_t pos = 0, opos = 0;
+    bool seen = false;
+    Lz4MtResult result = LZ4MT_RESULT_OK;
+    DecodeBuffers B;
+    uint8_t* tmp = nullptr;   // staging when a frame's output is unaligned or needs compaction
+    uint64_t tmpCap = 0;
+    if (outSize) *outSize = 0;
+    while (pos < frameSize) {
+        uint8_t h[kMaxHeader + 8] = {0};
+        const uint64_t avail = std::min<uint64_t>(sizeof(h), frameSize - pos);
+        HIPCHK(hipMemcpyAsync(h, f + pos, avail, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (avail < 4) break;  // 1-3 trailing bytes: end of stream (reference: OK at EOF)
+        const uint32_t magic = get32(h);
+        if (magic != kMagic) {
+            if (magic >= kSkippableMin && magic <= kSkippableMax) {
+                if (avail < 8) { result = LZ4MT_RESULT_INVALID_HEADER_SKIPPABLE_SIZE_UNREADABLE; break; }
+                pos = std::min<uint64_t>(frameSize, pos + 8 + (uint64_t)get32(h + 4));
+                continue;
+            }
+            // non-magic data: error before any frame, end of stream after one
+            // (the reference spins forever here, src/lz4mt.cpp:971-979)
+            if (!seen) result = LZ4MT_RESULT_INVALID_MAGIC_NUMBER;
+            break;
+        }
+        seen = true;
+        int hb = 0;
+        result = parse_header(h + 4, avail - 4, sd, &hb);
+        if (result != LZ4MT_RESULT_OK) break;
+        if (!sd->flg.blockIndependence) { result = LZ4MT_RESULT_BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET; break; }
+        const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
+        const int bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
+        WalkInfo wi{};
+        g_timing.mark(0, st);
+        result = walk_frame(f, frameSize, pos + 4 + hb, bm, bck, B, wi, st);
+        if (result != LZ4MT_RESULT_OK) break;
+        const uint64_t nb = wi.nBlocks;
+        // decode target: in place when 16-B aligned, else a staging buffer
+        const bool aligned = ((reinterpret_cast<uintptr_t>(out) + opos) & 15) == 0;
+        const uint64_t room = outCap > opos ? outCap - opos : 0;
+        uint8_t* target = out + opos;
+        uint64_t targetCap = room;
+        if (!aligned) {
+            if (tmpCap < nb * bm) {
+                hipFree(tmp);
+                tmpCap = nb * bm;
+                if (hipMalloc(reinterpret_cast<void**>(&tmp), tmpCap + 64) != hipSuccess) { tmp = nullptr; result = LZ4MT_RESULT_ERROR; break; }
+            }
+            target = tmp;
+            targetCap = std::min<uint64_t>(room, nb * bm);
+        }
+        g_timing.mark(1, st);
+        HIPCHK(launch_decode(f, B.recs, (uint32_t)nb, bm, target, targetCap, B.dsize, st));
+        g_timing.mark(2, st);
+        if (bck) HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, st));
+        HIPCHK(launch_block_verify(B.recs, (uint32_t)nb, B.digest, B.dsize, bm, bck, B.status, st));
+        g_timing.mark(3, st);
+        std::vector<int32_t> ds(nb), stv(nb);
+        if (nb) {
+            HIPCHK(hipMemcpyAsync(ds.data(), B.dsize, nb * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(stv.data(), B.status, nb * 4, hipMemcpyDeviceToHost, st));
+        }
+        HIPCHK(hipStreamSynchronize(st));
+        // first failing block wins, then the walk's own error (block order)
+        uint64_t good = nb;
+        for (uint64_t i = 0; i < nb; ++i)
+            if (stv[i] != 0) { good = i; result = (Lz4MtResult)stv[i]; break; }
+        if (good == nb && wi.result != 0) result = (Lz4MtResult)wi.result;
+        // gather decoded bytes of blocks [0, good) contiguously at out + opos
+        uint64_t produced = 0;
+        bool contiguous = aligned;
+        for (uint64_t i = 0; i < good; ++i) {
+            if (i + 1 < good && (uint64_t)ds[i] != bm) contiguous = false;
+            produced += (uint64_t)ds[i];
+        }
+        if (produced > room) { result = LZ4MT_RESULT_ERROR; break; }
+        if (!contiguous) {
+            // compaction: copy slots through staging in block order
+            uint8_t* srcBase = target;
+            if (aligned) {  // slots live in the output itself: stage them first
+                if (tmpCap < good * (uint64_t)bm) {
+                    hipFree(tmp);
+                    tmpCap = good * (uint64_t)bm;
+                    if (hipMalloc(reinterpret_cast<void**>(&tmp), tmpCap + 64) != hipSuccess) { tmp = nullptr; result = LZ4MT_RESULT_ERROR; break; }
+                }
+                HIPCHK(hipMemcpyAsync(tmp, target, std::min<uint64_t>(good * (uint64_t)bm, targetCap), hipMemcpyDeviceToDevice, st));
+                srcBase = tmp;
+            }
+            uint64_t w = 0;
+            for (uint64_t i = 0; i < good; ++i) {
+                if (ds[i] > 0)
+                    HIPCHK(hipMemcpyAsync(out + opos + w, srcBase + i * bm, (size_t)ds[i], hipMemcpyDeviceToDevice, st));
+                w += (uint64_t)ds[i];
+            }
+        }
+        if (result != LZ4MT_RESULT_OK) { opos += produced; break; }
+        uint64_t next = wi.endPos;
+        if (sck) {
+            if (next + 4 > frameSize) { opos += produced; result = LZ4MT_RESULT_CANNOT_READ_STREAM_CHECKSUM; break; }
+            uint8_t want[4];
+            HIPCHK(hipMemcpyAsync(want, f + next, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(launch_xxh32_stream(out + opos, produced, B.ssum, st));
+            uint32_t got = 0;
+            HIPCHK(hipMemcpyAsync(&got, B.ssum, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            next += 4;
+            if (got != get32(want)) { opos += produced; result = LZ4MT_RESULT_STREAM_CHECKSUM_MISMATCH; break; }
+        }
+        g_timing.mark(4, st);
+        opos += produced;
+        pos = next;
+    }
+    hipStreamSynchronize(st);
+    hipFree(tmp);
+    if (outSize) *outSize = opos;
+    return result;
+}
+
+// ===========================================================================
+// 3. utilities
+// ===========================================================================
+extern "C" int lz4mtHipGenSynthetic(void* d_dst, uint64_t n, uint64_t seed, void* stream) {
+    if (!have_device()) return -1;
+    return launch_gen_synthetic(static_cast<uint8_t*>(d_dst), n, seed, static_cast<hipStream_t>(stream)) == hipSuccess
+               ? 0 : -1;
+}
+
+extern "C" uint32_t lz4mtHipXxh32(const void* d_src, uint64_t len, void* stream) {
+    if (!have_device()) return 0;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    uint32_t* d = nullptr;
+    uint32_t h = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&d), 16) != hipSuccess) return 0;
+    if (launch_xxh32_stream(static_cast<const uint8_t*>(d_src), len, d, st) == hipSuccess &&
+        hipMemcpyAsync(&h, d, 4, hipMemcpyDeviceToHost, st) == hipSuccess)
+        hipStreamSynchronize(st);
+    hipFree(d);
+    return h;
+}
+
+extern "C" int lz4mtHipDeviceCount(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+extern "C" void lz4mtHipSetTiming(int enable) {
+    g_timing.enabled = enable != 0;
+    g_timing.valid = false;
+}
+
+extern "C" int lz4mtHipGetTimings(float* ms4) {
+    if (!g_timing.valid || !ms4) return -1;
+    for (int i = 0; i < 5; ++i)
+        if (!g_timing.ev[i]) return -1;
+    if (hipEventSynchronize(g_timing.ev[4]) != hipSuccess) return -1;
+    float a = 0, b = 0, c = 0, d = 0;
+    hipEventElapsedTime(&a, g_timing.ev[0], g_timing.ev[1]);
+    hipEventElapsedTime(&b, g_timing.ev[1], g_timing.ev[2]);
+    hipEventElapsedTime(&c, g_timing.ev[2], g_timing.ev[3]);
+    hipEventElapsedTime(&d, g_timing.ev[0], g_timing.ev[4]);
+    ms4[0] = a; ms4[1] = b; ms4[2] = c; ms4[3] = d;
+    return 0;
+}

@@ -1,0 +1,628 @@
+// lz4mt_frame.cpp — the drop-in lz4mt.h API over callbacks.
+//
+// lz4mtCompress / lz4mtDecompress keep the reference's contract
+// (src/lz4mt.cpp:851-1011): header via makeHeader, blocks in order, EOS,
+// optional content checksum; first error wins; read/readEof/readSeek/
+// readSkippable only on the calling thread; write strictly in block order;
+// the codec callbacks may run concurrently.  Two schedulers sit behind it:
+//
+//   PARALLEL / SEQUENTIAL  — host pipeline calling ctx->compress /
+//       ctx->decompress per block (a bounded ring of nPool = workers + 1
+//       blocks, worker threads, one in-order writer thread that also owns the
+//       serial content checksum).  Null codec callbacks default to the GPU
+//       block operators of lz4mt_hip.h.
+//   DEVICE (extension bit) — batched MI355X engine: blocks are read into a
+//       pinned batch, copied to HBM, encoded/decoded by one kernel launch per
+//       batch (wave per block), and written back in order; the serial
+//       content checksum runs on the host while the GPU works.
+//
+// Deliberate fixes vs the reference (documented in DESIGN.md): non-magic
+// bytes after a frame end the stream with OK (the reference loops forever,
+// src/lz4mt.cpp:971-979); skippable frames are skipped by reading when
+// readSkippable is null (the CLI leaves it null and segfaults,
+// src/main.cpp:767-775); the futures vector race (src/lz4mt.cpp:408,448) has
+// no counterpart; lz4mtResultToString names every code.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/lz4mt.h"
+#include "../../include/lz4mt_hip.h"
+#include "lz4mt_device.h"
+#include "lz4mt_host.h"
+
+namespace lz4mt {
+Lz4MtResult device_compress_body(const uint8_t* src, uint64_t n, uint32_t bm, int blockChecksum, uint8_t* ws,
+                                 uint8_t* body, uint32_t hdrLen, hipStream_t st, uint64_t** d_recOffOut);
+uint64_t compress_ws_bytes(uint64_t n, uint32_t bm);
+}  // namespace lz4mt
+
+using namespace lz4mt;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Context wrapper: first-error-wins result (reference Ctx, src/lz4mt.cpp:163-271)
+// ---------------------------------------------------------------------------
+class Session {
+public:
+    explicit Session(Lz4MtContext* c) : c_(c) {}
+
+    Lz4MtResult set(Lz4MtResult r) {
+        std::lock_guard<std::mutex> g(mu_);
+        if (c_->result == LZ4MT_RESULT_OK || c_->result == LZ4MT_RESULT_ERROR) c_->result = r;
+        return c_->result;
+    }
+    Lz4MtResult result() {
+        std::lock_guard<std::mutex> g(mu_);
+        return c_->result;
+    }
+    bool error() { return result() != LZ4MT_RESULT_OK; }
+    Lz4MtResult quit(Lz4MtResult r) {
+        set(r);
+        quit_ = true;
+        return r;
+    }
+    bool quitting() const { return quit_.load(); }
+
+    int read(void* d, int n) {
+        if (!c_->read) return 0;
+        const int r = c_->read(c_, d, n);
+        if (r < n) eofHint_ = true;
+        return r < 0 ? 0 : r;
+    }
+    bool readEof() { return c_->readEof ? c_->readEof(c_) != 0 : eofHint_; }
+    // readU32: a short read sets ERROR (reference Ctx::readU32)
+    bool readU32(uint32_t* v) {
+        if (error()) return false;
+        uint8_t b[4];
+        if (read(b, 4) != 4) { set(LZ4MT_RESULT_ERROR); return false; }
+        *v = get32(b);
+        return true;
+    }
+    bool write(const void* p, int n) {  // reference Ctx::writeBin
+        if (error()) return false;
+        if (!c_->write || c_->write(c_, p, n) != n) { set(LZ4MT_RESULT_ERROR); return false; }
+        return true;
+    }
+    bool writeU32(uint32_t v) {
+        uint8_t b[4];
+        put32(b, v);
+        return write(b, 4);
+    }
+    bool skip(uint32_t magic, uint32_t size) {
+        if (c_->readSkippable) return c_->readSkippable(c_, magic, size) >= 0;
+        std::vector<uint8_t> sink(std::min<uint32_t>(size, 1u << 20));
+        uint32_t left = size;
+        while (left) {
+            const int take = (int)std::min<uint32_t>(left, (uint32_t)sink.size());
+            const int got = read(sink.data(), take);
+            if (got <= 0) break;  // like fseek past EOF: not an error
+            left -= (uint32_t)got;
+        }
+        return true;
+    }
+    int compress(const char* s, char* d, int n, int cap) {
+        Lz4MtCompress fn = c_->compress ? c_->compress : lz4mtHipCompressBlock;
+        return fn(s, d, n, cap, c_->compressionLevel);
+    }
+    int decompress(const char* s, char* d, int n, int cap) {
+        Lz4MtDecompress fn = c_->decompress ? c_->decompress : lz4mtHipDecompressBlock;
+        return fn(s, d, n, cap);
+    }
+    Lz4MtMode mode() const { return c_->mode; }
+    int level() const { return c_->compressionLevel; }
+    void clearEofHint() { eofHint_ = false; }
+
+private:
+    Lz4MtContext* c_;
+    std::mutex mu_;
+    std::atomic<bool> quit_{false};
+    bool eofHint_ = false;
+};
+
+unsigned worker_count(const Session& s) {
+    if (s.mode() & LZ4MT_MODE_SEQUENTIAL) return 0;
+    const unsigned hw = std::thread::hardware_concurrency();
+    return hw ? hw : 1;
+}
+
+// ---------------------------------------------------------------------------
+// A small ordered pipeline: jobs are produced in order by the caller thread,
+// processed by W workers, and consumed strictly in order by one writer.
+// With W == 0 everything runs inline on the caller thread (SEQUENTIAL).
+// ---------------------------------------------------------------------------
+struct Job {
+    std::vector<char> in, out;
+    int n = 0;          // input bytes
+    int res = 0;        // codec result
+    bool raw = false;
+    uint32_t ck = 0;    // block checksum (compress: computed; decompress: expected)
+    bool ckbad = false; // decompress: stored checksum mismatched
+    bool skip = false;  // an earlier error: nothing to do
+    bool ready = false;
+};
+
+class Pipeline {
+public:
+    Pipeline(unsigned workers, unsigned slots, std::function<void(Job&)> work, std::function<void(Job&)> emit)
+        : work_(std::move(work)), emit_(std::move(emit)), jobs_(slots) {
+        for (unsigned i = 0; i < workers; ++i) threads_.emplace_back([this] { worker(); });
+        if (workers) writer_ = std::thread([this] { writer(); });
+        inline_ = workers == 0;
+    }
+    ~Pipeline() { finish(); }
+
+    // Returns the next free job slot (blocks while the ring is full).
+    Job& acquire() {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return produced_ - written_ < jobs_.size(); });
+        Job& j = jobs_[produced_ % jobs_.size()];
+        j.ready = false;
+        return j;
+    }
+    void submit() {
+        if (inline_) {
+            Job& j = jobs_[produced_ % jobs_.size()];
+            ++produced_;
+            work_(j);
+            emit_(j);
+            ++written_;
+            return;
+        }
+        std::lock_guard<std::mutex> g(mu_);
+        queue_.push_back(produced_++);
+        cv_.notify_all();
+    }
+    // Waits until every submitted job has been written.
+    void drain() {
+        if (inline_) return;
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return written_ == produced_; });
+    }
+    void finish() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+            cv_.notify_all();
+        }
+        for (auto& t : threads_) t.join();
+        threads_.clear();
+        if (writer_.joinable()) writer_.join();
+    }
+
+private:
+    void worker() {
+        for (;;) {
+            uint64_t id;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return stop_ || !queue_.empty(); });
+                if (queue_.empty()) return;
+                id = queue_.front();
+                queue_.pop_front();
+            }
+            Job& j = jobs_[id % jobs_.size()];
+            work_(j);
+            std::lock_guard<std::mutex> g(mu_);
+            j.ready = true;
+            cv_.notify_all();
+        }
+    }
+    void writer() {
+        for (;;) {
+            Job* j;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return (written_ < produced_ && jobs_[written_ % jobs_.size()].ready) ||
+                                         (stop_ && written_ == produced_); });
+                if (written_ == produced_) return;
+                j = &jobs_[written_ % jobs_.size()];
+            }
+            emit_(*j);
+            std::lock_guard<std::mutex> g(mu_);
+            ++written_;
+            cv_.notify_all();
+        }
+    }
+
+    std::function<void(Job&)> work_, emit_;
+    std::vector<Job> jobs_;
+    std::vector<std::thread> threads_;
+    std::thread writer_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<uint64_t> queue_;
+    uint64_t produced_ = 0, written_ = 0;
+    bool stop_ = false, inline_ = false;
+};
+
+// ---------------------------------------------------------------------------
+// compress: host scheduler (reference compress(), src/lz4mt.cpp:372-457)
+// ---------------------------------------------------------------------------
+void compress_host(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
+    const int bm = block_max_bytes(sd->bd.blockMaximumSize);
+    const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
+    const unsigned W = worker_count(s);
+    auto work = [&](Job& j) {
+        j.skip = s.error() || s.quitting();
+        if (j.skip) return;
+        j.out.resize((size_t)bm + 64);
+        j.res = s.compress(j.in.data(), j.out.data(), j.n, j.n);  // cap = srcSize (src/lz4mt.cpp:391)
+        j.raw = j.res <= 0;
+        if (bck) j.ck = j.raw ? HostXxh32::oneshot(j.in.data(), (size_t)j.n) : HostXxh32::oneshot(j.out.data(), (size_t)j.res);
+    };
+    auto emit = [&](Job& j) {
+        if (j.skip || s.error() || s.quitting()) return;
+        if (sck) xs.update(j.in.data(), (size_t)j.n);
+        if (j.raw) {
+            s.writeU32((uint32_t)j.n | kRawBit);
+            s.write(j.in.data(), j.n);
+        } else {
+            s.writeU32((uint32_t)j.res);
+            s.write(j.out.data(), j.res);
+        }
+        if (bck) s.writeU32(j.ck);
+    };
+    Pipeline pipe(W, W + 1, work, emit);
+    for (;;) {
+        if (s.error() || s.quitting()) break;
+        Job& j = pipe.acquire();
+        j.in.resize((size_t)bm);
+        j.n = s.read(j.in.data(), bm);
+        if (j.n <= 0) break;
+        pipe.submit();
+    }
+    pipe.drain();
+}
+
+// ---------------------------------------------------------------------------
+// compress: DEVICE batch engine
+// ---------------------------------------------------------------------------
+struct DeviceBuffers {
+    hipStream_t st = nullptr;
+    uint8_t *hIn = nullptr, *hOut = nullptr, *dIn = nullptr, *dOut = nullptr, *dWs = nullptr;
+    uint64_t inCap = 0, outCap = 0, wsCap = 0;
+    ~DeviceBuffers() {
+        if (st) hipStreamSynchronize(st);
+        if (hIn) hipHostFree(hIn);
+        if (hOut) hipHostFree(hOut);
+        if (dIn) hipFree(dIn);
+        if (dOut) hipFree(dOut);
+        if (dWs) hipFree(dWs);
+        if (st) hipStreamDestroy(st);
+    }
+    bool init(uint64_t in, uint64_t out, uint64_t ws) {
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
+        inCap = in; outCap = out; wsCap = ws;
+        return hipHostMalloc(reinterpret_cast<void**>(&hIn), in + 64, 0) == hipSuccess &&
+               hipHostMalloc(reinterpret_cast<void**>(&hOut), out + 64, 0) == hipSuccess &&
+               hipMalloc(reinterpret_cast<void**>(&dIn), in + 64) == hipSuccess &&
+               hipMalloc(reinterpret_cast<void**>(&dOut), out + 64) == hipSuccess &&
+               (ws == 0 || hipMalloc(reinterpret_cast<void**>(&dWs), ws + 64) == hipSuccess);
+    }
+};
+
+constexpr uint64_t kBatchBytes = 256ull << 20;
+
+void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
+    if (s.level() >= 3) { s.quit(LZ4MT_RESULT_BAD_ARG); return; }   // no GPU LZ4-HC
+    if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return; }
+    const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
+    const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
+    const uint64_t K = std::max<uint64_t>(1, kBatchBytes / bm);
+    const uint64_t inCap = K * bm;
+    const uint64_t bodyCap = inCap + K * 8 + 64;
+    DeviceBuffers B;
+    if (!B.init(inCap, bodyCap, compress_ws_bytes(inCap, bm))) { s.quit(LZ4MT_RESULT_ERROR); return; }
+    bool eof = false;
+    while (!eof && !s.error()) {
+        uint64_t total = 0;
+        for (uint64_t j = 0; j < K; ++j) {   // one read() per block, as the reference does
+            const int n = s.read(B.hIn + total, (int)bm);
+            if (n <= 0) { eof = true; break; }
+            total += (uint64_t)n;
+            if ((uint32_t)n < bm) break;     // short block ends the batch (block boundaries kept)
+        }
+        if (total == 0) break;
+        uint64_t* dRecOff = nullptr;
+        if (hipMemcpyAsync(B.dIn, B.hIn, total, hipMemcpyHostToDevice, B.st) != hipSuccess ||
+            device_compress_body(B.dIn, total, bm, bck, B.dWs, B.dOut, 0, B.st, &dRecOff) != LZ4MT_RESULT_OK) {
+            s.quit(LZ4MT_RESULT_ERROR);
+            return;
+        }
+        const uint64_t nb = (total + bm - 1) / bm;
+        uint64_t bodySize = 0;
+        hipMemcpyAsync(&bodySize, dRecOff + nb, 8, hipMemcpyDeviceToHost, B.st);
+        if (sck) xs.update(B.hIn, total);   // serial content checksum overlaps the kernels
+        if (hipStreamSynchronize(B.st) != hipSuccess) { s.quit(LZ4MT_RESULT_ERROR); return; }
+        if (hipMemcpyAsync(B.hOut, B.dOut, bodySize, hipMemcpyDeviceToHost, B.st) != hipSuccess ||
+            hipStreamSynchronize(B.st) != hipSuccess) {
+            s.quit(LZ4MT_RESULT_ERROR);
+            return;
+        }
+        for (uint64_t o = 0; o < bodySize;) {   // write() takes int sizes
+            const int chunk = (int)std::min<uint64_t>(bodySize - o, 1u << 30);
+            if (!s.write(B.hOut + o, chunk)) return;
+            o += (uint64_t)chunk;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// decompress: host scheduler (reference decompress(), src/lz4mt.cpp:593-734)
+// Returns true when the EOS mark was reached.
+// ---------------------------------------------------------------------------
+bool decompress_host(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
+    const int bm = block_max_bytes(sd->bd.blockMaximumSize);
+    const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
+    const unsigned W = worker_count(s);
+    auto work = [&](Job& j) {
+        j.skip = s.error() || s.quitting();
+        if (j.skip) return;
+        j.ckbad = bck && HostXxh32::oneshot(j.in.data(), (size_t)j.n) != j.ck;
+        if (j.raw) { j.res = j.n; return; }
+        j.out.resize((size_t)bm + 64);
+        j.res = s.decompress(j.in.data(), j.out.data(), j.n, bm);   // cap = blockMax (src/lz4mt.cpp:645)
+    };
+    auto emit = [&](Job& j) {   // reference worker tail, src/lz4mt.cpp:619-681
+        if (j.skip || s.error() || s.quitting()) return;
+        if (!j.raw && j.res < 0) { s.quit(LZ4MT_RESULT_DECOMPRESS_FAIL); return; }
+        const char* p = j.raw ? j.in.data() : j.out.data();
+        if (sck) xs.update(p, (size_t)j.res);
+        if (!s.write(p, j.res)) {
+            s.quit(j.raw ? LZ4MT_RESULT_CANNOT_WRITE_DATA_BLOCK : LZ4MT_RESULT_CANNOT_WRITE_DECODED_BLOCK);
+            return;
+        }
+        if (j.ckbad) s.quit(LZ4MT_RESULT_BLOCK_CHECKSUM_MISMATCH);
+    };
+    Pipeline pipe(W, W + 1, work, emit);
+    bool eos = false;
+    while (!eos && !s.quitting() && !s.error() && !s.readEof()) {
+        uint32_t bits = 0;
+        if (!s.readU32(&bits)) { s.quit(LZ4MT_RESULT_CANNOT_READ_BLOCK_SIZE); break; }
+        if (bits == 0) { eos = true; break; }
+        const int n = (int)(bits & ~kRawBit);
+        if (n > bm) { s.quit(LZ4MT_RESULT_INVALID_BLOCK_SIZE); break; }
+        Job& j = pipe.acquire();
+        j.in.resize((size_t)n + 64);
+        if (s.read(j.in.data(), n) != n || s.error()) { s.quit(LZ4MT_RESULT_CANNOT_READ_BLOCK_DATA); break; }
+        j.n = n;
+        j.raw = (bits & kRawBit) != 0;
+        j.ck = 0;
+        if (bck && !s.readU32(&j.ck)) { s.quit(LZ4MT_RESULT_CANNOT_READ_BLOCK_CHECKSUM); break; }
+        pipe.submit();
+    }
+    pipe.drain();
+    return eos;
+}
+
+// ---------------------------------------------------------------------------
+// decompress: DEVICE batch engine
+// ---------------------------------------------------------------------------
+bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
+    if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return false; }
+    const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
+    const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
+    const uint64_t K = std::max<uint64_t>(1, kBatchBytes / bm);
+    DeviceBuffers B;
+    if (!B.init(K * bm, K * bm, 0)) { s.quit(LZ4MT_RESULT_ERROR); return false; }
+    BlockRec* dRecs = nullptr;
+    int32_t *dDs = nullptr, *dSt = nullptr;
+    uint32_t* dDig = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&dRecs), K * sizeof(BlockRec)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&dDs), K * 4) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&dSt), K * 4) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&dDig), K * 4) != hipSuccess) {
+        s.quit(LZ4MT_RESULT_ERROR);
+        return false;
+    }
+    std::vector<BlockRec> recs(K);
+    std::vector<int32_t> ds(K), stv(K);
+    bool eos = false;
+    Lz4MtResult pending = LZ4MT_RESULT_OK;   // a read error found while filling the batch
+    while (!eos && pending == LZ4MT_RESULT_OK && !s.error() && !s.readEof()) {
+        uint64_t used = 0, nb = 0;
+        while (nb < K) {
+            uint32_t bits = 0;
+            if (s.readEof()) break;
+            if (!s.readU32(&bits)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_SIZE; break; }
+            if (bits == 0) { eos = true; break; }
+            const uint32_t n = bits & ~kRawBit;
+            if (n > bm) { pending = LZ4MT_RESULT_INVALID_BLOCK_SIZE; break; }
+            if (s.read(B.hIn + used, (int)n) != (int)n) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_DATA; break; }
+            uint32_t ck = 0;
+            if (bck && !s.readU32(&ck)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_CHECKSUM; break; }
+            recs[nb++] = BlockRec{used, bits, ck};
+            used = (used + n + 15) & ~15ull;
+        }
+        if (nb) {
+            if (hipMemcpyAsync(B.dIn, B.hIn, used, hipMemcpyHostToDevice, B.st) != hipSuccess ||
+                hipMemcpyAsync(dRecs, recs.data(), nb * sizeof(BlockRec), hipMemcpyHostToDevice, B.st) != hipSuccess ||
+                launch_decode(B.dIn, dRecs, (uint32_t)nb, bm, B.dOut, nb * bm, dDs, B.st) != hipSuccess ||
+                (bck && launch_xxh32_frame_blocks(B.dIn, dRecs, (uint32_t)nb, dDig, B.st) != hipSuccess) ||
+                launch_block_verify(dRecs, (uint32_t)nb, dDig, dDs, bm, bck, dSt, B.st) != hipSuccess ||
+                hipMemcpyAsync(ds.data(), dDs, nb * 4, hipMemcpyDeviceToHost, B.st) != hipSuccess ||
+                hipMemcpyAsync(stv.data(), dSt, nb * 4, hipMemcpyDeviceToHost, B.st) != hipSuccess ||
+                hipMemcpyAsync(B.hOut, B.dOut, nb * bm, hipMemcpyDeviceToHost, B.st) != hipSuccess ||
+                hipStreamSynchronize(B.st) != hipSuccess) {
+                s.quit(LZ4MT_RESULT_ERROR);
+                break;
+            }
+            // write in block order; the first failing block stops the frame
+            bool stop = false;
+            for (uint64_t i = 0; i < nb && !stop; ++i) {
+                const bool raw = (recs[i].bits & kRawBit) != 0;
+                if (stv[i] == 18 || stv[i] == 1) {
+                    // reference precedence: decode failure before writing
+                    s.quit(stv[i] == 18 ? LZ4MT_RESULT_DECOMPRESS_FAIL : LZ4MT_RESULT_ERROR);
+                    stop = true;
+                    break;
+                }
+                const uint8_t* p = B.hOut + i * bm;
+                const int n = ds[i];
+                if (sck) xs.update(p, (size_t)n);
+                if (!s.write(p, n)) {
+                    s.quit(raw ? LZ4MT_RESULT_CANNOT_WRITE_DATA_BLOCK : LZ4MT_RESULT_CANNOT_WRITE_DECODED_BLOCK);
+                    stop = true;
+                    break;
+                }
+                if (stv[i] == 16) { s.quit(LZ4MT_RESULT_BLOCK_CHECKSUM_MISMATCH); stop = true; }
+            }
+            if (stop) break;
+        }
+        if (pending != LZ4MT_RESULT_OK) { s.quit(pending); break; }
+    }
+    hipFree(dRecs); hipFree(dDs); hipFree(dSt); hipFree(dDig);
+    return eos;
+}
+
+}  // namespace
+
+// ===========================================================================
+// public API
+// ===========================================================================
+extern "C" Lz4MtContext lz4mtInitContext(void) {
+    Lz4MtContext c;
+    memset(&c, 0, sizeof(c));
+    c.result = LZ4MT_RESULT_OK;
+    c.mode = LZ4MT_MODE_PARALLEL;
+    c.compressionLevel = 0;
+    return c;
+}
+
+extern "C" Lz4MtStreamDescriptor lz4mtInitStreamDescriptor(void) {
+    Lz4MtStreamDescriptor d;
+    memset(&d, 0, sizeof(d));
+    d.flg.streamChecksum = 1;
+    d.flg.blockIndependence = 1;
+    d.flg.versionNumber = 1;
+    d.bd.blockMaximumSize = 7;
+    return d;
+}
+
+extern "C" Lz4MtResult lz4mtCompress(Lz4MtContext* ctx, const Lz4MtStreamDescriptor* sd) {
+    if (!ctx || !sd) return LZ4MT_RESULT_BAD_ARG;
+    Session s(ctx);
+    // header (makeHeader, src/lz4mt.cpp:335-369)
+    const Lz4MtResult v = validate_sd(sd);
+    if (v != LZ4MT_RESULT_OK) return s.quit(v);
+    uint8_t hdr[kMaxHeader];
+    const int hl = build_header(sd, hdr);
+    if (!ctx->write || ctx->write(ctx, hdr, hl) != hl) return s.quit(LZ4MT_RESULT_CANNOT_WRITE_HEADER);
+    if (!sd->flg.blockIndependence) return s.quit(LZ4MT_RESULT_BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET);
+    HostXxh32 xs(0);
+    if (ctx->mode & LZ4MT_MODE_DEVICE) compress_device(s, sd, xs);
+    else compress_host(s, sd, xs);
+    if (s.result() != LZ4MT_RESULT_OK) return s.result();
+    if (!s.writeU32(0)) return s.quit(LZ4MT_RESULT_CANNOT_WRITE_EOS);
+    if (sd->flg.streamChecksum && !s.writeU32(xs.digest())) return s.quit(LZ4MT_RESULT_CANNOT_WRITE_STREAM_CHECKSUM);
+    return LZ4MT_RESULT_OK;
+}
+
+extern "C" Lz4MtResult lz4mtDecompress(Lz4MtContext* ctx, Lz4MtStreamDescriptor* sd) {
+    if (!ctx || !sd) return LZ4MT_RESULT_BAD_ARG;
+    Session s(ctx);
+    bool seen = false;
+    s.set(LZ4MT_RESULT_OK);
+    while (!s.quitting() && !s.error() && !s.readEof()) {
+        uint32_t magic = 0;
+        if (!s.readU32(&magic)) {
+            // end of input between frames is the normal end (src/lz4mt.cpp:951-957)
+            s.set(s.readEof() ? LZ4MT_RESULT_OK : LZ4MT_RESULT_INVALID_HEADER);
+            break;
+        }
+        if (magic != kMagic) {
+            if (magic >= kSkippableMin && magic <= kSkippableMax) {
+                uint32_t size = 0;
+                if (!s.readU32(&size)) { s.set(LZ4MT_RESULT_INVALID_HEADER_SKIPPABLE_SIZE_UNREADABLE); break; }
+                if (!s.skip(magic, size) || s.error()) { s.set(LZ4MT_RESULT_INVALID_HEADER_CANNOT_SKIP_SKIPPABLE_AREA); break; }
+                s.clearEofHint();
+                continue;
+            }
+            if (!seen) s.set(LZ4MT_RESULT_INVALID_MAGIC_NUMBER);
+            break;   // trailing non-frame data ends the stream
+        }
+        seen = true;
+        // readHeader (src/lz4mt.cpp:541-590)
+        uint8_t h[kMaxHeader];
+        if (s.read(h, 2) != 2) { s.quit(LZ4MT_RESULT_INVALID_HEADER); break; }
+        Lz4MtStreamDescriptor tmp = *sd;
+        parse_flg(h[0], &tmp.flg);
+        parse_bd(h[1], &tmp.bd);
+        const Lz4MtResult vr = validate_sd(&tmp);
+        if (vr != LZ4MT_RESULT_OK) { *sd = tmp; s.quit(vr); break; }
+        const int nex = (tmp.flg.streamSize ? 8 : 0) + (tmp.flg.presetDictionary ? 4 : 0) + 1;
+        if (s.read(h + 2, nex) != nex) { *sd = tmp; s.quit(LZ4MT_RESULT_INVALID_HEADER); break; }
+        int hb = 0;
+        const Lz4MtResult hr = parse_header(h, (size_t)(2 + nex), &tmp, &hb);
+        *sd = tmp;
+        if (hr != LZ4MT_RESULT_OK) { s.quit(hr); break; }
+        if (!sd->flg.blockIndependence) { s.quit(LZ4MT_RESULT_BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET); break; }
+        HostXxh32 xs(0);
+        const bool eos = (ctx->mode & LZ4MT_MODE_DEVICE) ? decompress_device(s, sd, xs) : decompress_host(s, sd, xs);
+        if (s.error() || s.quitting()) break;
+        if (!eos) { s.quit(LZ4MT_RESULT_CANNOT_READ_BLOCK_SIZE); break; }
+        if (sd->flg.streamChecksum) {
+            uint32_t want = 0;
+            if (!s.readU32(&want)) { s.set(LZ4MT_RESULT_CANNOT_READ_STREAM_CHECKSUM); break; }
+            if (xs.digest() != want) { s.set(LZ4MT_RESULT_STREAM_CHECKSUM_MISMATCH); break; }
+        }
+    }
+    return s.result();
+}
+
+extern "C" const char* lz4mtResultToString(Lz4MtResult r) {
+    // Same strings as reference src/lz4mt_result.cpp:4-89; codes 16, 24 and
+    // 25 are named too (the reference prints "Unknown code" for them).
+    static const char* const names[] = {
+        "OK", "ERROR", "INVALID_MAGIC_NUMBER", "INVALID_HEADER", "PRESET_DICTIONARY_IS_NOT_SUPPORTED_YET",
+        "BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET", "INVALID_VERSION", "INVALID_HEADER_CHECKSUM",
+        "INVALID_BLOCK_MAXIMUM_SIZE", "CANNOT_WRITE_HEADER", "CANNOT_WRITE_EOS", "CANNOT_WRITE_STREAM_CHECKSUM",
+        "CANNOT_READ_BLOCK_SIZE", "CANNOT_READ_BLOCK_DATA", "CANNOT_READ_BLOCK_CHECKSUM",
+        "CANNOT_READ_STREAM_CHECKSUM", "BLOCK_CHECKSUM_MISMATCH", "STREAM_CHECKSUM_MISMATCH", "DECOMPRESS_FAIL",
+        "BAD_ARG", "INVALID_BLOCK_SIZE", "INVALID_HEADER_RESERVED1", "INVALID_HEADER_RESERVED2",
+        "INVALID_HEADER_RESERVED3", "INVALID_HEADER_SKIPPABLE_SIZE_UNREADABLE",
+        "INVALID_HEADER_CANNOT_SKIP_SKIPPABLE_AREA", "CANNOT_WRITE_DATA_BLOCK", "CANNOT_WRITE_DECODED_BLOCK"};
+    const unsigned i = (unsigned)r;
+    return i < sizeof(names) / sizeof(names[0]) ? names[i] : "Unknown code";
+}
+
+extern "C" int lz4mtResultToLz4cExitCode(Lz4MtResult r) {
+    // lz4c exit codes per result (reference src/lz4mt_result.cpp:92-270)
+    switch (r) {
+        case LZ4MT_RESULT_OK: return 0;
+        case LZ4MT_RESULT_INVALID_MAGIC_NUMBER: return 44;
+        case LZ4MT_RESULT_INVALID_HEADER_SKIPPABLE_SIZE_UNREADABLE: return 42;
+        case LZ4MT_RESULT_INVALID_HEADER_CANNOT_SKIP_SKIPPABLE_AREA: return 43;
+        case LZ4MT_RESULT_CANNOT_WRITE_HEADER: return 32;
+        case LZ4MT_RESULT_CANNOT_WRITE_EOS:
+        case LZ4MT_RESULT_CANNOT_WRITE_STREAM_CHECKSUM: return 37;
+        case LZ4MT_RESULT_INVALID_HEADER: return 61;
+        case LZ4MT_RESULT_INVALID_VERSION: return 62;
+        case LZ4MT_RESULT_INVALID_HEADER_RESERVED1: return 65;
+        case LZ4MT_RESULT_PRESET_DICTIONARY_IS_NOT_SUPPORTED_YET: return 66;
+        case LZ4MT_RESULT_INVALID_HEADER_RESERVED2:
+        case LZ4MT_RESULT_INVALID_HEADER_RESERVED3: return 67;
+        case LZ4MT_RESULT_INVALID_BLOCK_MAXIMUM_SIZE: return 68;
+        case LZ4MT_RESULT_INVALID_HEADER_CHECKSUM: return 69;
+        case LZ4MT_RESULT_CANNOT_READ_BLOCK_SIZE: return 71;
+        case LZ4MT_RESULT_INVALID_BLOCK_SIZE: return 72;
+        case LZ4MT_RESULT_CANNOT_READ_BLOCK_DATA: return 73;
+        case LZ4MT_RESULT_CANNOT_READ_BLOCK_CHECKSUM:
+        case LZ4MT_RESULT_CANNOT_READ_STREAM_CHECKSUM: return 74;
+        case LZ4MT_RESULT_BLOCK_CHECKSUM_MISMATCH:
+        case LZ4MT_RESULT_STREAM_CHECKSUM_MISMATCH: return 75;
+        case LZ4MT_RESULT_CANNOT_WRITE_DATA_BLOCK: return 76;
+        case LZ4MT_RESULT_DECOMPRESS_FAIL: return 77;
+        case LZ4MT_RESULT_CANNOT_WRITE_DECODED_BLOCK: return 78;
+        default: return 1;
+    }
+}

@@ -1,0 +1,917 @@
+// lz4mt_kernels.hip — hand-written CDNA4 (gfx950) kernels for the lz4mt hot path.
+//
+//   k_encode        LZ4 1.9.3 greedy parse, one wavefront per frame block
+//                   (replaces ctx.compress = LZ4_compress_limitedOutput,
+//                   reference src/lz4mt.cpp:391, src/main.cpp:749-751)
+//   k_decode        LZ4_decompress_safe 1.9.3 state machine, one wavefront
+//                   per block (replaces ctx.decompress, src/lz4mt.cpp:645-646)
+//   k_xxh32_*       XXH32 seed 0 of stored blocks / whole streams
+//                   (replaces Lz4Mt::Xxh32, src/lz4mt_xxh32.cpp:14-58)
+//   k_frame_*       exclusive scan + scatter of the block records into one
+//                   contiguous frame (replaces the ordered write chain,
+//                   src/lz4mt.cpp:407-428), and the device-side frame walk
+//                   (src/lz4mt.cpp:685-727)
+//   k_gen_synthetic the pinned synthetic input
+//
+// Wave-level design: every block is an independent serial
+// parse, so a block is owned by ONE 64-lane wavefront; lanes work on the
+// data-parallel parts (64 speculative match probes per step, 64-lane
+// backward/forward match extension, lane-parallel literal/match copies),
+// while the parse state lives in wave-uniform registers.  The hash table
+// (16 KiB) and the decoder's history ring (16 KiB) sit in LDS.
+#include "lz4mt_device.h"
+
+namespace lz4mt {
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+#define WAVE_SYNC() __builtin_amdgcn_wave_barrier()
+
+__device__ __forceinline__ uint32_t laneid() { return __lane_id(); }
+
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+// mask of lanes <= L (L in [0,63])
+__device__ __forceinline__ uint64_t mask_le(uint32_t L) { return (L >= 63) ? ~0ull : ((2ull << L) - 1ull); }
+
+// Little-endian 32-bit read at an arbitrary byte address.  Only the aligned
+// dwords that hold requested bytes are touched, so it never reads a dword
+// that lies wholly past the last requested byte.
+__device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t lo = q[0];
+    const uint32_t hi = sh ? q[1] : 0u;
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+constexpr uint32_t kP1 = 2654435761u, kP2 = 2246822519u, kP3 = 3266489917u, kP4 = 668265263u, kP5 = 374761393u;
+
+// ---------------------------------------------------------------------------
+// Encoder
+// ---------------------------------------------------------------------------
+// Probe schedule of LZ4_compress_generic's search loop: probe k sits at
+// s + F(k) with step(k) = max(1, (63 + k) >> 6)  (searchMatchNb >> 6).
+__device__ __forceinline__ uint32_t probe_off(uint32_t k) {
+    if (k == 0) return 0;
+    const uint32_t q = (k - 1) >> 6, r = (k - 1) & 63;
+    return 1 + 32 * q * (q + 1) + r * (q + 1);
+}
+__device__ __forceinline__ uint32_t probe_step(uint32_t k) { return k == 0 ? 1u : ((63 + k) >> 6); }
+
+template <bool U16>
+__device__ __forceinline__ uint32_t lz4_hash(uint32_t w0, uint32_t w1) {
+    if (U16) return (w0 * 2654435761u) >> 19;                         // hash4, 13 bits
+    const uint64_t v = ((uint64_t)w1 << 32) | w0;                     // hash5, 12 bits
+    return (uint32_t)(((v << 24) * 889523592379ull) >> 52);
+}
+
+// One window of up to 64 probes.  Lane roles: [INSERT][TEST] SEARCH...
+//   INSERT: table insertion only (position 0 at block start, ip-2 after a match)
+//   TEST:   LZ4's "test next position" probe right after a match
+//   SEARCH: probe k0 + j of the skip-accelerated search loop
+struct Win {
+    uint32_t hasIns, hasTest, insPos, testPos, s, k0;
+    __device__ __forceinline__ uint32_t pos(uint32_t L) const {
+        const uint32_t ns = hasIns + hasTest;
+        if (L < hasIns) return insPos;
+        if (L < ns) return testPos;
+        return s + probe_off(k0 + (L - ns));
+    }
+};
+
+// Emits one sequence (or the final literal run when !hasMatch) with all
+// lanes, one output byte per lane per step.
+__device__ __forceinline__ void emit_seq(const uint8_t* __restrict__ s, uint8_t* __restrict__ d, uint32_t op,
+                                         uint32_t anchor, uint32_t lit, bool hasMatch, uint32_t off, uint32_t mc) {
+    const uint32_t L = laneid();
+    const uint32_t litExt = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
+    const uint32_t litRem = lit >= 15 ? (lit - 15) % 255 : 0;
+    const uint32_t mlExt = (hasMatch && mc >= 15) ? (mc - 15) / 255 + 1 : 0;
+    const uint32_t mlRem = mc >= 15 ? (mc - 15) % 255 : 0;
+    const uint32_t token = ((lit < 15 ? lit : 15) << 4) | (hasMatch ? (mc < 15 ? mc : 15) : 0);
+    const uint32_t litEnd = 1 + litExt + lit;
+    const uint32_t total = litEnd + (hasMatch ? 2 + mlExt : 0);
+    for (uint32_t base = 0; base < total; base += 64) {
+        const uint32_t x = base + L;
+        if (x < total) {
+            uint32_t v;
+            if (x == 0) v = token;
+            else if (x <= litExt) v = (x < litExt) ? 255u : litRem;
+            else if (x < litEnd) v = s[anchor + (x - 1 - litExt)];
+            else {
+                const uint32_t y = x - litEnd;
+                if (y == 0) v = off & 255;
+                else if (y == 1) v = off >> 8;
+                else v = (y - 2 + 1 < mlExt) ? 255u : mlRem;
+            }
+            d[op + x] = (uint8_t)v;
+        }
+    }
+}
+
+template <bool U16>
+__device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8_t* __restrict__ d, uint32_t cap,
+                                uint32_t* __restrict__ Traw, uint8_t* __restrict__ S) {
+    const uint32_t L = laneid();
+    const uint32_t bound = n + n / 255 + 16;
+    const bool limited = cap < bound;
+    if (n == 0) {
+        if (limited && cap == 0) return 0;
+        if (L == 0) d[0] = 0;
+        return 1;
+    }
+    uint16_t* T16 = reinterpret_cast<uint16_t*>(Traw);
+    // zero the 16 KiB table
+    {
+        uint4* T4 = reinterpret_cast<uint4*>(Traw);
+        for (uint32_t i = L; i < 1024; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
+    }
+    WAVE_SYNC();
+
+    const uint32_t mflimitP1 = n - kMfLimit + 1;
+    const uint32_t matchlimit = n - kLastLiterals;
+    uint32_t anchor = 0, op = 0;
+
+    if (n < (uint32_t)kMinLength) goto last_literals;
+    {
+        Win W{1, 0, 0, 0, 1, 0};  // T[h(0)] = 0; search from ip = 1
+        for (;;) {
+            // ---------------- one probe window ----------------
+            const uint32_t ns = W.hasIns + W.hasTest;
+            const bool isIns = L < W.hasIns;
+            const bool isTest = !isIns && L < ns;
+            const bool isSearch = L >= ns;
+            const uint32_t k = W.k0 + (L - ns);
+            const uint32_t p = W.pos(L);
+            const bool live = !isSearch || p <= mflimitP1;
+            const bool term = isSearch && live && (p + probe_step(k) > mflimitP1);
+            uint32_t w0 = 0, w1 = 0;
+            if (live) {
+                const uint32_t* q = reinterpret_cast<const uint32_t*>(s + (p & ~3u));
+                const uint32_t sh = p & 3;
+                const uint32_t d0 = q[0], d1 = q[1];
+                const uint32_t d2 = sh ? q[2] : 0u;
+                w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+                w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            }
+            const uint32_t h = live ? lz4_hash<U16>(w0, w1) : 0u;
+            // duplicate-hash detection inside the window (S is scratch; any
+            // aliasing only costs an extra group iteration)
+            S[h & 4095] = (uint8_t)L;
+            const uint32_t told = U16 ? (uint32_t)T16[h] : Traw[h];
+            WAVE_SYNC();
+            const uint32_t sv = S[h & 4095];
+            uint64_t pending = ballot(live && sv != L);
+            int pred = -1;
+            uint64_t gmask = 1ull << L;
+            while (pending) {  // one iteration per group of equal hashes
+                const int leader = __ffsll((long long)pending) - 1;
+                const uint32_t key = rdlane(h, leader);
+                const uint64_t m = ballot(live && h == key);
+                if ((m >> L) & 1) {
+                    gmask = m;
+                    const uint64_t below = m & ((1ull << L) - 1ull);
+                    pred = below ? 63 - __clzll((long long)below) : -1;
+                }
+                pending &= ~m;
+            }
+            const uint32_t cand = pred >= 0 ? W.pos((uint32_t)pred) : told;
+            bool ok = false;
+            if (live && !isIns && !term) {
+                const bool distok = U16 || (cand + kDistMax >= p);
+                if (distok) ok = (ld32u(s + cand) == w0);
+            }
+            const uint64_t sm = ballot(live && (term || ok));
+            const int w = sm ? __ffsll((long long)sm) - 1 : 64;
+            const bool wTerm = (w < 64) && ((ballot(term) >> w) & 1);
+            const int wlim = (w == 64) ? 63 : (wTerm ? w - 1 : w);
+            // table writes: last member of each hash group among lanes <= wlim
+            if (wlim >= 0 && live && (int)L <= wlim) {
+                const uint64_t later = gmask & ~mask_le(L) & mask_le((uint32_t)wlim);
+                if (!later) {
+                    if (U16) T16[h] = (uint16_t)p; else Traw[h] = p;
+                }
+            }
+            WAVE_SYNC();
+            if (w == 64) {  // no stop: continue the search
+                W.k0 += 64 - ns;
+                W.hasIns = 0; W.hasTest = 0;
+                continue;
+            }
+            if (wTerm) goto last_literals;
+
+            // ---------------- match found ----------------
+            uint32_t ip = rdlane(p, w);
+            uint32_t cd = rdlane(cand, w);
+            const bool wasTest = (ballot(isTest) >> w) & 1;
+            if (!wasTest) {  // catch up (LZ4: while ip>anchor && match>base && ip[-1]==match[-1])
+                const uint32_t maxb = min(ip - anchor, cd);
+                uint32_t back = 0;
+                while (back < maxb) {
+                    const uint32_t kk = back + L + 1;
+                    bool eq = false;
+                    if (kk <= maxb) eq = s[ip - kk] == s[cd - kk];
+                    const uint64_t fm = ballot(!eq);
+                    if (fm) { back += (uint32_t)(__ffsll((long long)fm) - 1); break; }
+                    back += 64;
+                }
+                ip -= back; cd -= back;
+            }
+            // forward extension (LZ4_count up to matchlimit)
+            uint32_t mc = 0;
+            {
+                const uint32_t lim = matchlimit - (ip + kMinMatch);
+                for (;;) {
+                    const uint32_t rel = mc + 4 * L;
+                    uint32_t eqb = 0;
+                    if (rel < lim) {
+                        const uint32_t x = ld32u(s + ip + kMinMatch + rel) ^ ld32u(s + cd + kMinMatch + rel);
+                        eqb = x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u;
+                        eqb = min(eqb, lim - rel);
+                    }
+                    const uint64_t nf = ballot(eqb < 4);
+                    if (nf) {
+                        const int f = __ffsll((long long)nf) - 1;
+                        mc += 4 * (uint32_t)f + rdlane(eqb, f);
+                        break;
+                    }
+                    mc += 256;
+                }
+            }
+            const uint32_t lit = ip - anchor;
+            if (limited) {
+                if (!wasTest && op + 1 + lit + 8 + lit / 255 > cap) return 0;
+                const uint32_t litExt = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
+                if (op + 1 + litExt + lit + 2 + 6 + (mc + 240) / 255 > cap) return 0;
+            }
+            emit_seq(s, d, op, anchor, lit, true, ip - cd, mc);
+            {
+                const uint32_t litExt = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
+                const uint32_t mlExt = mc >= 15 ? (mc - 15) / 255 + 1 : 0;
+                op += 1 + litExt + lit + 2 + mlExt;
+            }
+            ip += mc + kMinMatch;
+            anchor = ip;
+            if (ip >= mflimitP1) goto last_literals;
+            W = Win{1, 1, ip - 2, ip, ip + 1, 0};
+        }
+    }
+last_literals : {
+    const uint32_t run = n - anchor;
+    if (limited && op + run + 1 + (run + 240) / 255 > cap) return 0;
+    emit_seq(s, d, op, anchor, run, false, 0, 0);
+    const uint32_t ext = run >= 15 ? (run - 15) / 255 + 1 : 0;
+    op += 1 + ext + run;
+}
+    return (int32_t)op;
+}
+
+__global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, uint64_t srcSize, uint32_t blockSize,
+                                               uint8_t* __restrict__ slots, uint64_t slotStride,
+                                               uint32_t capOverride, int32_t* __restrict__ csize) {
+    __shared__ __attribute__((aligned(16))) uint32_t T[4096];  // 16 KiB: u32[4096] or u16[8192]
+    __shared__ __attribute__((aligned(16))) uint8_t S[4096];   // duplicate-hash scratch
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
+    const uint32_t cap = (capOverride == 0xFFFFFFFFu) ? n : capOverride;   // lz4mt: cap = n
+    const uint8_t* s = src + off;
+    uint8_t* d = slots + (uint64_t)b * slotStride;
+    int32_t r;
+    if (n < (uint32_t)kLimit64K) r = encode_block<true>(s, n, d, cap, T, S);
+    else r = encode_block<false>(s, n, d, cap, T, S);
+    if (laneid() == 0) csize[b] = r;
+}
+
+hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks, uint8_t* slots,
+                         uint64_t slotStride, uint32_t capOverride, int32_t* csize, hipStream_t st) {
+    if (nBlocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_encode, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, slotStride,
+                       capOverride, csize);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Decoder
+// ---------------------------------------------------------------------------
+constexpr int32_t kRing = 16384;   // LDS history ring (bytes)
+constexpr int32_t kInWin = 2048;   // LDS input window (bytes)
+constexpr int32_t kFlush = 1024;   // ring -> HBM flush granule (64 lanes x 16 B)
+
+struct Dec {
+    const uint8_t* src;   // compressed block
+    int64_t len;
+    uint8_t* dst;         // block's output slot (16-B aligned)
+    int64_t physcap;      // bytes of the slot that exist
+    uint8_t* ring;
+    uint8_t* win;
+    int64_t wlo;          // block-relative position of win[0]
+    int64_t flushed;      // [0, flushed) stored to dst
+    int64_t completed;    // [0, completed) known complete in memory
+
+    __device__ __forceinline__ void refill(int64_t i) {
+        const uintptr_t base = (reinterpret_cast<uintptr_t>(src) + (uintptr_t)i) & ~uintptr_t(15);
+        wlo = (int64_t)(base - reinterpret_cast<uintptr_t>(src));
+        const uintptr_t end = reinterpret_cast<uintptr_t>(src) + (uintptr_t)len;
+        const uint32_t L = laneid();
+        WAVE_SYNC();
+#pragma unroll
+        for (int h = 0; h < kInWin / 1024; ++h) {
+            const uintptr_t a = base + (uintptr_t)(h * 1024 + 16 * L);
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (a < end) v = *reinterpret_cast<const uint4*>(a);
+            *reinterpret_cast<uint4*>(win + h * 1024 + 16 * L) = v;
+        }
+        WAVE_SYNC();
+    }
+    __device__ __forceinline__ uint32_t in8(int64_t i) {
+        if (i < 0 || i >= len) return 0;
+        if (i < wlo || i >= wlo + kInWin) refill(i);
+        return win[i - wlo];
+    }
+    // flush every complete kFlush chunk below `upto`
+    __device__ __forceinline__ void flush_to(int64_t upto) {
+        const uint32_t L = laneid();
+        while (flushed + kFlush <= upto) {
+            const uint4 v = *reinterpret_cast<const uint4*>(ring + ((flushed & (kRing - 1)) + 16 * L));
+            const int64_t o = flushed + 16 * L;
+            if (o + 16 <= physcap) *reinterpret_cast<uint4*>(dst + o) = v;
+            flushed += kFlush;
+        }
+    }
+    __device__ __forceinline__ void flush_tail(int64_t op) {
+        flush_to(op);
+        const uint32_t L = laneid();
+        for (int64_t o = flushed + L; o < op; o += 64)
+            if (o < physcap) dst[o] = ring[o & (kRing - 1)];
+        flushed = op;
+    }
+    __device__ __forceinline__ void copy_lit(int64_t ip, int64_t op, int64_t n) {
+        const uint32_t L = laneid();
+        const bool inWin = ip >= wlo && ip + n <= wlo + kInWin;
+        for (int64_t c = 0; c < n; c += 64) {
+            flush_to(op + c);
+            const int64_t i = ip + c + L;
+            if (c + L < n) {
+                const uint32_t v = inWin ? win[i - wlo] : src[i];
+                ring[(op + c + L) & (kRing - 1)] = (uint8_t)v;
+            }
+            WAVE_SYNC();
+        }
+    }
+    __device__ __forceinline__ void copy_match(int64_t op, uint32_t offset, int64_t n) {
+        const uint32_t L = laneid();
+        // out[x] = out[op - offset + ((x - op) mod offset)]; offset 0 => zeros (LZ4 1.9.3)
+        const uint32_t magic = (offset > 0 && offset < 64) ? (65536u + offset - 1) / offset : 0u;
+        for (int64_t c = 0; c < n; c += 64) {
+            const int64_t o = op + c;
+            flush_to(o);
+            if ((int64_t)offset > kRing && completed < o - kRing) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                completed = flushed;
+            }
+            if (c + L < n) {
+                uint32_t v = 0;
+                if (offset) {
+                    int64_t sp;
+                    if (offset >= 64) sp = o + L - offset;
+                    else {
+                        const uint32_t kq = (L * magic) >> 16;   // L / offset for L < 64
+                        sp = o + L - (int64_t)(kq + 1) * offset;
+                    }
+                    v = (sp >= o - kRing) ? ring[sp & (kRing - 1)] : dst[sp];
+                }
+                ring[(o + L) & (kRing - 1)] = (uint8_t)v;
+            }
+            WAVE_SYNC();
+        }
+    }
+    // read_variable_length(); returns 0 ok, -1 initial error, -2 loop error
+    __device__ __forceinline__ int rvl(int64_t& ip, int64_t lencheck, bool loopCheck, bool initialCheck,
+                                       int64_t& length) {
+        length = 0;
+        if (initialCheck && ip >= lencheck) return -1;
+        uint32_t sv;
+        do {
+            sv = in8(ip);
+            ip++;
+            length += sv;
+            if (loopCheck && ip >= lencheck) return -2;
+        } while (sv == 255);
+        return 0;
+    }
+};
+
+// LZ4_decompress_safe (lz4 1.9.3, LZ4_FAST_DEC_LOOP=1): same accept/reject
+// decisions and return values as the oracle restatement (oracle/lz4_oracle.c).
+__device__ int32_t decode_block(Dec& D, int64_t cap) {
+    const int64_t iend = D.len, oend = cap;
+    const int64_t shortiend = iend - 16, shortoend = oend - 32;
+    int64_t ip = 0, op = 0, cpy = 0, match = 0, length = 0, ext = 0;
+    uint32_t token = 0, offset = 0;
+    int e;
+
+    if (cap == 0) return (D.len == 1 && D.in8(0) == 0) ? 0 : -1;
+    if (D.len == 0) return -1;
+
+#define PHYS_CHECK(end_) \
+    if ((end_) > D.physcap) return kDecodeOutputTooSmall;
+
+    if (oend - op < 64) goto safe_decode;
+    for (;;) {
+        token = D.in8(ip++);
+        length = token >> 4;
+        if (length == 15) {
+            e = D.rvl(ip, iend - 15, true, true, ext);
+            length += ext;
+            if (e == -1) goto output_error;
+            cpy = op + length;
+            if (cpy > oend - 32 || ip + length > iend - 32) goto safe_literal_copy;
+        } else {
+            cpy = op + length;
+            if (ip > iend - 17) goto safe_literal_copy;
+        }
+        PHYS_CHECK(cpy);
+        D.copy_lit(ip, op, length);
+        ip += length;
+        op = cpy;
+        offset = D.in8(ip) | (D.in8(ip + 1) << 8);
+        ip += 2;
+        match = op - (int64_t)offset;
+        length = token & 15;
+        if (length == 15) {
+            if (match < 0) goto output_error;
+            e = D.rvl(ip, iend - kLastLiterals + 1, true, false, ext);
+            length += ext;
+            if (e != 0) goto output_error;
+            length += kMinMatch;
+            if (op + length >= oend - 64) goto safe_match_copy;
+        } else {
+            length += kMinMatch;
+            if (op + length >= oend - 64) goto safe_match_copy;
+            if (match >= 0 && offset >= 8) {
+                PHYS_CHECK(op + length);
+                D.copy_match(op, offset, length);
+                op += length;
+                continue;
+            }
+        }
+        if (match < 0) goto output_error;
+        cpy = op + length;
+        PHYS_CHECK(cpy);
+        D.copy_match(op, offset, length);
+        op = cpy;
+    }
+
+safe_decode:
+    for (;;) {
+        token = D.in8(ip++);
+        length = token >> 4;
+        if (length != 15 && ip < shortiend && op <= shortoend) {
+            PHYS_CHECK(op + length);
+            D.copy_lit(ip, op, length);
+            op += length;
+            ip += length;
+            length = token & 15;
+            offset = D.in8(ip) | (D.in8(ip + 1) << 8);
+            ip += 2;
+            match = op - (int64_t)offset;
+            if (length != 15 && offset >= 8 && match >= 0) {
+                PHYS_CHECK(op + length + kMinMatch);
+                D.copy_match(op, offset, length + kMinMatch);
+                op += length + kMinMatch;
+                continue;
+            }
+            goto copy_match;
+        }
+        if (length == 15) {
+            e = D.rvl(ip, iend - 15, true, true, ext);
+            length += ext;
+            if (e == -1) goto output_error;
+        }
+        cpy = op + length;
+    safe_literal_copy:
+        if (cpy > oend - kMfLimit || ip + length > iend - (2 + 1 + kLastLiterals)) {
+            if (ip + length != iend || cpy > oend) goto output_error;
+            PHYS_CHECK(cpy);
+            D.copy_lit(ip, op, length);
+            ip += length;
+            op += length;
+            break;
+        }
+        PHYS_CHECK(cpy);
+        D.copy_lit(ip, op, length);
+        ip += length;
+        op = cpy;
+        offset = D.in8(ip) | (D.in8(ip + 1) << 8);
+        ip += 2;
+        match = op - (int64_t)offset;
+        length = token & 15;
+    copy_match:
+        if (length == 15) {
+            e = D.rvl(ip, iend - kLastLiterals + 1, true, false, ext);
+            length += ext;
+            if (e != 0) goto output_error;
+        }
+        length += kMinMatch;
+    safe_match_copy:
+        if (match < 0) goto output_error;
+        cpy = op + length;
+        if (cpy > oend - kLastLiterals) goto output_error;
+        PHYS_CHECK(cpy);
+        D.copy_match(op, offset, length);
+        op = cpy;
+    }
+#undef PHYS_CHECK
+    D.flush_tail(op);
+    return (int32_t)op;
+
+output_error:
+    return (int32_t)(-ip) - 1;
+}
+
+// raw (incompressible) block: src at any alignment -> dst 16-B aligned
+__device__ void copy_raw(const uint8_t* src, uint8_t* dst, int64_t n) {
+    const uint32_t L = laneid();
+    const int64_t nd = n >> 2;   // whole destination dwords
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
+    for (int64_t base = 0; base < nd; base += 64 * 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t j = base + u * 64 + L;
+            if (j < nd) d32[j] = ld32u(src + 4 * j);
+        }
+    }
+    for (int64_t i = nd * 4 + L; i < n; i += 64) dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ frame, const BlockRec* __restrict__ recs,
+                                               uint32_t blockMax, uint8_t* __restrict__ out, uint64_t outCap,
+                                               int32_t* __restrict__ dsize) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kInWin];
+    const uint32_t b = blockIdx.x;
+    const BlockRec r = recs[b];
+    const uint64_t slot = (uint64_t)b * blockMax;
+    const int64_t physcap = outCap > slot ? (int64_t)min<uint64_t>(blockMax, outCap - slot) : 0;
+    const int64_t len = r.bits & 0x7FFFFFFFu;
+    int32_t res;
+    if (r.bits & 0x80000000u) {
+        if (len > physcap) res = kDecodeOutputTooSmall;
+        else { copy_raw(frame + r.offset, out + slot, len); res = (int32_t)len; }
+    } else {
+        Dec D;
+        D.src = frame + r.offset;
+        D.len = len;
+        D.dst = out + slot;
+        D.physcap = physcap;
+        D.ring = ring;
+        D.win = win;
+        D.wlo = INT64_MIN / 4;
+        D.flushed = 0;
+        D.completed = 0;
+        res = decode_block(D, (int64_t)blockMax);
+    }
+    if (laneid() == 0) dsize[b] = res;
+}
+
+hipError_t launch_decode(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax, uint8_t* out,
+                         uint64_t outCap, int32_t* dsize, hipStream_t st) {
+    if (nBlocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_decode, dim3(nBlocks), dim3(64), 0, st, frame, recs, blockMax, out, outCap, dsize);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// XXH32: 4 lanes per block (one per accumulator), 16 blocks per wavefront
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t xround(uint32_t acc, uint32_t w) { return rotl32(acc + w * kP2, 13) * kP1; }
+
+// All 4 lanes of a quad call this with the same (p, len); lane c = quad lane.
+__device__ uint32_t xxh32_quad(const uint8_t* p, uint64_t len, uint32_t c, uint32_t quadBase) {
+    uint32_t v = (c == 0) ? kP1 + kP2 : (c == 1) ? kP2 : (c == 2) ? 0u : (uint32_t)(0u - kP1);
+    const uint64_t ns = len >> 4;
+    uint64_t i = 0;
+    for (; i + 8 <= ns; i += 8) {
+        uint32_t w[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) w[u] = ld32u(p + 16 * (i + u) + 4 * c);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v = xround(v, w[u]);
+    }
+    for (; i < ns; ++i) v = xround(v, ld32u(p + 16 * i + 4 * c));
+    const uint32_t v1 = __shfl(v, quadBase + 0), v2 = __shfl(v, quadBase + 1);
+    const uint32_t v3 = __shfl(v, quadBase + 2), v4 = __shfl(v, quadBase + 3);
+    uint32_t h;
+    if (len >= 16) h = rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18);
+    else h = kP5;
+    h += (uint32_t)len;
+    uint64_t o = ns << 4;
+    for (; o + 4 <= len; o += 4) h = rotl32(h + ld32u(p + o) * kP3, 17) * kP4;
+    for (; o < len; ++o) h = rotl32(h + p[o] * kP5, 11) * kP1;
+    h ^= h >> 15; h *= kP2; h ^= h >> 13; h *= kP3; h ^= h >> 16;
+    return h;
+}
+
+// stored bytes of compress-side block b: the slot if it compressed, else the source
+__global__ void __launch_bounds__(256) k_xxh32_stored(const uint8_t* __restrict__ src, const uint8_t* __restrict__ slots,
+                                                      uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                                                      const int32_t* __restrict__ csize, uint32_t* __restrict__ digest) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t b = t >> 2, c = t & 3;
+    const uint32_t quadBase = laneid() & ~3u;
+    const bool valid = b < nBlocks;
+    const uint32_t bb = valid ? b : nBlocks - 1;
+    const uint64_t off = (uint64_t)bb * blockSize;
+    const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
+    const int32_t cs = csize[bb];
+    const uint8_t* p = cs > 0 ? slots + off : src + off;
+    const uint64_t len = cs > 0 ? (uint64_t)cs : n;
+    const uint32_t h = xxh32_quad(p, len, c, quadBase);
+    if (valid && c == 0) digest[b] = h;
+}
+
+__global__ void __launch_bounds__(256) k_xxh32_frame_blocks(const uint8_t* __restrict__ frame,
+                                                            const BlockRec* __restrict__ recs, uint32_t nBlocks,
+                                                            uint32_t* __restrict__ digest) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t b = t >> 2, c = t & 3;
+    const uint32_t quadBase = laneid() & ~3u;
+    const bool valid = b < nBlocks;
+    const BlockRec r = recs[valid ? b : nBlocks - 1];
+    const uint32_t h = xxh32_quad(frame + r.offset, r.bits & 0x7FFFFFFFu, c, quadBase);
+    if (valid && c == 0) digest[b] = h;
+}
+
+// whole-stream XXH32 (lz4mt's serial content checksum): ONE quad, by design
+__global__ void __launch_bounds__(64) k_xxh32_stream(const uint8_t* __restrict__ p, uint64_t len,
+                                                     uint32_t* __restrict__ digest) {
+    const uint32_t L = laneid();
+    const uint32_t h = xxh32_quad(p, len, L & 3, L & ~3u);
+    if (L == 0) *digest = h;
+}
+
+hipError_t launch_xxh32_stored(const uint8_t* src, const uint8_t* slots, uint64_t srcSize, uint32_t blockSize,
+                               uint32_t nBlocks, const int32_t* csize, uint32_t* digest, hipStream_t st) {
+    if (nBlocks == 0) return hipSuccess;
+    const uint32_t threads = nBlocks * 4;
+    hipLaunchKernelGGL(k_xxh32_stored, dim3((threads + 255) / 256), dim3(256), 0, st, src, slots, srcSize, blockSize,
+                       nBlocks, csize, digest);
+    return hipGetLastError();
+}
+
+hipError_t launch_xxh32_frame_blocks(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t* digest,
+                                     hipStream_t st) {
+    if (nBlocks == 0) return hipSuccess;
+    const uint32_t threads = nBlocks * 4;
+    hipLaunchKernelGGL(k_xxh32_frame_blocks, dim3((threads + 255) / 256), dim3(256), 0, st, frame, recs, nBlocks,
+                       digest);
+    return hipGetLastError();
+}
+
+hipError_t launch_xxh32_stream(const uint8_t* p, uint64_t len, uint32_t* digest, hipStream_t st) {
+    hipLaunchKernelGGL(k_xxh32_stream, dim3(1), dim3(64), 0, st, p, len, digest);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Frame assembly: record sizes -> exclusive scan -> scatter
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_frame_scan(const int32_t* __restrict__ csize, uint64_t srcSize,
+                                                     uint32_t blockSize, uint32_t nBlocks, int blockChecksum,
+                                                     uint64_t* __restrict__ recOff) {
+    __shared__ uint64_t part[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (nBlocks + 1023) / 1024;
+    const uint32_t lo = min(nBlocks, t * per), hi = min(nBlocks, lo + per);
+    auto recsz = [&](uint32_t b) -> uint64_t {
+        const uint64_t off = (uint64_t)b * blockSize;
+        const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
+        const int32_t cs = csize[b];
+        return 4ull + (cs > 0 ? (uint64_t)cs : n) + (blockChecksum ? 4ull : 0ull);
+    };
+    uint64_t sum = 0;
+    for (uint32_t b = lo; b < hi; ++b) sum += recsz(b);
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint64_t v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint64_t run = part[t] - sum;  // exclusive base
+    for (uint32_t b = lo; b < hi; ++b) { recOff[b] = run; run += recsz(b); }
+    if (t == 1023) recOff[nBlocks] = part[1023];
+}
+
+__global__ void __launch_bounds__(256) k_frame_assemble(const uint8_t* __restrict__ src, const uint8_t* __restrict__ slots,
+                                                        uint64_t srcSize, uint32_t blockSize,
+                                                        const int32_t* __restrict__ csize,
+                                                        const uint32_t* __restrict__ bsum,
+                                                        const uint64_t* __restrict__ recOff, int blockChecksum,
+                                                        uint8_t* __restrict__ frame, uint32_t hdrLen) {
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
+    const int32_t cs = csize[b];
+    const uint8_t* sp = cs > 0 ? slots + off : src + off;   // 16-B aligned
+    const uint64_t L = cs > 0 ? (uint64_t)cs : n;
+    const uint32_t bits = cs > 0 ? (uint32_t)cs : (n | 0x80000000u);
+    uint8_t* rec = frame + hdrLen + recOff[b];
+    uint8_t* D = rec + 4;
+    if (t < 4) rec[t] = (uint8_t)(bits >> (8 * t));
+    if (blockChecksum && t >= 4 && t < 8) D[L + (t - 4)] = (uint8_t)(bsum[b] >> (8 * (t - 4)));
+    const uintptr_t Da = reinterpret_cast<uintptr_t>(D);
+    const uintptr_t A0 = (Da + 15) & ~uintptr_t(15);
+    const uintptr_t E = Da + L, E0 = E & ~uintptr_t(15);
+    if (A0 >= E0) {  // short payload: bytes only
+        for (uint64_t i = t; i < L; i += 256) D[i] = sp[i];
+        return;
+    }
+    const uint64_t head = A0 - Da, tailStart = E0 - Da;
+    for (uint64_t i = t; i < head; i += 256) D[i] = sp[i];
+    for (uint64_t i = tailStart + t; i < L; i += 256) D[i] = sp[i];
+    // middle: 16-B aligned destination chunks gathered from the source
+    const uint64_t nchunks = (E0 - A0) >> 4;
+    for (uint64_t j = t; j < nchunks; j += 256) {
+        const uint64_t so = head + 16 * j;                 // source byte offset of this chunk
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(sp + (so & ~3ull));
+        const uint32_t s3 = (uint32_t)(so & 3);
+        const uint32_t a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+        const uint32_t a4 = s3 ? q[4] : 0u;
+        uint4 v;
+        v.x = __builtin_amdgcn_alignbyte(a1, a0, s3);
+        v.y = __builtin_amdgcn_alignbyte(a2, a1, s3);
+        v.z = __builtin_amdgcn_alignbyte(a3, a2, s3);
+        v.w = __builtin_amdgcn_alignbyte(a4, a3, s3);
+        *reinterpret_cast<uint4*>(A0 + 16 * j) = v;
+    }
+}
+
+struct HdrBytes { uint8_t b[20]; };
+
+__global__ void k_frame_finalize(uint8_t* __restrict__ frame, HdrBytes hdr, uint32_t hdrLen,
+                                 const uint64_t* __restrict__ recOff, uint32_t nBlocks,
+                                 const uint32_t* __restrict__ streamSum, uint64_t* __restrict__ frameSize) {
+    const uint32_t t = threadIdx.x;
+    if (t < hdrLen) frame[t] = hdr.b[t];
+    const uint64_t eos = hdrLen + recOff[nBlocks];
+    if (t < 4) frame[eos + t] = 0;
+    uint64_t total = eos + 4;
+    if (streamSum) {
+        if (t < 4) frame[eos + 4 + t] = (uint8_t)(*streamSum >> (8 * t));
+        total += 4;
+    }
+    if (t == 0) *frameSize = total;
+}
+
+hipError_t launch_frame_scan(const int32_t* csize, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                             int blockChecksum, uint64_t* recOff, hipStream_t st) {
+    hipLaunchKernelGGL(k_frame_scan, dim3(1), dim3(1024), 0, st, csize, srcSize, blockSize, nBlocks, blockChecksum,
+                       recOff);
+    return hipGetLastError();
+}
+
+hipError_t launch_frame_assemble(const uint8_t* src, const uint8_t* slots, uint64_t srcSize, uint32_t blockSize,
+                                 uint32_t nBlocks, const int32_t* csize, const uint32_t* bsum, const uint64_t* recOff,
+                                 int blockChecksum, uint8_t* frame, uint32_t hdrLen, hipStream_t st) {
+    if (nBlocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_frame_assemble, dim3(nBlocks), dim3(256), 0, st, src, slots, srcSize, blockSize, csize, bsum,
+                       recOff, blockChecksum, frame, hdrLen);
+    return hipGetLastError();
+}
+
+hipError_t launch_frame_finalize(uint8_t* frame, const uint8_t* hdr, uint32_t hdrLen, const uint64_t* recOff,
+                                 uint32_t nBlocks, const uint32_t* streamSum, uint64_t* frameSize, hipStream_t st) {
+    HdrBytes h{};
+    for (uint32_t i = 0; i < hdrLen && i < 20; ++i) h.b[i] = hdr[i];
+    hipLaunchKernelGGL(k_frame_finalize, dim3(1), dim3(64), 0, st, frame, h, hdrLen, recOff, nBlocks, streamSum,
+                       frameSize);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Frame walk (decompress side): follows the block size words serially.
+// Result codes follow src/lz4mt.cpp:685-727.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rd32b(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+__global__ void k_frame_walk(const uint8_t* __restrict__ frame, uint64_t frameSize, uint64_t pos, uint32_t blockMax,
+                             int blockChecksum, uint32_t maxBlocks, BlockRec* __restrict__ recs,
+                             WalkInfo* __restrict__ info) {
+    if (threadIdx.x != 0) return;
+    uint32_t nb = 0;
+    int32_t result = 0;
+    for (;;) {
+        if (pos + 4 > frameSize) { result = 12; break; }             // CANNOT_READ_BLOCK_SIZE
+        const uint32_t bits = rd32b(frame + pos);
+        pos += 4;
+        if (bits == 0) break;                                        // EOS
+        const uint32_t sz = bits & 0x7FFFFFFFu;
+        if (sz > blockMax) { result = 20; break; }                   // INVALID_BLOCK_SIZE
+        if (pos + sz > frameSize) { result = 13; pos = frameSize; break; }  // CANNOT_READ_BLOCK_DATA
+        BlockRec r{pos, bits, 0};
+        pos += sz;
+        if (blockChecksum) {
+            if (pos + 4 > frameSize) { result = 14; break; }         // CANNOT_READ_BLOCK_CHECKSUM
+            r.checksum = rd32b(frame + pos);
+            pos += 4;
+        }
+        if (nb >= maxBlocks) { result = 1; break; }
+        recs[nb++] = r;
+    }
+    info->endPos = pos;
+    info->nBlocks = nb;
+    info->result = result;
+}
+
+hipError_t launch_frame_walk(const uint8_t* frame, uint64_t frameSize, uint64_t bodyPos, uint32_t blockMax,
+                             int blockChecksum, uint32_t maxBlocks, BlockRec* recs, WalkInfo* info, hipStream_t st) {
+    hipLaunchKernelGGL(k_frame_walk, dim3(1), dim3(64), 0, st, frame, frameSize, bodyPos, blockMax, blockChecksum,
+                       maxBlocks, recs, info);
+    return hipGetLastError();
+}
+
+// Per-block decode status in the reference's precedence: decode failure
+// (src/lz4mt.cpp:647-650) before block checksum mismatch (675-681).
+__global__ void k_block_verify(const BlockRec* __restrict__ recs, uint32_t nBlocks, const uint32_t* __restrict__ digest,
+                               const int32_t* __restrict__ dsize, uint32_t blockMax, int blockChecksum,
+                               int32_t* __restrict__ status) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nBlocks) return;
+    int32_t st = 0;
+    if (dsize[b] < 0) st = (dsize[b] == kDecodeOutputTooSmall) ? 1 : 18;   // ERROR / DECOMPRESS_FAIL
+    else if (blockChecksum && digest[b] != recs[b].checksum) st = 16;      // BLOCK_CHECKSUM_MISMATCH
+    status[b] = st;
+}
+
+hipError_t launch_block_verify(const BlockRec* recs, uint32_t nBlocks, const uint32_t* digest, const int32_t* dsize,
+                               uint32_t blockMax, int blockChecksum, int32_t* status, hipStream_t st) {
+    if (nBlocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_block_verify, dim3((nBlocks + 255) / 256), dim3(256), 0, st, recs, nBlocks, digest, dsize,
+                       blockMax, blockChecksum, status);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic input: one workgroup per 64 KiB segment,
+// generated serially by lane 0 in LDS (back-copies read LDS), then stored
+// with coalesced 16-B writes.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t sm_next(uint64_t& s) {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(64) k_gen_synthetic(uint8_t* __restrict__ dst, uint64_t n, uint64_t seed) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[65536 + 128];
+    const uint64_t seg = blockIdx.x;
+    if (threadIdx.x == 0) {
+        uint64_t s = seed + seg * 0x9E3779B97F4A7C15ull;
+        uint32_t len = 0;
+        while (len < 65536) {
+            const uint64_t r = sm_next(s);
+            if (len >= 64 && (r & 255) < 76) {
+                const uint32_t Lm = 4 + (uint32_t)((r >> 8) & 63);
+                const uint32_t lim = len < 65535 ? len : 65535;
+                const uint32_t off = 1 + (uint32_t)((r >> 16) % lim);
+                for (uint32_t k = 0; k < Lm; ++k, ++len) buf[len] = buf[len - off];
+            } else {
+                const uint32_t cnt = (uint32_t)((r >> 8) & 15) + 1;
+                for (uint32_t k = 0; k < cnt; ++k) buf[len++] = (uint8_t)(97 + (sm_next(s) >> 40) % 26);
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t base = seg * 65536;
+    const uint64_t take = (n - base) < 65536 ? (n - base) : 65536;
+    if (take == 65536 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        for (uint32_t i = threadIdx.x; i < 4096; i += 64)
+            reinterpret_cast<uint4*>(dst + base)[i] = reinterpret_cast<const uint4*>(buf)[i];
+    } else {
+        for (uint64_t i = threadIdx.x; i < take; i += 64) dst[base + i] = buf[i];
+    }
+}
+
+hipError_t launch_gen_synthetic(uint8_t* dst, uint64_t n, uint64_t seed, hipStream_t st) {
+    const uint64_t segs = (n + 65535) / 65536;
+    if (segs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_synthetic, dim3((uint32_t)segs), dim3(64), 0, st, dst, n, seed);
+    return hipGetLastError();
+}
+
+}  // namespace lz4mt

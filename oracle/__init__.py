@@ -1,0 +1,113 @@
+"""ctypes wrapper of oracle/liblz4mt_oracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, and only as the checker / CPU baseline.  The product
+(lz4mt_amd/) never imports it.  See lz4_oracle.h for what it restates and
+how it is pinned (liblz4 1.9.3, python-xxhash, lz4 CLI).
+"""
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblz4mt_oracle.so")
+
+
+class FrameParams(ctypes.Structure):
+    _fields_ = [("streamChecksum", ctypes.c_int), ("blockChecksum", ctypes.c_int), ("blockMaxId", ctypes.c_int),
+                ("streamSizeFlag", ctypes.c_int), ("streamSize", ctypes.c_uint64)]
+
+
+def build():
+    subprocess.run(["make", "-C", HERE, "-s"], check=True)
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        build()
+    lib = ctypes.CDLL(LIB_PATH)
+    u8p, sz = ctypes.c_void_p, ctypes.c_size_t
+    lib.orc_xxh32.restype = ctypes.c_uint32
+    lib.orc_xxh32.argtypes = [u8p, sz, ctypes.c_uint32]
+    lib.orc_lz4_compress_bound.restype = ctypes.c_int
+    lib.orc_lz4_compress.argtypes = [u8p, u8p, ctypes.c_int, ctypes.c_int]
+    lib.orc_lz4_decompress_safe.argtypes = [u8p, u8p, ctypes.c_int, ctypes.c_int]
+    lib.orc_frame_bound.restype = sz
+    lib.orc_frame_bound.argtypes = [sz, ctypes.POINTER(FrameParams)]
+    lib.orc_frame_compress.restype = sz
+    lib.orc_frame_compress.argtypes = [u8p, sz, u8p, ctypes.POINTER(FrameParams), ctypes.c_int]
+    lib.orc_frame_decompress.argtypes = [u8p, sz, u8p, sz, ctypes.POINTER(sz), ctypes.c_int]
+    lib.orc_gen_synthetic.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64]
+    lib.orc_gen_random.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64]
+    lib.orc_pipeline_roundtrip.argtypes = [u8p, sz, ctypes.POINTER(FrameParams), ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz)]
+    return lib
+
+
+lib = _load()
+
+
+def _buf(data):
+    return ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+
+
+def xxh32(data, seed=0):
+    return lib.orc_xxh32(_buf(data), len(data), seed)
+
+
+def compress_block(data, cap=None):
+    """LZ4_compress_limitedOutput(src, dst, n, cap) restated; b'' when it does not fit."""
+    cap = len(data) if cap is None else cap
+    dst = ctypes.create_string_buffer(max(cap, lib.orc_lz4_compress_bound(len(data))) + 16)
+    n = lib.orc_lz4_compress(_buf(data), dst, len(data), cap)
+    return dst.raw[:n]
+
+
+def decompress_block(block, cap):
+    """LZ4_decompress_safe restated: (ret, bytes)."""
+    dst = ctypes.create_string_buffer(max(cap, 1) + 16)
+    n = lib.orc_lz4_decompress_safe(_buf(block), dst, len(block), cap)
+    return n, (dst.raw[:n] if n > 0 else b"")
+
+
+def params(block_max_id=7, stream_checksum=True, block_checksum=False, stream_size=None):
+    return FrameParams(1 if stream_checksum else 0, 1 if block_checksum else 0, block_max_id,
+                       0 if stream_size is None else 1, stream_size or 0)
+
+
+def compress_frame(data, p=None, threads=8):
+    p = p or params()
+    cap = lib.orc_frame_bound(len(data), ctypes.byref(p))
+    dst = ctypes.create_string_buffer(cap)
+    n = lib.orc_frame_compress(_buf(data), len(data), dst, ctypes.byref(p), threads)
+    return dst.raw[:n]
+
+
+def decompress_frame(frame, out_cap, threads=8):
+    """(result code, decoded bytes) with lz4mtDecompress semantics."""
+    dst = ctypes.create_string_buffer(max(out_cap, 1))
+    osz = ctypes.c_size_t(0)
+    r = lib.orc_frame_decompress(_buf(frame), len(frame), dst, out_cap, ctypes.byref(osz), threads)
+    return r, dst.raw[:osz.value]
+
+
+def gen_synthetic(n, seed=42):
+    b = ctypes.create_string_buffer(max(n, 1))
+    lib.orc_gen_synthetic(b, n, seed)
+    return b.raw[:n]
+
+
+def gen_random(n, seed=7):
+    b = ctypes.create_string_buffer(max(n, 1))
+    lib.orc_gen_random(b, n, seed)
+    return b.raw[:n]
+
+
+def pipeline_roundtrip(data_buf, n, p, threads):
+    """lz4mt-shaped CPU pipeline timing: (compress_s, decompress_s, frame_bytes)."""
+    secs = (ctypes.c_double * 2)()
+    fs = ctypes.c_size_t(0)
+    err = lib.orc_pipeline_roundtrip(data_buf, n, ctypes.byref(p), threads, secs, ctypes.byref(fs))
+    if err:
+        raise RuntimeError("oracle pipeline decode error")
+    return secs[0], secs[1], fs.value

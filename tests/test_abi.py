@@ -1,0 +1,187 @@
+"""CPU-side checks of the drop-in boundary (no GPU compute here).
+
+* the library loads and exports every symbol include/*.h declares;
+* struct layouts match the reference's x86-64 ABI (src/lz4mt.h:102-147);
+* the headers compile as C and C++;
+* init/result functions behave like the reference (src/lz4mt.cpp:851-895,
+  src/lz4mt_result.cpp);
+* the host frame engine (lz4mtCompress / lz4mtDecompress) driven by a
+  plug-in CPU codec (liblz4 1.9.3 via the reference's own operator API)
+  writes the golden frames and reports the reference's error codes;
+* device entry points fail loudly without a GPU.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT, read_golden
+
+import lz4mt_amd as L
+from lz4mt_amd import _abi
+
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("lz4mt.h", "lz4mt_hip.h", "lz4mt_io.h")]
+LIBLZ4 = "/lib/x86_64-linux-gnu/liblz4.so.1"
+
+
+def declared_functions():
+    names = set()
+    for h in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b(lz4mt\w+)\s*\(", text, flags=re.M):
+            if not m.group(0).lstrip().startswith("typedef"):
+                names.add(m.group(1))
+    return names
+
+
+def test_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", _abi.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    declared = declared_functions()
+    assert len(declared) >= 30
+    missing = declared - exported
+    assert not missing, missing
+    assert declared == set(_abi.PROTOTYPES), declared ^ set(_abi.PROTOTYPES)
+
+
+def test_struct_layout_matches_reference_abi():
+    C = _abi.Lz4MtContext
+    assert ctypes.sizeof(C) == 96
+    offs = {n: getattr(C, n).offset for n, _ in C._fields_}
+    assert offs == {"result": 0, "readCtx": 8, "read": 16, "readSkippable": 24, "readSeek": 32, "readEof": 40,
+                    "writeCtx": 48, "write": 56, "compress": 64, "compressBound": 72, "decompress": 80,
+                    "mode": 88, "compressionLevel": 92}
+    S = _abi.Lz4MtStreamDescriptor
+    assert ctypes.sizeof(S) == 32
+    assert (S.flg.offset, S.bd.offset, S.streamSize.offset, S.dictId.offset) == (0, 7, 16, 24)
+
+
+@pytest.mark.parametrize("compiler,ext", [("gcc", "c"), ("g++", "cpp")])
+def test_headers_compile(tmp_path, compiler, ext):
+    src = tmp_path / f"t.{ext}"
+    src.write_text('#include "lz4mt.h"\n#include "lz4mt_hip.h"\n#include "lz4mt_io.h"\n'
+                   "_Static_assert(sizeof(Lz4MtContext) == 96, \"ctx\");\n" if ext == "c" else
+                   '#include "lz4mt.h"\n#include "lz4mt_hip.h"\n#include "lz4mt_io.h"\n'
+                   "static_assert(sizeof(Lz4MtContext) == 96, \"ctx\");\n"
+                   "static_assert(sizeof(Lz4MtStreamDescriptor) == 32, \"sd\");\n")
+    subprocess.run([compiler, "-Wall", "-Werror", "-c", "-I", os.path.join(ROOT, "include"), str(src), "-o",
+                    str(tmp_path / "t.o")], check=True)
+
+
+def test_init_functions():
+    c = L.init_context()
+    assert c.result == 0 and c.mode == L.MODE_PARALLEL and c.compressionLevel == 0
+    assert not any([c.read, c.write, c.compress, c.decompress, c.readEof, c.readSeek, c.readSkippable])
+    sd = L.init_stream_descriptor()
+    assert (sd.flg.streamChecksum, sd.flg.blockIndependence, sd.flg.versionNumber, sd.bd.blockMaximumSize) == \
+        (1, 1, 1, 7)
+    assert (sd.flg.blockChecksum, sd.flg.streamSize, sd.flg.presetDictionary, sd.streamSize, sd.dictId) == \
+        (0, 0, 0, 0, 0)
+
+
+def test_result_strings_and_exit_codes():
+    for i, name in enumerate(L.RESULT_NAMES):
+        assert L.result_to_string(i) == name
+    assert L.result_to_string(99) == "Unknown code"
+    expect = {0: 0, 1: 1, 2: 44, 3: 61, 4: 66, 5: 1, 6: 62, 7: 69, 8: 68, 9: 32, 10: 37, 11: 37, 12: 71, 13: 73,
+              14: 74, 15: 74, 16: 75, 17: 75, 18: 77, 19: 1, 20: 72, 21: 65, 22: 67, 23: 67, 24: 42, 25: 43,
+              26: 76, 27: 78}
+    for code, e in expect.items():
+        assert L.result_to_exit_code(code) == e, code
+
+
+def test_device_entry_points_fail_without_gpu():
+    if L.device_count() > 0:
+        pytest.skip("a HIP device is present")
+    assert L.lib.lz4mtHipCompressBlock(b"abcdabcdabcdabcd", ctypes.create_string_buffer(64), 16, 16, 0) < 0
+    sd = L.init_stream_descriptor()
+    r = L.lib.lz4mtHipCompressFrame(None, 0, ctypes.c_void_p(1), 1 << 20, None, ctypes.byref(sd), None, 0, None)
+    assert r == L.Result.ERROR
+
+
+# ---------------------------------------------------------------------------
+# host frame engine with a plug-in CPU codec (the reference's operator API)
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def cpu_codec():
+    if not os.path.exists(LIBLZ4):
+        pytest.skip("liblz4 not present")
+    lz = ctypes.CDLL(LIBLZ4)
+
+    def comp(src, dst, n, cap, level):
+        return lz.LZ4_compress_limitedOutput(ctypes.c_void_p(src), ctypes.c_void_p(dst), n, cap)
+
+    def decomp(src, dst, n, cap):
+        return lz.LZ4_decompress_safe(ctypes.c_void_p(src), ctypes.c_void_p(dst), n, cap)
+    return comp, decomp
+
+
+@pytest.mark.parametrize("mode", [L.MODE_SEQUENTIAL, L.MODE_PARALLEL])
+def test_host_engine_writes_golden_frames(golden, golden_inputs, cpu_codec, mode):
+    comp, decomp = cpu_codec
+    for f in golden["frames"]:
+        if golden_inputs[f["input"]].__len__() > 70_000 and f["bid"] == 4:
+            continue   # keep the CPU suite fast
+        data = golden_inputs[f["input"]]
+        sd = L.make_sd(f["bid"], f["stream_checksum"], f["block_checksum"])
+        r, frame = L.compress(data, sd, mode=mode, compress_cb=comp)
+        assert r == 0, (f["file"], L.result_to_string(r))
+        assert frame == read_golden(f["file"]), f["file"]
+        r, out, sd2 = L.decompress(frame, len(data) + 64, mode=mode, decompress_cb=decomp)
+        assert r == 0 and out == data, (f["file"], L.result_to_string(r))
+        assert (sd2.bd.blockMaximumSize, sd2.flg.blockChecksum, sd2.flg.streamChecksum) == \
+            (f["bid"], int(f["block_checksum"]), int(f["stream_checksum"]))
+
+
+def test_host_engine_error_codes(golden_inputs, cpu_codec):
+    comp, decomp = cpu_codec
+    data = golden_inputs["syn300k"]
+    r, f = L.compress(data, L.make_sd(5, True, True), compress_cb=comp)
+    assert r == 0
+
+    def dec(b):
+        return L.decompress(b, len(data) + 64, mode=L.MODE_SEQUENTIAL, decompress_cb=decomp)[0]
+    R = L.Result
+    assert dec(f) == R.OK
+    assert dec(b"\x01\x02\x03\x04rest") == R.INVALID_MAGIC_NUMBER
+    bad = bytearray(f); bad[6] ^= 1
+    assert dec(bytes(bad)) == R.INVALID_HEADER_CHECKSUM
+    bad = bytearray(f); bad[4] &= 0x3F
+    assert dec(bytes(bad)) == R.INVALID_VERSION
+    bad = bytearray(f); bad[5] = 0x30
+    assert dec(bytes(bad)) == R.INVALID_BLOCK_MAXIMUM_SIZE
+    bad = bytearray(f); bad[20] ^= 0xFF
+    assert dec(bytes(bad)) in (R.BLOCK_CHECKSUM_MISMATCH, R.DECOMPRESS_FAIL)
+    assert dec(f[:-2]) == R.CANNOT_READ_STREAM_CHECKSUM
+    assert dec(f[:100]) == R.CANNOT_READ_BLOCK_DATA
+    bad = bytearray(f); bad[-1] ^= 1
+    assert dec(bytes(bad)) == R.STREAM_CHECKSUM_MISMATCH
+    skip = (0x184D2A51).to_bytes(4, "little") + (5).to_bytes(4, "little") + b"12345"
+    r, out, _ = L.decompress(f + skip + f + b"junkjunk", 2 * len(data) + 64, decompress_cb=decomp)
+    assert r == R.OK and out == data + data
+    # block-dependent frames are out of scope and say so
+    sd = L.make_sd(7)
+    sd.flg.blockIndependence = 0
+    assert L.compress(b"abc", sd, compress_cb=comp)[0] == R.BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET
+
+
+def test_cstdio_adapters(tmp_path, golden_inputs, cpu_codec):
+    comp, decomp = cpu_codec
+    data = golden_inputs["text20k"]
+    src, dst = tmp_path / "in.bin", tmp_path / "out.lz4"
+    src.write_bytes(data)
+    ctx = L.init_context()
+    keep = [_abi.COMPRESS_FN(comp)]
+    ctx.compress = ctypes.cast(keep[0], ctypes.c_void_p)
+    L.lib.lz4mtIoBindCstdio(ctypes.byref(ctx))
+    assert L.lib.lz4mtIoOpenIstream(ctypes.byref(ctx), str(src).encode())
+    assert L.lib.lz4mtIoOpenOstream(ctypes.byref(ctx), str(dst).encode(), 0)
+    sd = L.init_stream_descriptor()
+    assert L.lib.lz4mtCompress(ctypes.byref(ctx), ctypes.byref(sd)) == 0
+    L.lib.lz4mtIoCloseIstream(ctypes.byref(ctx))
+    L.lib.lz4mtIoCloseOstream(ctypes.byref(ctx))
+    assert dst.read_bytes() == read_golden("frames/text20k.B7Sx.lz4")
+    assert L.lib.lz4mtIoGetFilesize(str(dst).encode()) == dst.stat().st_size

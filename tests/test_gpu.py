@@ -1,0 +1,220 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and
+the golden fixtures.  Bit-exact everywhere: this path is byte/integer work.
+
+Sizes: golden fixtures (bytes .. 300 KB), random block fuzz vs the oracle,
+the SURVEY.md App. F known answers at 256 MiB (frame size + XXH32 for all 10
+flag rows), and a 2 GiB round trip checked through size-independent
+properties (XXH32 of input == XXH32 of output, per-block checksums verified
+by the decoder, block sample vs the oracle).
+"""
+import ctypes
+import random
+
+import pytest
+import torch
+import xxhash
+
+import oracle
+from conftest import read_golden
+
+pytestmark = pytest.mark.gpu
+
+L = None
+
+
+@pytest.fixture(scope="module", autouse=True)
+def lib():
+    global L
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    import lz4mt_amd
+    L = lz4mt_amd
+    assert L.device_count() > 0
+    return L
+
+
+def dev(b):
+    t = torch.empty(max(len(b), 1), dtype=torch.uint8, device="cuda")
+    if b:
+        t[:len(b)].copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
+    return t[:len(b)]
+
+
+def host(t):
+    return bytes(t.cpu().numpy().tobytes())
+
+
+# ---------------------------------------------------------------------------
+# block operators (reference plugin signatures)
+# ---------------------------------------------------------------------------
+def test_block_compress_golden(golden, golden_inputs):
+    import hashlib
+    for v in golden["blocks"]:
+        data = golden_inputs[v["input"]][:v["n"]]
+        c = L.compress_block(data, v["cap"])
+        assert len(c) == v["ret"] and hashlib.sha1(c).hexdigest() == v["sha1"], v
+
+
+def test_block_compress_fuzz_vs_oracle():
+    rnd = random.Random(3)
+    syn = oracle.gen_synthetic(1 << 20)
+    for t in range(80):
+        n = rnd.choice([1, 7, 12, 13, 14, 20, 64, 100, 1000, 4095, 65535, 65546, 65547, 65548, 100_000, 262_144])
+        kind = t % 5
+        if kind == 0:
+            d = syn[:n]
+        elif kind == 1:
+            d = bytes(rnd.randrange(3) for _ in range(n))
+        elif kind == 2:
+            d = oracle.gen_random(n, t)
+        elif kind == 3:
+            d = (bytes(rnd.randrange(256) for _ in range(rnd.randrange(1, 70))) * (n + 1))[:n]
+        else:
+            d = bytes(n)
+        for cap in (n, max(n - 1, 0), n + n // 255 + 16, n // 2):
+            assert L.compress_block(d, cap) == oracle.compress_block(d, cap), (t, n, cap)
+
+
+def test_block_decompress_golden(golden, decode_blob):
+    for v in golden["decode"]:
+        blk = decode_blob[v["off"]:v["off"] + v["len"]]
+        r, out = L.decompress_block(blk, v["cap"])
+        assert r == v["ret"], v
+        if r >= 0:
+            assert xxhash.xxh32(out).intdigest() == v["out_xxh32"], v
+
+
+def test_block_decompress_crafted(golden):
+    for v in golden["crafted"]:
+        r, out = L.decompress_block(bytes.fromhex(v["block_hex"]), v["cap"])
+        assert r == v["ret"], v
+        if r >= 0:
+            assert xxhash.xxh32(out).intdigest() == v["out_xxh32"], v
+
+
+def test_block_decompress_long_matches():
+    # long overlapping / far matches (ring and HBM paths of the decoder)
+    rnd = random.Random(8)
+    parts = []
+    for i in range(300):
+        parts.append(bytes([rnd.randrange(256)]) * rnd.randrange(1, 5000))
+        parts.append(oracle.gen_random(rnd.randrange(1, 300), i))
+    d = b"".join(parts)[:4 << 20]
+    d = d + d[:40_000] + oracle.gen_synthetic(200_000)[:100_000] + d[100:70_000]
+    for n in (len(d) // 3, len(d)):
+        blk = oracle.compress_block(d[:n], n + n // 255 + 16)
+        r, out = L.decompress_block(blk, 4 << 20 if n <= 4 << 20 else n)
+        assert r == n and out == d[:n]
+
+
+# ---------------------------------------------------------------------------
+# device-resident frames
+# ---------------------------------------------------------------------------
+def test_gen_synthetic_matches_oracle():
+    for n in (1, 65536, 100_000, 8 << 20):
+        t = L.gen_synthetic(n)
+        assert host(t) == oracle.gen_synthetic(n)
+    assert L.xxh32(L.gen_synthetic(8 << 20)) == 0xD89F562C
+
+
+def test_device_xxh32():
+    rnd = random.Random(2)
+    for n in (0, 1, 15, 16, 17, 1000, 65537):
+        b = bytes(rnd.randrange(256) for _ in range(n))
+        assert L.xxh32(dev(b)) == xxhash.xxh32(b).intdigest()
+
+
+def test_frames_golden(golden, golden_inputs):
+    for f in golden["frames"]:
+        data = golden_inputs[f["input"]]
+        sd = L.make_sd(f["bid"], f["stream_checksum"], f["block_checksum"])
+        fr = L.compress_frame(dev(data), sd)
+        assert host(fr) == read_golden(f["file"]), f["file"]
+        out, r = L.decompress_frame(dev(read_golden(f["file"])))
+        assert r == 0 and host(out) == data, f["file"]
+
+
+def test_frame_decode_errors(golden_inputs):
+    data = golden_inputs["syn300k"]
+    f = host(L.compress_frame(dev(data), L.make_sd(5, True, True)))
+    R = L.Result
+
+    def code(b):
+        out = torch.empty(len(data) + (1 << 20), dtype=torch.uint8, device="cuda")
+        return L.decompress_frame(dev(b), out=out, check=False)[1]
+    assert code(f) == R.OK
+    assert code(b"\x01\x02\x03\x04rest") == R.INVALID_MAGIC_NUMBER
+    bad = bytearray(f); bad[6] ^= 1
+    assert code(bytes(bad)) == R.INVALID_HEADER_CHECKSUM
+    bad = bytearray(f); bad[20] ^= 0xFF
+    assert code(bytes(bad)) in (R.BLOCK_CHECKSUM_MISMATCH, R.DECOMPRESS_FAIL)
+    assert code(f[:-2]) == R.CANNOT_READ_STREAM_CHECKSUM
+    assert code(f[:100]) == R.CANNOT_READ_BLOCK_DATA
+    bad = bytearray(f); bad[-1] ^= 1
+    assert code(bytes(bad)) == R.STREAM_CHECKSUM_MISMATCH
+    skip = (0x184D2A51).to_bytes(4, "little") + (5).to_bytes(4, "little") + b"12345"
+    out = torch.empty(2 * len(data) + (1 << 20), dtype=torch.uint8, device="cuda")
+    o, r = L.decompress_frame(dev(f + skip + f + b"junkjunk"), out=out, check=False)
+    assert r == R.OK and host(o) == data + data
+
+
+@pytest.fixture(scope="module")
+def syn256():
+    t = L.gen_synthetic(256 << 20)
+    assert L.xxh32(t) == 0xE6F24EBA
+    return t
+
+
+@pytest.mark.parametrize("row", [
+    ((1, 0, 7), 133159140, 0x157099A8), ((0, 0, 7), 133159136, 0x8AC5DBC8), ((1, 1, 7), 133159396, 0xC532D9D2),
+    ((0, 1, 7), 133159392, 0x1686045A), ((1, 0, 4), 131940148, 0xFC3A55A1), ((1, 0, 5), 136141814, 0xAF5572EC),
+    ((1, 0, 6), 133770948, 0x7D1BC1BA), ((0, 1, 4), 131956528, 0xAB492B3C), ((0, 1, 5), 136145906, 0xE62BB3AC),
+    ((0, 1, 6), 133771968, 0x535404A3)])
+def test_known_answers_256mib(row, syn256):
+    (sc, bc, bid), size, h = row
+    fr = L.compress_frame(syn256, L.make_sd(bid, bool(sc), bool(bc)))
+    assert fr.numel() == size
+    assert L.xxh32(fr) == h
+    out, r = L.decompress_frame(fr)
+    assert r == 0 and out.numel() == syn256.numel() and L.xxh32(out) == 0xE6F24EBA
+
+
+def test_roundtrip_2gib_properties():
+    n = 2 << 30
+    src = L.gen_synthetic(n, seed=1234)
+    h_in = L.xxh32(src)
+    sd = L.make_sd(7, stream_checksum=False, block_checksum=True)
+    fr = L.compress_frame(src, sd)
+    # sample blocks against the oracle
+    f_host_head = host(fr[:3 << 20])
+    blk0 = oracle.compress_block(host(src[:4 << 20]), 4 << 20)
+    assert f_host_head[7:11] == len(blk0).to_bytes(4, "little")
+    assert f_host_head[11:11 + len(blk0)][:1 << 20] == blk0[:1 << 20]
+    out, r = L.decompress_frame(fr)
+    assert r == 0 and out.numel() == n
+    assert L.xxh32(out) == h_in
+    del out, fr, src
+    torch.cuda.empty_cache()
+
+
+def test_incompressible_is_raw():
+    d = oracle.gen_random(3 << 20, 5)
+    fr = host(L.compress_frame(dev(d), L.make_sd(6, True, True)))
+    assert fr == oracle.compress_frame(d, oracle.params(6, True, True))
+    assert int.from_bytes(fr[7:11], "little") == (1 << 20) | 0x80000000
+
+
+# ---------------------------------------------------------------------------
+# the lz4mt.h callback API on the GPU
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("mode", ["SEQUENTIAL", "PARALLEL", "DEVICE"])
+def test_callback_api_on_gpu(golden_inputs, mode):
+    m = {"SEQUENTIAL": L.MODE_SEQUENTIAL, "PARALLEL": L.MODE_PARALLEL, "DEVICE": L.MODE_DEVICE}[mode]
+    data = golden_inputs["syn300k"] + golden_inputs["zeros300k"] + golden_inputs["random100k"]
+    for bid, sck, bck in ((4, True, True), (7, True, False), (5, False, True)):
+        sd = L.make_sd(bid, sck, bck)
+        r, frame = L.compress(data, sd, mode=m)
+        assert r == 0, L.result_to_string(r)
+        assert frame == oracle.compress_frame(data, oracle.params(bid, sck, bck)), (mode, bid)
+        r, out, _ = L.decompress(frame, len(data) + 64, mode=m)
+        assert r == 0 and out == data, (mode, bid, L.result_to_string(r))

@@ -1,0 +1,148 @@
+"""Pins the CPU oracle (oracle/) before anything is checked against it.
+
+Pins: golden fixtures from liblz4 1.9.3 / the lz4 1.9.3 CLI / python-xxhash
+(tests/golden/make_golden.py), the SURVEY.md App. F known answers (computed
+there by the reference build), and — where the image has it — liblz4 itself.
+"""
+import ctypes
+import os
+import random
+
+import pytest
+import xxhash
+
+import oracle
+from conftest import read_golden
+
+LIBLZ4 = "/lib/x86_64-linux-gnu/liblz4.so.1"
+
+
+def test_xxh32_matches_python_xxhash():
+    rnd = random.Random(5)
+    for n in [0, 1, 3, 4, 15, 16, 17, 31, 32, 33, 100, 1000, 65536, 100_003]:
+        b = bytes(rnd.randrange(256) for _ in range(n))
+        assert oracle.xxh32(b) == xxhash.xxh32(b, seed=0).intdigest(), n
+    assert oracle.xxh32(b"") == 0x02CC5D05
+
+
+def test_generator_known_answers():
+    seg0 = oracle.gen_synthetic(65536)
+    assert oracle.xxh32(seg0) == 0x3069E8CC                        # App. F segment 0
+    assert oracle.xxh32(oracle.gen_synthetic(8 << 20)) == 0xD89F562C  # App. F first 8 MiB
+
+
+def test_blocks_vs_golden(golden, golden_inputs):
+    import hashlib
+    for v in golden["blocks"]:
+        data = golden_inputs[v["input"]][:v["n"]]
+        c = oracle.compress_block(data, v["cap"])
+        assert len(c) == v["ret"], v
+        assert hashlib.sha1(c).hexdigest() == v["sha1"], v
+
+
+def test_decode_vectors_vs_golden(golden, decode_blob):
+    for v in golden["decode"]:
+        blk = decode_blob[v["off"]:v["off"] + v["len"]]
+        r, out = oracle.decompress_block(blk, v["cap"])
+        assert r == v["ret"], v
+        if r >= 0:
+            assert xxhash.xxh32(out).intdigest() == v["out_xxh32"]
+
+
+def test_crafted_decode_vectors(golden):
+    for v in golden["crafted"]:
+        r, out = oracle.decompress_block(bytes.fromhex(v["block_hex"]), v["cap"])
+        assert r == v["ret"], v
+        if r >= 0:
+            assert xxhash.xxh32(out).intdigest() == v["out_xxh32"], v
+
+
+def test_frames_vs_golden(golden, golden_inputs):
+    for f in golden["frames"]:
+        data = golden_inputs[f["input"]]
+        p = oracle.params(f["bid"], f["stream_checksum"], f["block_checksum"])
+        got = oracle.compress_frame(data, p)
+        assert got == read_golden(f["file"]), f["file"]
+        r, out = oracle.decompress_frame(got, len(data) + (4 << 20))
+        assert r == 0 and out == data, f["file"]
+
+
+def test_empty_frame_bytes():
+    # empty input -> 04224d186470b9 00000000 055dcc02
+    assert oracle.compress_frame(b"").hex() == "04224d186470b900000000055dcc02"
+
+
+def test_frame_decode_error_codes(golden_inputs):
+    data = golden_inputs["syn300k"]
+    f = oracle.compress_frame(data, oracle.params(5, True, True))
+    cap = len(data) + (1 << 20)
+    assert oracle.decompress_frame(f, cap)[0] == 0
+    assert oracle.decompress_frame(b"\x01\x02\x03\x04rest", cap)[0] == 2        # INVALID_MAGIC_NUMBER
+    bad = bytearray(f); bad[6] ^= 1
+    assert oracle.decompress_frame(bytes(bad), cap)[0] == 7                     # INVALID_HEADER_CHECKSUM
+    bad = bytearray(f); bad[4] = (bad[4] & 0x3F)
+    assert oracle.decompress_frame(bytes(bad), cap)[0] == 6                     # INVALID_VERSION
+    bad = bytearray(f); bad[20] ^= 0xFF
+    assert oracle.decompress_frame(bytes(bad), cap)[0] in (16, 18)              # checksum / decode fail
+    assert oracle.decompress_frame(f[:-2], cap)[0] == 15                        # CANNOT_READ_STREAM_CHECKSUM
+    assert oracle.decompress_frame(f[:100], cap)[0] == 13                       # CANNOT_READ_BLOCK_DATA
+    bad = bytearray(f); bad[-1] ^= 1
+    assert oracle.decompress_frame(bytes(bad), cap)[0] == 17                    # STREAM_CHECKSUM_MISMATCH
+    # concatenated + skippable frames, trailing garbage after a frame is OK
+    skip = (0x184D2A51).to_bytes(4, "little") + (5).to_bytes(4, "little") + b"12345"
+    r, out = oracle.decompress_frame(f + skip + f + b"junkjunk", 2 * cap)
+    assert r == 0 and out == data + data
+
+
+@pytest.mark.parametrize("row", [
+    ((1, 0, 7), 133159140, 0x157099A8), ((0, 0, 7), 133159136, 0x8AC5DBC8), ((1, 1, 7), 133159396, 0xC532D9D2),
+    ((0, 1, 7), 133159392, 0x1686045A), ((1, 0, 4), 131940148, 0xFC3A55A1), ((1, 0, 5), 136141814, 0xAF5572EC),
+    ((1, 0, 6), 133770948, 0x7D1BC1BA), ((0, 1, 4), 131956528, 0xAB492B3C), ((0, 1, 5), 136145906, 0xE62BB3AC),
+    ((0, 1, 6), 133771968, 0x535404A3)])
+def test_known_answers_256mib(row, synthetic_256):
+    (sc, bc, bid), size, h = row
+    f = oracle.compress_frame(synthetic_256, oracle.params(bid, bool(sc), bool(bc)), threads=8)
+    assert len(f) == size
+    assert oracle.xxh32(f) == h
+
+
+@pytest.fixture(scope="module")
+def synthetic_256():
+    d = oracle.gen_synthetic(256 << 20)
+    assert oracle.xxh32(d) == 0xE6F24EBA   # App. F
+    return d
+
+
+@pytest.mark.skipif(not os.path.exists(LIBLZ4), reason="liblz4 1.9.3 not in this image")
+def test_differential_vs_liblz4():
+    """Fuzz the restatement against the library lz4mt binds (not available on every box)."""
+    L = ctypes.CDLL(LIBLZ4)
+    assert L.LZ4_versionNumber() == 10903
+    rnd = random.Random(11)
+    syn = oracle.gen_synthetic(1 << 20)
+    for t in range(120):
+        n = rnd.choice([0, 5, 12, 13, 64, 999, 4096, 65535, 65546, 65547, 65548, 70000, 200_000])
+        kind = t % 4
+        if kind == 0:
+            d = syn[rnd.randrange(0, len(syn) - n + 1):][:n]
+        elif kind == 1:
+            d = bytes(rnd.randrange(4) for _ in range(n))
+        elif kind == 2:
+            d = os.urandom(n)
+        else:
+            d = (bytes(rnd.randrange(256) for _ in range(rnd.randrange(1, 40))) * (n + 1))[:n]
+        assert len(d) == n
+        for cap in (n, max(n - 1, 0), n + n // 255 + 16):
+            dst = ctypes.create_string_buffer(max(cap, 1) + 64)
+            r = L.LZ4_compress_default(d, dst, n, cap)
+            assert oracle.compress_block(d, cap) == dst.raw[:r], (t, n, cap)
+        blk = dst.raw[:r]
+        for _ in range(10):
+            m = bytearray(blk)
+            if m:
+                m[rnd.randrange(len(m))] = rnd.randrange(256)
+            cap = rnd.choice([n, n + 20, 65536, 4 << 20])
+            o = ctypes.create_string_buffer(cap + 64)
+            want = L.LZ4_decompress_safe(bytes(m), o, len(m), cap)
+            got, out = oracle.decompress_block(bytes(m), cap)
+            assert got == want and (got < 0 or out == o.raw[:got])
