@@ -90,6 +90,15 @@ int lz4mtHipDeviceCount(void);
 void lz4mtHipSetTiming(int enable);
 int lz4mtHipGetTimings(float* ms4);
 
+/* ---- 4. diagnostics ----------------------------------------------------- */
+/* Runs s_memtime-stamped twins of the encode / decode kernels (never the
+ * product launch) and sums per-phase shader cycles over all blocks.
+ * encode: [hash, table+dedup, verify+table writes, catch-up, count, emit,
+ * windows, loop overhead]; decode: [parse, literal copy, ring match copy,
+ * HBM match copy, -, total, matches, HBM matches]. */
+int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* stats8, void* stream);
+int lz4mtHipDebugDecodeStats(const void* d_frame, uint64_t frameSize, uint64_t* stats8, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

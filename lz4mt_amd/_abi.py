@@ -104,6 +104,8 @@ PROTOTYPES = {
     "lz4mtHipDeviceCount": (c_int, []),
     "lz4mtHipSetTiming": (None, [c_int]),
     "lz4mtHipGetTimings": (c_int, [ctypes.POINTER(c_float)]),
+    "lz4mtHipDebugEncodeStats": (c_int, [c_void_p, c_uint64, c_uint32, ctypes.POINTER(c_uint64), c_void_p]),
+    "lz4mtHipDebugDecodeStats": (c_int, [c_void_p, c_uint64, ctypes.POINTER(c_uint64), c_void_p]),
     # lz4mt_io.h
     "lz4mtIoOpenIstream": (c_int, [CTX_P, c_char_p]),
     "lz4mtIoOpenOstream": (c_int, [CTX_P, c_char_p, c_int]),

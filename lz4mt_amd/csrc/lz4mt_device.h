@@ -59,6 +59,10 @@ hipError_t launch_frame_walk(const uint8_t* frame, uint64_t frameSize, uint64_t 
                              hipStream_t st);
 hipError_t launch_block_verify(const BlockRec* recs, uint32_t nBlocks, const uint32_t* digest, const int32_t* dsize,
                                uint32_t blockMax, int blockChecksum, int32_t* status, hipStream_t st);
+hipError_t launch_encode_stats(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                               uint8_t* slots, int32_t* csize, uint64_t* stats, hipStream_t st);
+hipError_t launch_decode_stats(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax,
+                               uint8_t* out, uint64_t outCap, int32_t* dsize, uint64_t* stats, hipStream_t st);
 hipError_t launch_gen_synthetic(uint8_t* dst, uint64_t n, uint64_t seed, hipStream_t st);
 
 }  // namespace lz4mt

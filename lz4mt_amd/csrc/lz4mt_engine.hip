@@ -526,3 +526,68 @@ extern "C" int lz4mtHipGetTimings(float* ms4) {
     ms4[0] = a; ms4[1] = b; ms4[2] = c; ms4[3] = d;
     return 0;
 }
+
+// ===========================================================================
+// 4. diagnostics: phase cycle counts of the encode / decode kernels
+// ===========================================================================
+extern "C" int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* stats8,
+                                        void* stream) {
+    if (!have_device() || blockSize == 0) return -1;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint64_t nb = (n + blockSize - 1) / blockSize;
+    uint8_t* slots = nullptr;
+    int32_t* cs = nullptr;
+    uint64_t* dst = nullptr;
+    int rc = -1;
+    if (hipMalloc(reinterpret_cast<void**>(&slots), nb * blockSize + 64) == hipSuccess &&
+        hipMalloc(reinterpret_cast<void**>(&cs), nb * 4 + 4) == hipSuccess &&
+        hipMalloc(reinterpret_cast<void**>(&dst), nb * 64 + 64) == hipSuccess &&
+        launch_encode_stats(static_cast<const uint8_t*>(d_src), n, blockSize, (uint32_t)nb, slots, cs, dst, st) ==
+            hipSuccess) {
+        std::vector<uint64_t> h(nb * 8);
+        if (hipMemcpyAsync(h.data(), dst, nb * 64, hipMemcpyDeviceToHost, st) == hipSuccess &&
+            hipStreamSynchronize(st) == hipSuccess) {
+            for (int i = 0; i < 8; ++i) stats8[i] = 0;
+            for (uint64_t b = 0; b < nb; ++b)
+                for (int i = 0; i < 8; ++i) stats8[i] += h[b * 8 + i];
+            rc = 0;
+        }
+    }
+    hipFree(slots); hipFree(cs); hipFree(dst);
+    return rc;
+}
+
+extern "C" int lz4mtHipDebugDecodeStats(const void* d_frame, uint64_t frameSize, uint64_t* stats8, void* stream) {
+    if (!have_device()) return -1;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint8_t* f = static_cast<const uint8_t*>(d_frame);
+    uint8_t h[kMaxHeader + 8] = {0};
+    const uint64_t avail = std::min<uint64_t>(sizeof(h), frameSize);
+    if (hipMemcpyAsync(h, f, avail, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+        return -1;
+    Lz4MtStreamDescriptor sd;
+    int hb = 0;
+    if (get32(h) != kMagic || parse_header(h + 4, avail - 4, &sd, &hb) != LZ4MT_RESULT_OK) return -1;
+    const uint32_t bm = (uint32_t)block_max_bytes(sd.bd.blockMaximumSize);
+    DecodeBuffers B;
+    WalkInfo wi{};
+    if (walk_frame(f, frameSize, 4 + hb, bm, sd.flg.blockChecksum, B, wi, st) != LZ4MT_RESULT_OK) return -1;
+    uint8_t* out = nullptr;
+    uint64_t* dst = nullptr;
+    int rc = -1;
+    const uint64_t nb = wi.nBlocks;
+    if (hipMalloc(reinterpret_cast<void**>(&out), nb * bm + 64) == hipSuccess &&
+        hipMalloc(reinterpret_cast<void**>(&dst), nb * 64 + 64) == hipSuccess &&
+        launch_decode_stats(f, B.recs, (uint32_t)nb, bm, out, nb * bm, B.dsize, dst, st) == hipSuccess) {
+        std::vector<uint64_t> hs(nb * 8);
+        if (hipMemcpyAsync(hs.data(), dst, nb * 64, hipMemcpyDeviceToHost, st) == hipSuccess &&
+            hipStreamSynchronize(st) == hipSuccess) {
+            for (int i = 0; i < 8; ++i) stats8[i] = 0;
+            for (uint64_t b = 0; b < nb; ++b)
+                for (int i = 0; i < 8; ++i) stats8[i] += hs[b * 8 + i];
+            rc = 0;
+        }
+    }
+    hipFree(out); hipFree(dst);
+    return rc;
+}

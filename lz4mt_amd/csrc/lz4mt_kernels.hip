@@ -118,10 +118,23 @@ __device__ __forceinline__ void emit_seq(const uint8_t* __restrict__ s, uint8_t*
     }
 }
 
-template <bool U16>
+// Diagnostic stamps (separate kernels, never in the product launch):
+// accumulate s_memtime deltas per phase into uniform registers.
+#define STAMP_T() (ST ? (uint64_t)__builtin_amdgcn_s_memtime() : 0ull)
+#define STAMP_ADD(i, t0)                          \
+    do {                                          \
+        if (ST) {                                 \
+            const uint64_t t1_ = STAMP_T();       \
+            acc[i] += t1_ - (t0);                 \
+            t0 = t1_;                             \
+        }                                         \
+    } while (0)
+
+template <bool U16, bool ST>
 __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8_t* __restrict__ d, uint32_t cap,
-                                uint32_t* __restrict__ Traw, uint8_t* __restrict__ S) {
+                                uint32_t* __restrict__ Traw, uint8_t* __restrict__ S, uint64_t* acc) {
     const uint32_t L = laneid();
+    uint64_t ts = STAMP_T();
     const uint32_t bound = n + n / 255 + 16;
     const bool limited = cap < bound;
     if (n == 0) {
@@ -146,6 +159,8 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
         Win W{1, 0, 0, 0, 1, 0};  // T[h(0)] = 0; search from ip = 1
         for (;;) {
             // ---------------- one probe window ----------------
+            if (ST) acc[6] += 1;
+            STAMP_ADD(7, ts);
             const uint32_t ns = W.hasIns + W.hasTest;
             const bool isIns = L < W.hasIns;
             const bool isTest = !isIns && L < ns;
@@ -164,6 +179,7 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
                 w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
             }
             const uint32_t h = live ? lz4_hash<U16>(w0, w1) : 0u;
+            STAMP_ADD(0, ts);
             // duplicate-hash detection inside the window (S is scratch; any
             // aliasing only costs an extra group iteration)
             S[h & 4095] = (uint8_t)L;
@@ -185,6 +201,7 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
                 pending &= ~m;
             }
             const uint32_t cand = pred >= 0 ? W.pos((uint32_t)pred) : told;
+            STAMP_ADD(1, ts);
             bool ok = false;
             if (live && !isIns && !term) {
                 const bool distok = U16 || (cand + kDistMax >= p);
@@ -202,6 +219,7 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
                 }
             }
             WAVE_SYNC();
+            STAMP_ADD(2, ts);
             if (w == 64) {  // no stop: continue the search
                 W.k0 += 64 - ns;
                 W.hasIns = 0; W.hasTest = 0;
@@ -226,6 +244,7 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
                 }
                 ip -= back; cd -= back;
             }
+            STAMP_ADD(3, ts);
             // forward extension (LZ4_count up to matchlimit)
             uint32_t mc = 0;
             {
@@ -247,6 +266,7 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
                     mc += 256;
                 }
             }
+            STAMP_ADD(4, ts);
             const uint32_t lit = ip - anchor;
             if (limited) {
                 if (!wasTest && op + 1 + lit + 8 + lit / 255 > cap) return 0;
@@ -259,6 +279,7 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
                 const uint32_t mlExt = mc >= 15 ? (mc - 15) / 255 + 1 : 0;
                 op += 1 + litExt + lit + 2 + mlExt;
             }
+            STAMP_ADD(5, ts);
             ip += mc + kMinMatch;
             anchor = ip;
             if (ip >= mflimitP1) goto last_literals;
@@ -287,9 +308,29 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
     const uint8_t* s = src + off;
     uint8_t* d = slots + (uint64_t)b * slotStride;
     int32_t r;
-    if (n < (uint32_t)kLimit64K) r = encode_block<true>(s, n, d, cap, T, S);
-    else r = encode_block<false>(s, n, d, cap, T, S);
+    if (n < (uint32_t)kLimit64K) r = encode_block<true, false>(s, n, d, cap, T, S, nullptr);
+    else r = encode_block<false, false>(s, n, d, cap, T, S, nullptr);
     if (laneid() == 0) csize[b] = r;
+}
+
+// diagnostic twin of k_encode: per-block phase cycle counts in stats[b*8 .. +8]
+__global__ void __launch_bounds__(64) k_encode_stats(const uint8_t* __restrict__ src, uint64_t srcSize,
+                                                     uint32_t blockSize, uint8_t* __restrict__ slots,
+                                                     uint64_t slotStride, int32_t* __restrict__ csize,
+                                                     uint64_t* __restrict__ stats) {
+    __shared__ __attribute__((aligned(16))) uint32_t T[4096];
+    __shared__ __attribute__((aligned(16))) uint8_t S[4096];
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
+    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int32_t r;
+    if (n < (uint32_t)kLimit64K) r = encode_block<true, true>(src + off, n, slots + b * slotStride, n, T, S, acc);
+    else r = encode_block<false, true>(src + off, n, slots + b * slotStride, n, T, S, acc);
+    if (laneid() == 0) {
+        csize[b] = r;
+        for (int i = 0; i < 8; ++i) stats[b * 8 + i] = acc[i];
+    }
 }
 
 hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks, uint8_t* slots,
@@ -307,7 +348,10 @@ constexpr int32_t kRing = 16384;   // LDS history ring (bytes)
 constexpr int32_t kInWin = 2048;   // LDS input window (bytes)
 constexpr int32_t kFlush = 1024;   // ring -> HBM flush granule (64 lanes x 16 B)
 
+template <bool ST>
 struct Dec {
+    uint64_t* acc;
+    uint64_t ts;
     const uint8_t* src;   // compressed block
     int64_t len;
     uint8_t* dst;         // block's output slot (16-B aligned)
@@ -356,6 +400,7 @@ struct Dec {
         flushed = op;
     }
     __device__ __forceinline__ void copy_lit(int64_t ip, int64_t op, int64_t n) {
+        STAMP_ADD(0, ts);
         const uint32_t L = laneid();
         const bool inWin = ip >= wlo && ip + n <= wlo + kInWin;
         for (int64_t c = 0; c < n; c += 64) {
@@ -367,8 +412,11 @@ struct Dec {
             }
             WAVE_SYNC();
         }
+        STAMP_ADD(1, ts);
     }
     __device__ __forceinline__ void copy_match(int64_t op, uint32_t offset, int64_t n) {
+        STAMP_ADD(0, ts);
+        if (ST) { acc[6] += 1; acc[7] += (int64_t)offset > kRing ? 1 : 0; }
         const uint32_t L = laneid();
         // out[x] = out[op - offset + ((x - op) mod offset)]; offset 0 => zeros (LZ4 1.9.3)
         const uint32_t magic = (offset > 0 && offset < 64) ? (65536u + offset - 1) / offset : 0u;
@@ -394,6 +442,7 @@ struct Dec {
             }
             WAVE_SYNC();
         }
+        STAMP_ADD((int64_t)offset > kRing ? 3 : 2, ts);
     }
     // read_variable_length(); returns 0 ok, -1 initial error, -2 loop error
     __device__ __forceinline__ int rvl(int64_t& ip, int64_t lencheck, bool loopCheck, bool initialCheck,
@@ -413,7 +462,8 @@ struct Dec {
 
 // LZ4_decompress_safe (lz4 1.9.3, LZ4_FAST_DEC_LOOP=1): same accept/reject
 // decisions and return values as the oracle restatement (oracle/lz4_oracle.c).
-__device__ int32_t decode_block(Dec& D, int64_t cap) {
+template <bool ST>
+__device__ int32_t decode_block(Dec<ST>& D, int64_t cap) {
     const int64_t iend = D.len, oend = cap;
     const int64_t shortiend = iend - 16, shortoend = oend - 32;
     int64_t ip = 0, op = 0, cpy = 0, match = 0, length = 0, ext = 0;
@@ -569,7 +619,9 @@ __global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ frame
         if (len > physcap) res = kDecodeOutputTooSmall;
         else { copy_raw(frame + r.offset, out + slot, len); res = (int32_t)len; }
     } else {
-        Dec D;
+        Dec<false> D;
+        D.acc = nullptr;
+        D.ts = 0;
         D.src = frame + r.offset;
         D.len = len;
         D.dst = out + slot;
@@ -582,6 +634,51 @@ __global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ frame
         res = decode_block(D, (int64_t)blockMax);
     }
     if (laneid() == 0) dsize[b] = res;
+}
+
+__global__ void __launch_bounds__(64) k_decode_stats(const uint8_t* __restrict__ frame,
+                                                     const BlockRec* __restrict__ recs, uint32_t blockMax,
+                                                     uint8_t* __restrict__ out, uint64_t outCap,
+                                                     int32_t* __restrict__ dsize, uint64_t* __restrict__ stats) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kInWin];
+    const uint32_t b = blockIdx.x;
+    const BlockRec r = recs[b];
+    const uint64_t slot = (uint64_t)b * blockMax;
+    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    Dec<true> D;
+    D.acc = acc;
+    D.ts = t0;
+    D.src = frame + r.offset;
+    D.len = r.bits & 0x7FFFFFFFu;
+    D.dst = out + slot;
+    D.physcap = (int64_t)min<uint64_t>(blockMax, outCap - slot);
+    D.ring = ring;
+    D.win = win;
+    D.wlo = INT64_MIN / 4;
+    D.flushed = 0;
+    D.completed = 0;
+    const int32_t res = decode_block(D, (int64_t)blockMax);
+    acc[5] = __builtin_amdgcn_s_memtime() - t0;
+    if (laneid() == 0) {
+        dsize[b] = res;
+        for (int i = 0; i < 8; ++i) stats[b * 8 + i] = acc[i];
+    }
+}
+
+hipError_t launch_decode_stats(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax,
+                               uint8_t* out, uint64_t outCap, int32_t* dsize, uint64_t* stats, hipStream_t st) {
+    hipLaunchKernelGGL(k_decode_stats, dim3(nBlocks), dim3(64), 0, st, frame, recs, blockMax, out, outCap, dsize,
+                       stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_encode_stats(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                               uint8_t* slots, int32_t* csize, uint64_t* stats, hipStream_t st) {
+    hipLaunchKernelGGL(k_encode_stats, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots,
+                       (uint64_t)blockSize, csize, stats);
+    return hipGetLastError();
 }
 
 hipError_t launch_decode(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax, uint8_t* out,

@@ -1,0 +1,43 @@
+"""Per-phase cycle breakdown of the encode/decode kernels (diagnostic twins).
+
+usage: python tools/kstats.py [GiB] [block_id]
+"""
+import ctypes
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import lz4mt_amd as L  # noqa: E402
+
+gib = float(sys.argv[1]) if len(sys.argv) > 1 else 8.0
+bid = int(sys.argv[2]) if len(sys.argv) > 2 else 7
+bm = 1 << (8 + 2 * bid)
+n = int(gib * (1 << 30)) // bm * bm
+src = L.gen_synthetic(n)
+torch.cuda.synchronize()
+st = (ctypes.c_uint64 * 8)()
+t = time.time()
+assert L.lib.lz4mtHipDebugEncodeStats(ctypes.c_void_p(src.data_ptr()), n, bm, st, None) == 0
+wall = time.time() - t
+e = list(st)
+nb = n // bm
+names = ["hash", "table+dedup", "verify+twrite", "catchup", "count", "emit", "windows", "loop-ovh"]
+tot = sum(e[:6]) + e[7]
+print(f"ENCODE {gib} GiB B{bid}: wall {wall*1e3:.1f} ms, blocks {nb}, windows {e[6]}, cycles/block {tot/nb:.3e}")
+for i in (0, 1, 2, 3, 4, 5, 7):
+    print(f"  {names[i]:14s} {e[i]/tot*100:5.1f}%  {e[i]/max(e[6],1):8.1f} cyc/window")
+sd = L.make_sd(bid, False, True)
+fr = L.compress_frame(src, sd)
+torch.cuda.synchronize()
+t = time.time()
+assert L.lib.lz4mtHipDebugDecodeStats(ctypes.c_void_p(fr.data_ptr()), fr.numel(), st, None) == 0
+wall = time.time() - t
+d = list(st)
+print(f"DECODE: wall {wall*1e3:.1f} ms (incl. walk+alloc), total cycles/block {d[5]/nb:.3e}, matches {d[6]}, "
+      f"HBM matches {d[7]} ({d[7]/max(d[6],1)*100:.1f}%)")
+dn = ["parse", "literal copy", "ring match", "HBM match"]
+for i in range(4):
+    print(f"  {dn[i]:14s} {d[i]/d[5]*100:5.1f}%  {d[i]/max(d[6],1):8.1f} cyc/match")
