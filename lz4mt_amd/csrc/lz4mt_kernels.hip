@@ -53,6 +53,18 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 
+// Diagnostic stamps (separate kernels, never in the product launch):
+// accumulate s_memtime deltas per phase into uniform registers.
+#define STAMP_T() (ST ? (uint64_t)__builtin_amdgcn_s_memtime() : 0ull)
+#define STAMP_ADD(i, t0)                          \
+    do {                                          \
+        if (ST) {                                 \
+            const uint64_t t1_ = STAMP_T();       \
+            acc[i] += t1_ - (t0);                 \
+            t0 = t1_;                             \
+        }                                         \
+    } while (0)
+
 constexpr uint32_t kP1 = 2654435761u, kP2 = 2246822519u, kP3 = 3266489917u, kP4 = 668265263u, kP5 = 374761393u;
 
 // ---------------------------------------------------------------------------
@@ -88,51 +100,103 @@ struct Win {
     }
 };
 
-// Emits one sequence (or the final literal run when !hasMatch) with all
-// lanes, one output byte per lane per step.
-__device__ __forceinline__ void emit_seq(const uint8_t* __restrict__ s, uint8_t* __restrict__ d, uint32_t op,
-                                         uint32_t anchor, uint32_t lit, bool hasMatch, uint32_t off, uint32_t mc) {
+// Source view of one block: a 2 KiB LDS ring holding src[B, B + kRingE)
+// (B a multiple of 512, advanced as the parse moves) in front of global
+// memory.  Every read falls back to global for positions outside the ring,
+// so the ring only changes speed, never results.
+constexpr uint32_t kRingE = 2048;
+constexpr uint32_t kRingMaskW = kRingE / 4 - 1;   // ring index mask in dwords
+constexpr uint32_t kDedup = 1024;                 // duplicate-hash scratch entries
+
+struct SrcView {
+    const uint8_t* s;
+    uint32_t n;
+    uint32_t* ring;   // kRingE bytes
+    uint32_t B;
+
+    __device__ __forceinline__ void load_chunk(uint32_t c) {   // src[c, c+512) -> ring, c % 512 == 0
+        const uint32_t L = laneid();
+        const uint32_t pos = c + 8 * L;
+        uint32_t a = 0, b = 0;
+        if (pos < n) a = *reinterpret_cast<const uint32_t*>(s + pos);
+        if (pos + 4 < n) b = *reinterpret_cast<const uint32_t*>(s + pos + 4);
+        ring[((pos >> 2) + 0) & kRingMaskW] = a;
+        ring[((pos >> 2) + 1) & kRingMaskW] = b;
+    }
+    __device__ __forceinline__ void init() {
+        B = 0;
+        for (uint32_t c = 0; c < kRingE; c += 512) load_chunk(c);
+        WAVE_SYNC();
+    }
+    // make the ring end at or beyond `hi` (uniform)
+    __device__ __forceinline__ void cover(uint32_t hi) {
+        if (hi <= B + kRingE) return;
+        const uint32_t nb = (hi - kRingE + 511) & ~511u;
+        const uint32_t from = (nb >= B + kRingE) ? nb : B + kRingE;
+        WAVE_SYNC();
+        for (uint32_t c = from; c < nb + kRingE; c += 512) load_chunk(c);
+        B = nb;
+        WAVE_SYNC();
+    }
+    __device__ __forceinline__ bool in_ring(uint32_t pos, uint32_t len) const {
+        return pos >= B && pos + len <= B + kRingE;
+    }
+    __device__ __forceinline__ uint32_t rd4(uint32_t pos) const {   // bytes [pos, pos+4) little-endian
+        if (in_ring(pos, 4)) {
+            const uint32_t w = pos >> 2, sh = pos & 3;
+            const uint32_t lo = ring[w & kRingMaskW];
+            const uint32_t hi = sh ? ring[(w + 1) & kRingMaskW] : 0u;
+            return __builtin_amdgcn_alignbyte(hi, lo, sh);
+        }
+        return ld32u(s + pos);
+    }
+    __device__ __forceinline__ uint32_t rd1(uint32_t pos) const {
+        if (in_ring(pos, 1)) return (ring[(pos >> 2) & kRingMaskW] >> (8 * (pos & 3))) & 255u;
+        return s[pos];
+    }
+};
+
+// Emits one sequence (or the final literal run when !hasMatch): header bytes
+// (token + literal-length bytes), literals 4 per lane, then the offset and
+// match-length bytes.  Byte stores: the destination has no alignment.
+__device__ __forceinline__ void emit_seq(const SrcView& V, uint8_t* __restrict__ d, uint32_t op, uint32_t anchor,
+                                         uint32_t lit, bool hasMatch, uint32_t off, uint32_t mc) {
     const uint32_t L = laneid();
     const uint32_t litExt = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
     const uint32_t litRem = lit >= 15 ? (lit - 15) % 255 : 0;
     const uint32_t mlExt = (hasMatch && mc >= 15) ? (mc - 15) / 255 + 1 : 0;
     const uint32_t mlRem = mc >= 15 ? (mc - 15) % 255 : 0;
     const uint32_t token = ((lit < 15 ? lit : 15) << 4) | (hasMatch ? (mc < 15 ? mc : 15) : 0);
-    const uint32_t litEnd = 1 + litExt + lit;
-    const uint32_t total = litEnd + (hasMatch ? 2 + mlExt : 0);
-    for (uint32_t base = 0; base < total; base += 64) {
-        const uint32_t x = base + L;
-        if (x < total) {
+    const uint32_t head = 1 + litExt;
+    for (uint32_t x = L; x < head; x += 64) d[op + x] = (uint8_t)(x == 0 ? token : (x < litExt ? 255u : litRem));
+    uint8_t* dl = d + op + head;
+    for (uint32_t base = 0; base < lit; base += 256) {
+        const uint32_t i = base + 4 * L;
+        if (i < lit) {
+            const uint32_t v = V.rd4(anchor + i);   // may read past the run; only `lit` bytes are stored
+            dl[i] = (uint8_t)v;
+            if (i + 1 < lit) dl[i + 1] = (uint8_t)(v >> 8);
+            if (i + 2 < lit) dl[i + 2] = (uint8_t)(v >> 16);
+            if (i + 3 < lit) dl[i + 3] = (uint8_t)(v >> 24);
+        }
+    }
+    if (hasMatch) {
+        uint8_t* dt = dl + lit;
+        const uint32_t tail = 2 + mlExt;
+        for (uint32_t y = L; y < tail; y += 64) {
             uint32_t v;
-            if (x == 0) v = token;
-            else if (x <= litExt) v = (x < litExt) ? 255u : litRem;
-            else if (x < litEnd) v = s[anchor + (x - 1 - litExt)];
-            else {
-                const uint32_t y = x - litEnd;
-                if (y == 0) v = off & 255;
-                else if (y == 1) v = off >> 8;
-                else v = (y - 2 + 1 < mlExt) ? 255u : mlRem;
-            }
-            d[op + x] = (uint8_t)v;
+            if (y == 0) v = off & 255;
+            else if (y == 1) v = off >> 8;
+            else v = (y - 1 < mlExt) ? 255u : mlRem;
+            dt[y] = (uint8_t)v;
         }
     }
 }
 
-// Diagnostic stamps (separate kernels, never in the product launch):
-// accumulate s_memtime deltas per phase into uniform registers.
-#define STAMP_T() (ST ? (uint64_t)__builtin_amdgcn_s_memtime() : 0ull)
-#define STAMP_ADD(i, t0)                          \
-    do {                                          \
-        if (ST) {                                 \
-            const uint64_t t1_ = STAMP_T();       \
-            acc[i] += t1_ - (t0);                 \
-            t0 = t1_;                             \
-        }                                         \
-    } while (0)
-
 template <bool U16, bool ST>
 __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8_t* __restrict__ d, uint32_t cap,
-                                uint32_t* __restrict__ Traw, uint8_t* __restrict__ S, uint64_t* acc) {
+                                uint32_t* __restrict__ Traw, uint8_t* __restrict__ S, uint32_t* __restrict__ ringE,
+                                uint64_t* acc) {
     const uint32_t L = laneid();
     uint64_t ts = STAMP_T();
     const uint32_t bound = n + n / 255 + 16;
@@ -143,12 +207,12 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
         return 1;
     }
     uint16_t* T16 = reinterpret_cast<uint16_t*>(Traw);
-    // zero the 16 KiB table
     {
         uint4* T4 = reinterpret_cast<uint4*>(Traw);
         for (uint32_t i = L; i < 1024; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
     }
-    WAVE_SYNC();
+    SrcView V{s, n, ringE, 0};
+    V.init();
 
     const uint32_t mflimitP1 = n - kMfLimit + 1;
     const uint32_t matchlimit = n - kLastLiterals;
@@ -169,23 +233,23 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
             const uint32_t p = W.pos(L);
             const bool live = !isSearch || p <= mflimitP1;
             const bool term = isSearch && live && (p + probe_step(k) > mflimitP1);
+            {
+                const uint32_t plast = W.pos(63);
+                V.cover((plast < mflimitP1 ? plast : mflimitP1) + 8);
+            }
             uint32_t w0 = 0, w1 = 0;
             if (live) {
-                const uint32_t* q = reinterpret_cast<const uint32_t*>(s + (p & ~3u));
-                const uint32_t sh = p & 3;
-                const uint32_t d0 = q[0], d1 = q[1];
-                const uint32_t d2 = sh ? q[2] : 0u;
-                w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-                w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                w0 = V.rd4(p);
+                if (!U16) w1 = V.rd4(p + 4);
             }
             const uint32_t h = live ? lz4_hash<U16>(w0, w1) : 0u;
             STAMP_ADD(0, ts);
-            // duplicate-hash detection inside the window (S is scratch; any
-            // aliasing only costs an extra group iteration)
-            S[h & 4095] = (uint8_t)L;
+            // duplicate-hash detection inside the window (aliasing of the
+            // scratch index only costs an extra group iteration)
+            S[h & (kDedup - 1)] = (uint8_t)L;
             const uint32_t told = U16 ? (uint32_t)T16[h] : Traw[h];
             WAVE_SYNC();
-            const uint32_t sv = S[h & 4095];
+            const uint32_t sv = S[h & (kDedup - 1)];
             uint64_t pending = ballot(live && sv != L);
             int pred = -1;
             uint64_t gmask = 1ull << L;
@@ -205,7 +269,7 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
             bool ok = false;
             if (live && !isIns && !term) {
                 const bool distok = U16 || (cand + kDistMax >= p);
-                if (distok) ok = (ld32u(s + cand) == w0);
+                if (distok) ok = (V.rd4(cand) == w0);
             }
             const uint64_t sm = ballot(live && (term || ok));
             const int w = sm ? __ffsll((long long)sm) - 1 : 64;
@@ -228,79 +292,86 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
             if (wTerm) goto last_literals;
 
             // ---------------- match found ----------------
-            uint32_t ip = rdlane(p, w);
-            uint32_t cd = rdlane(cand, w);
+            const uint32_t ip = rdlane(p, w);
+            const uint32_t cd = rdlane(cand, w);
             const bool wasTest = (ballot(isTest) >> w) & 1;
-            if (!wasTest) {  // catch up (LZ4: while ip>anchor && match>base && ip[-1]==match[-1])
-                const uint32_t maxb = min(ip - anchor, cd);
-                uint32_t back = 0;
-                while (back < maxb) {
-                    const uint32_t kk = back + L + 1;
-                    bool eq = false;
-                    if (kk <= maxb) eq = s[ip - kk] == s[cd - kk];
-                    const uint64_t fm = ballot(!eq);
-                    if (fm) { back += (uint32_t)(__ffsll((long long)fm) - 1); break; }
-                    back += 64;
+            // Catch-up and forward count in one round: with back = catch-up
+            // length, LZ4_count from the caught-up position equals
+            // back + count from ip+4 (the skipped bytes are known equal).
+            const uint32_t maxb = wasTest ? 0u : min(ip - anchor, cd);
+            const uint32_t lim = matchlimit - (ip + kMinMatch);
+            V.cover(min(ip + kMinMatch + 256, n));
+            uint32_t back = 0, mc = 0;
+            bool backDone = maxb == 0, cntDone = false;
+            while (!(backDone && cntDone)) {
+                bool beq = false;
+                uint32_t eqb = 0;
+                const uint32_t kk = back + L + 1;
+                if (!backDone && kk <= maxb) beq = V.rd1(ip - kk) == V.rd1(cd - kk);
+                const uint32_t rel = mc + 4 * L;
+                if (!cntDone && rel < lim) {
+                    const uint32_t x = V.rd4(ip + kMinMatch + rel) ^ V.rd4(cd + kMinMatch + rel);
+                    eqb = x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u;
+                    eqb = min(eqb, lim - rel);
                 }
-                ip -= back; cd -= back;
-            }
-            STAMP_ADD(3, ts);
-            // forward extension (LZ4_count up to matchlimit)
-            uint32_t mc = 0;
-            {
-                const uint32_t lim = matchlimit - (ip + kMinMatch);
-                for (;;) {
-                    const uint32_t rel = mc + 4 * L;
-                    uint32_t eqb = 0;
-                    if (rel < lim) {
-                        const uint32_t x = ld32u(s + ip + kMinMatch + rel) ^ ld32u(s + cd + kMinMatch + rel);
-                        eqb = x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u;
-                        eqb = min(eqb, lim - rel);
-                    }
+                if (!backDone) {
+                    const uint64_t fm = ballot(!beq);
+                    if (fm) { back += (uint32_t)(__ffsll((long long)fm) - 1); backDone = true; }
+                    else { back += 64; backDone = back >= maxb; }
+                }
+                if (!cntDone) {
                     const uint64_t nf = ballot(eqb < 4);
                     if (nf) {
                         const int f = __ffsll((long long)nf) - 1;
                         mc += 4 * (uint32_t)f + rdlane(eqb, f);
-                        break;
+                        cntDone = true;
+                    } else {
+                        mc += 256;
                     }
-                    mc += 256;
                 }
             }
+            STAMP_ADD(3, ts);
+            const uint32_t ipm = ip - back;          // caught-up match start
+            const uint32_t mcf = mc + back;          // LZ4_count from ipm + 4
+            const uint32_t lit = ipm - anchor;
             STAMP_ADD(4, ts);
-            const uint32_t lit = ip - anchor;
             if (limited) {
                 if (!wasTest && op + 1 + lit + 8 + lit / 255 > cap) return 0;
                 const uint32_t litExt = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
-                if (op + 1 + litExt + lit + 2 + 6 + (mc + 240) / 255 > cap) return 0;
+                if (op + 1 + litExt + lit + 2 + 6 + (mcf + 240) / 255 > cap) return 0;
             }
-            emit_seq(s, d, op, anchor, lit, true, ip - cd, mc);
+            emit_seq(V, d, op, anchor, lit, true, ip - cd, mcf);
             {
                 const uint32_t litExt = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
-                const uint32_t mlExt = mc >= 15 ? (mc - 15) / 255 + 1 : 0;
+                const uint32_t mlExt = mcf >= 15 ? (mcf - 15) / 255 + 1 : 0;
                 op += 1 + litExt + lit + 2 + mlExt;
             }
             STAMP_ADD(5, ts);
-            ip += mc + kMinMatch;
-            anchor = ip;
-            if (ip >= mflimitP1) goto last_literals;
-            W = Win{1, 1, ip - 2, ip, ip + 1, 0};
+            const uint32_t ipe = ip + kMinMatch + mc;  // = ipm + mcf + 4
+            anchor = ipe;
+            if (ipe >= mflimitP1) goto last_literals;
+            W = Win{1, 1, ipe - 2, ipe, ipe + 1, 0};
         }
     }
 last_literals : {
     const uint32_t run = n - anchor;
     if (limited && op + run + 1 + (run + 240) / 255 > cap) return 0;
-    emit_seq(s, d, op, anchor, run, false, 0, 0);
+    emit_seq(V, d, op, anchor, run, false, 0, 0);
     const uint32_t ext = run >= 15 ? (run - 15) / 255 + 1 : 0;
     op += 1 + ext + run;
 }
     return (int32_t)op;
 }
 
+#define ENCODE_LDS                                                        \
+    __shared__ __attribute__((aligned(16))) uint32_t T[4096];   /* 16 KiB */ \
+    __shared__ __attribute__((aligned(16))) uint32_t R[kRingE / 4]; /* 2 KiB */ \
+    __shared__ __attribute__((aligned(16))) uint8_t S[kDedup];  /* 1 KiB */
+
 __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, uint64_t srcSize, uint32_t blockSize,
                                                uint8_t* __restrict__ slots, uint64_t slotStride,
                                                uint32_t capOverride, int32_t* __restrict__ csize) {
-    __shared__ __attribute__((aligned(16))) uint32_t T[4096];  // 16 KiB: u32[4096] or u16[8192]
-    __shared__ __attribute__((aligned(16))) uint8_t S[4096];   // duplicate-hash scratch
+    ENCODE_LDS
     const uint32_t b = blockIdx.x;
     const uint64_t off = (uint64_t)b * blockSize;
     const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
@@ -308,8 +379,8 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
     const uint8_t* s = src + off;
     uint8_t* d = slots + (uint64_t)b * slotStride;
     int32_t r;
-    if (n < (uint32_t)kLimit64K) r = encode_block<true, false>(s, n, d, cap, T, S, nullptr);
-    else r = encode_block<false, false>(s, n, d, cap, T, S, nullptr);
+    if (n < (uint32_t)kLimit64K) r = encode_block<true, false>(s, n, d, cap, T, S, R, nullptr);
+    else r = encode_block<false, false>(s, n, d, cap, T, S, R, nullptr);
     if (laneid() == 0) csize[b] = r;
 }
 
@@ -318,15 +389,14 @@ __global__ void __launch_bounds__(64) k_encode_stats(const uint8_t* __restrict__
                                                      uint32_t blockSize, uint8_t* __restrict__ slots,
                                                      uint64_t slotStride, int32_t* __restrict__ csize,
                                                      uint64_t* __restrict__ stats) {
-    __shared__ __attribute__((aligned(16))) uint32_t T[4096];
-    __shared__ __attribute__((aligned(16))) uint8_t S[4096];
+    ENCODE_LDS
     const uint32_t b = blockIdx.x;
     const uint64_t off = (uint64_t)b * blockSize;
     const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
     uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int32_t r;
-    if (n < (uint32_t)kLimit64K) r = encode_block<true, true>(src + off, n, slots + b * slotStride, n, T, S, acc);
-    else r = encode_block<false, true>(src + off, n, slots + b * slotStride, n, T, S, acc);
+    if (n < (uint32_t)kLimit64K) r = encode_block<true, true>(src + off, n, slots + b * slotStride, n, T, S, R, acc);
+    else r = encode_block<false, true>(src + off, n, slots + b * slotStride, n, T, S, R, acc);
     if (laneid() == 0) {
         csize[b] = r;
         for (int i = 0; i < 8; ++i) stats[b * 8 + i] = acc[i];
@@ -693,24 +763,54 @@ hipError_t launch_decode(const uint8_t* frame, const BlockRec* recs, uint32_t nB
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t xround(uint32_t acc, uint32_t w) { return rotl32(acc + w * kP2, 13) * kP1; }
 
-// All 4 lanes of a quad call this with the same (p, len); lane c = quad lane.
-__device__ uint32_t xxh32_quad(const uint8_t* p, uint64_t len, uint32_t c, uint32_t quadBase) {
-    uint32_t v = (c == 0) ? kP1 + kP2 : (c == 1) ? kP2 : (c == 2) ? 0u : (uint32_t)(0u - kP1);
-    const uint64_t ns = len >> 4;
-    uint64_t i = 0;
-    for (; i + 8 <= ns; i += 8) {
-        uint32_t w[8];
+// One wavefront hashes one byte range: the range streams through LDS in
+// 1 KiB chunks (64 lanes x 16 B, loaded one chunk ahead), lanes 0..3 run
+// the four accumulator chains (v1..v4 of XXH32) over each chunk.
+__device__ __forceinline__ uint4 load16u(const uint8_t* p) {   // 16 bytes at any alignment
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+    const uint32_t a4 = sh ? q[4] : 0u;
+    uint4 v;
+    v.x = __builtin_amdgcn_alignbyte(a1, a0, sh);
+    v.y = __builtin_amdgcn_alignbyte(a2, a1, sh);
+    v.z = __builtin_amdgcn_alignbyte(a3, a2, sh);
+    v.w = __builtin_amdgcn_alignbyte(a4, a3, sh);
+    return v;
+}
+
+__device__ uint32_t xxh32_wave(const uint8_t* p, uint64_t len, uint32_t* __restrict__ buf /* 512 dwords */) {
+    const uint32_t L = laneid();
+    uint32_t v = (L == 0) ? kP1 + kP2 : (L == 1) ? kP2 : (L == 2) ? 0u : (uint32_t)(0u - kP1);
+    const uint64_t ns = len >> 4;            // whole 16-byte stripes
+    const uint64_t nch = (ns + 63) >> 6;     // 1 KiB chunks
+    uint4 r = make_uint4(0, 0, 0, 0);
+    if (nch && (uint64_t)L < ns) r = load16u(p + 16 * L);
+    uint32_t cur = 0;
+    for (uint64_t ch = 0; ch < nch; ++ch) {
+        reinterpret_cast<uint4*>(buf + cur * 256)[L] = r;
+        const uint64_t nxt = (ch + 1) * 64 + L;
+        if (ch + 1 < nch && nxt < ns) r = load16u(p + 16 * nxt);
+        WAVE_SYNC();
+        if (L < 4) {
+            const uint32_t m = (uint32_t)min<uint64_t>(64, ns - ch * 64);
+            const uint32_t* cb = buf + cur * 256 + L;
+            uint32_t i = 0;
+            for (; i + 8 <= m; i += 8) {
+                uint32_t w[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) w[u] = ld32u(p + 16 * (i + u) + 4 * c);
+                for (int u = 0; u < 8; ++u) w[u] = cb[4 * (i + u)];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v = xround(v, w[u]);
+                for (int u = 0; u < 8; ++u) v = xround(v, w[u]);
+            }
+            for (; i < m; ++i) v = xround(v, cb[4 * i]);
+        }
+        WAVE_SYNC();
+        cur ^= 1;
     }
-    for (; i < ns; ++i) v = xround(v, ld32u(p + 16 * i + 4 * c));
-    const uint32_t v1 = __shfl(v, quadBase + 0), v2 = __shfl(v, quadBase + 1);
-    const uint32_t v3 = __shfl(v, quadBase + 2), v4 = __shfl(v, quadBase + 3);
-    uint32_t h;
-    if (len >= 16) h = rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18);
-    else h = kP5;
+    const uint32_t v1 = rdlane(v, 0), v2 = rdlane(v, 1), v3 = rdlane(v, 2), v4 = rdlane(v, 3);
+    uint32_t h = len >= 16 ? rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18) : kP5;
     h += (uint32_t)len;
     uint64_t o = ns << 4;
     for (; o + 4 <= len; o += 4) h = rotl32(h + ld32u(p + o) * kP3, 17) * kP4;
@@ -720,58 +820,48 @@ __device__ uint32_t xxh32_quad(const uint8_t* p, uint64_t len, uint32_t c, uint3
 }
 
 // stored bytes of compress-side block b: the slot if it compressed, else the source
-__global__ void __launch_bounds__(256) k_xxh32_stored(const uint8_t* __restrict__ src, const uint8_t* __restrict__ slots,
-                                                      uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
-                                                      const int32_t* __restrict__ csize, uint32_t* __restrict__ digest) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t b = t >> 2, c = t & 3;
-    const uint32_t quadBase = laneid() & ~3u;
-    const bool valid = b < nBlocks;
-    const uint32_t bb = valid ? b : nBlocks - 1;
-    const uint64_t off = (uint64_t)bb * blockSize;
+__global__ void __launch_bounds__(64) k_xxh32_stored(const uint8_t* __restrict__ src, const uint8_t* __restrict__ slots,
+                                                     uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                                                     const int32_t* __restrict__ csize, uint32_t* __restrict__ digest) {
+    __shared__ __attribute__((aligned(16))) uint32_t buf[512];
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = (uint64_t)b * blockSize;
     const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
-    const int32_t cs = csize[bb];
-    const uint8_t* p = cs > 0 ? slots + off : src + off;
-    const uint64_t len = cs > 0 ? (uint64_t)cs : n;
-    const uint32_t h = xxh32_quad(p, len, c, quadBase);
-    if (valid && c == 0) digest[b] = h;
+    const int32_t cs = csize[b];
+    const uint32_t h = xxh32_wave(cs > 0 ? slots + off : src + off, cs > 0 ? (uint64_t)cs : n, buf);
+    if (laneid() == 0) digest[b] = h;
 }
 
-__global__ void __launch_bounds__(256) k_xxh32_frame_blocks(const uint8_t* __restrict__ frame,
-                                                            const BlockRec* __restrict__ recs, uint32_t nBlocks,
-                                                            uint32_t* __restrict__ digest) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t b = t >> 2, c = t & 3;
-    const uint32_t quadBase = laneid() & ~3u;
-    const bool valid = b < nBlocks;
-    const BlockRec r = recs[valid ? b : nBlocks - 1];
-    const uint32_t h = xxh32_quad(frame + r.offset, r.bits & 0x7FFFFFFFu, c, quadBase);
-    if (valid && c == 0) digest[b] = h;
+__global__ void __launch_bounds__(64) k_xxh32_frame_blocks(const uint8_t* __restrict__ frame,
+                                                           const BlockRec* __restrict__ recs, uint32_t nBlocks,
+                                                           uint32_t* __restrict__ digest) {
+    __shared__ __attribute__((aligned(16))) uint32_t buf[512];
+    const uint32_t b = blockIdx.x;
+    const BlockRec r = recs[b];
+    const uint32_t h = xxh32_wave(frame + r.offset, r.bits & 0x7FFFFFFFu, buf);
+    if (laneid() == 0) digest[b] = h;
 }
 
-// whole-stream XXH32 (lz4mt's serial content checksum): ONE quad, by design
+// whole-stream XXH32 (lz4mt's serial content checksum): ONE wave, by design
 __global__ void __launch_bounds__(64) k_xxh32_stream(const uint8_t* __restrict__ p, uint64_t len,
                                                      uint32_t* __restrict__ digest) {
-    const uint32_t L = laneid();
-    const uint32_t h = xxh32_quad(p, len, L & 3, L & ~3u);
-    if (L == 0) *digest = h;
+    __shared__ __attribute__((aligned(16))) uint32_t buf[512];
+    const uint32_t h = xxh32_wave(p, len, buf);
+    if (laneid() == 0) *digest = h;
 }
 
 hipError_t launch_xxh32_stored(const uint8_t* src, const uint8_t* slots, uint64_t srcSize, uint32_t blockSize,
                                uint32_t nBlocks, const int32_t* csize, uint32_t* digest, hipStream_t st) {
     if (nBlocks == 0) return hipSuccess;
-    const uint32_t threads = nBlocks * 4;
-    hipLaunchKernelGGL(k_xxh32_stored, dim3((threads + 255) / 256), dim3(256), 0, st, src, slots, srcSize, blockSize,
-                       nBlocks, csize, digest);
+    hipLaunchKernelGGL(k_xxh32_stored, dim3(nBlocks), dim3(64), 0, st, src, slots, srcSize, blockSize, nBlocks, csize,
+                       digest);
     return hipGetLastError();
 }
 
 hipError_t launch_xxh32_frame_blocks(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t* digest,
                                      hipStream_t st) {
     if (nBlocks == 0) return hipSuccess;
-    const uint32_t threads = nBlocks * 4;
-    hipLaunchKernelGGL(k_xxh32_frame_blocks, dim3((threads + 255) / 256), dim3(256), 0, st, frame, recs, nBlocks,
-                       digest);
+    hipLaunchKernelGGL(k_xxh32_frame_blocks, dim3(nBlocks), dim3(64), 0, st, frame, recs, nBlocks, digest);
     return hipGetLastError();
 }
 
