@@ -173,7 +173,14 @@ __device__ __forceinline__ void emit_seq(const SrcView& V, uint8_t* __restrict__
     for (uint32_t base = 0; base < lit; base += 256) {
         const uint32_t i = base + 4 * L;
         if (i < lit) {
-            const uint32_t v = V.rd4(anchor + i);   // may read past the run; only `lit` bytes are stored
+            uint32_t v;
+            if (i + 4 <= lit) {
+                v = V.rd4(anchor + i);
+            } else {   // tail: never touch bytes past the run (the block may end the buffer)
+                v = V.rd1(anchor + i);
+                if (i + 1 < lit) v |= V.rd1(anchor + i + 1) << 8;
+                if (i + 2 < lit) v |= V.rd1(anchor + i + 2) << 16;
+            }
             dl[i] = (uint8_t)v;
             if (i + 1 < lit) dl[i + 1] = (uint8_t)(v >> 8);
             if (i + 2 < lit) dl[i + 2] = (uint8_t)(v >> 16);
@@ -441,8 +448,14 @@ struct Dec {
 #pragma unroll
         for (int h = 0; h < kInWin / 1024; ++h) {
             const uintptr_t a = base + (uintptr_t)(h * 1024 + 16 * L);
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (a < end) v = *reinterpret_cast<const uint4*>(a);
+            const uint32_t* q = reinterpret_cast<const uint32_t*>(a);
+            uint4 v = make_uint4(0, 0, 0, 0);   // dword-granular: never past the block's last dword
+            if (a + 12 < end) v = *reinterpret_cast<const uint4*>(a);
+            else {
+                if (a < end) v.x = q[0];
+                if (a + 4 < end) v.y = q[1];
+                if (a + 8 < end) v.z = q[2];
+            }
             *reinterpret_cast<uint4*>(win + h * 1024 + 16 * L) = v;
         }
         WAVE_SYNC();
