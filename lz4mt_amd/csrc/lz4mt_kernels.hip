@@ -103,39 +103,63 @@ struct Win {
 // Source view of one block: a 2 KiB LDS ring holding src[B, B + kRingE)
 // (B a multiple of 512, advanced as the parse moves) in front of global
 // memory.  Every read falls back to global for positions outside the ring,
-// so the ring only changes speed, never results.
+// so the ring only changes speed, never results.  The next 512-byte chunk
+// is prefetched into registers one advance ahead, so an advance normally
+// finds its data already landed.
 constexpr uint32_t kRingE = 2048;
 constexpr uint32_t kRingMaskW = kRingE / 4 - 1;   // ring index mask in dwords
 constexpr uint32_t kDedup = 1024;                 // duplicate-hash scratch entries
+constexpr uint32_t kOutRing = 1024;               // LDS staging of the compressed output
+constexpr uint32_t kOutFlush = 512;               // flush granule (64 lanes x 8 B)
 
 struct SrcView {
     const uint8_t* s;
     uint32_t n;
     uint32_t* ring;   // kRingE bytes
     uint32_t B;
+    uint32_t pfPos;   // position of the prefetched chunk in (pa, pb)
+    uint32_t pa, pb;
 
-    __device__ __forceinline__ void load_chunk(uint32_t c) {   // src[c, c+512) -> ring, c % 512 == 0
-        const uint32_t L = laneid();
-        const uint32_t pos = c + 8 * L;
-        uint32_t a = 0, b = 0;
+    __device__ __forceinline__ void fetch(uint32_t c, uint32_t& a, uint32_t& b) const {
+        const uint32_t pos = c + 8 * laneid();
+        a = 0; b = 0;
         if (pos < n) a = *reinterpret_cast<const uint32_t*>(s + pos);
         if (pos + 4 < n) b = *reinterpret_cast<const uint32_t*>(s + pos + 4);
-        ring[((pos >> 2) + 0) & kRingMaskW] = a;
-        ring[((pos >> 2) + 1) & kRingMaskW] = b;
+    }
+    __device__ __forceinline__ void store(uint32_t c, uint32_t a, uint32_t b) {
+        const uint32_t w = (c >> 2) + 2 * laneid();
+        ring[w & kRingMaskW] = a;
+        ring[(w + 1) & kRingMaskW] = b;
     }
     __device__ __forceinline__ void init() {
         B = 0;
-        for (uint32_t c = 0; c < kRingE; c += 512) load_chunk(c);
+        for (uint32_t c = 0; c < kRingE; c += 512) {
+            uint32_t a, b;
+            fetch(c, a, b);
+            store(c, a, b);
+        }
+        pfPos = kRingE;
+        fetch(pfPos, pa, pb);
         WAVE_SYNC();
     }
     // make the ring end at or beyond `hi` (uniform)
     __device__ __forceinline__ void cover(uint32_t hi) {
         if (hi <= B + kRingE) return;
-        const uint32_t nb = (hi - kRingE + 511) & ~511u;
-        const uint32_t from = (nb >= B + kRingE) ? nb : B + kRingE;
         WAVE_SYNC();
-        for (uint32_t c = from; c < nb + kRingE; c += 512) load_chunk(c);
+        const uint32_t nb = (hi - kRingE + 511) & ~511u;
+        if (nb == B + 512 && pfPos == B + kRingE) {   // common case: one chunk, already prefetched
+            store(pfPos, pa, pb);
+        } else {
+            const uint32_t from = (nb >= B + kRingE) ? nb : B + kRingE;
+            for (uint32_t c = from; c < nb + kRingE; c += 512) {
+                uint32_t a, b;
+                if (c == pfPos) { a = pa; b = pb; } else fetch(c, a, b);
+                store(c, a, b);
+            }
+        }
         B = nb;
+        pfPos = B + kRingE;
+        fetch(pfPos, pa, pb);   // next advance's chunk: in flight, not waited on
         WAVE_SYNC();
     }
     __device__ __forceinline__ bool in_ring(uint32_t pos, uint32_t len) const {
@@ -156,54 +180,85 @@ struct SrcView {
     }
 };
 
-// Emits one sequence (or the final literal run when !hasMatch): header bytes
-// (token + literal-length bytes), literals 4 per lane, then the offset and
-// match-length bytes.  Byte stores: the destination has no alignment.
-__device__ __forceinline__ void emit_seq(const SrcView& V, uint8_t* __restrict__ d, uint32_t op, uint32_t anchor,
-                                         uint32_t lit, bool hasMatch, uint32_t off, uint32_t mc) {
+// Compressed output staged in a 1 KiB LDS ring; complete 512-byte chunks are
+// flushed with 8-byte stores.  Global stores are rare, so the vmcnt waits of
+// the candidate loads do not queue behind byte stores.
+struct OutView {
+    uint8_t* d;       // block slot (8-byte aligned)
+    uint8_t* ring;    // kOutRing bytes
+    uint32_t flushed;
+
+    __device__ __forceinline__ void put(uint32_t pos, uint32_t v) { ring[pos & (kOutRing - 1)] = (uint8_t)v; }
+    __device__ __forceinline__ void flush_to(uint32_t upto) {   // flush complete chunks below `upto`
+        while (flushed + kOutFlush <= upto) {
+            WAVE_SYNC();
+            const uint32_t o = flushed + 8 * laneid();
+            const uint2 v = *reinterpret_cast<const uint2*>(ring + (o & (kOutRing - 1)));
+            *reinterpret_cast<uint2*>(d + o) = v;
+            flushed += kOutFlush;
+        }
+    }
+    __device__ __forceinline__ void finish(uint32_t op) {
+        flush_to(op);
+        WAVE_SYNC();
+        for (uint32_t o = flushed + laneid(); o < op; o += 64) d[o] = ring[o & (kOutRing - 1)];
+        flushed = op;
+    }
+};
+
+__device__ __forceinline__ uint32_t ext_len(uint32_t v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
+
+// Stages literal bytes src[from + i] for i in [i0, i1) at out position
+// base + i, 4 per lane, flushing complete chunks below `safe + i` between
+// pieces (bytes below `safe` are final).
+__device__ __forceinline__ void stage_lits(const SrcView& V, OutView& O, uint32_t from, uint32_t i0, uint32_t i1,
+                                           uint32_t base, bool flush, uint32_t safe) {
     const uint32_t L = laneid();
-    const uint32_t litExt = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
-    const uint32_t litRem = lit >= 15 ? (lit - 15) % 255 : 0;
-    const uint32_t mlExt = (hasMatch && mc >= 15) ? (mc - 15) / 255 + 1 : 0;
-    const uint32_t mlRem = mc >= 15 ? (mc - 15) % 255 : 0;
-    const uint32_t token = ((lit < 15 ? lit : 15) << 4) | (hasMatch ? (mc < 15 ? mc : 15) : 0);
-    const uint32_t head = 1 + litExt;
-    for (uint32_t x = L; x < head; x += 64) d[op + x] = (uint8_t)(x == 0 ? token : (x < litExt ? 255u : litRem));
-    uint8_t* dl = d + op + head;
-    for (uint32_t base = 0; base < lit; base += 256) {
-        const uint32_t i = base + 4 * L;
-        if (i < lit) {
+    for (uint32_t piece = i0; piece < i1; piece += 256) {
+        if (flush) O.flush_to(safe + piece);
+        const uint32_t i = piece + 4 * L;
+        if (i < i1) {
             uint32_t v;
-            if (i + 4 <= lit) {
-                v = V.rd4(anchor + i);
+            if (i + 4 <= i1) {
+                v = V.rd4(from + i);
             } else {   // tail: never touch bytes past the run (the block may end the buffer)
-                v = V.rd1(anchor + i);
-                if (i + 1 < lit) v |= V.rd1(anchor + i + 1) << 8;
-                if (i + 2 < lit) v |= V.rd1(anchor + i + 2) << 16;
+                v = V.rd1(from + i);
+                if (i + 1 < i1) v |= V.rd1(from + i + 1) << 8;
+                if (i + 2 < i1) v |= V.rd1(from + i + 2) << 16;
             }
-            dl[i] = (uint8_t)v;
-            if (i + 1 < lit) dl[i + 1] = (uint8_t)(v >> 8);
-            if (i + 2 < lit) dl[i + 2] = (uint8_t)(v >> 16);
-            if (i + 3 < lit) dl[i + 3] = (uint8_t)(v >> 24);
+            O.put(base + i, v);
+            if (i + 1 < i1) O.put(base + i + 1, v >> 8);
+            if (i + 2 < i1) O.put(base + i + 2, v >> 16);
+            if (i + 3 < i1) O.put(base + i + 3, v >> 24);
         }
+        WAVE_SYNC();
     }
-    if (hasMatch) {
-        uint8_t* dt = dl + lit;
-        const uint32_t tail = 2 + mlExt;
-        for (uint32_t y = L; y < tail; y += 64) {
-            uint32_t v;
-            if (y == 0) v = off & 255;
-            else if (y == 1) v = off >> 8;
-            else v = (y - 1 < mlExt) ? 255u : mlRem;
-            dt[y] = (uint8_t)v;
-        }
+}
+
+// `cnt` length bytes (255 ... 255 rem) at pos, flushing between 64-byte
+// pieces; every byte below pos is final.
+__device__ __forceinline__ void put_ext(OutView& O, uint32_t pos, uint32_t cnt, uint32_t rem) {
+    for (uint32_t base = 0; base < cnt; base += 64) {
+        O.flush_to(pos + base);
+        const uint32_t x = base + laneid();
+        if (x < cnt) O.put(pos + x, x + 1 < cnt ? 255u : rem);
+        WAVE_SYNC();
     }
+}
+
+// token + literal-length bytes at op (everything below op is final)
+__device__ __forceinline__ void put_head(OutView& O, uint32_t op, uint32_t lit, uint32_t mcNibble) {
+    const uint32_t token = ((lit < 15 ? lit : 15) << 4) | mcNibble;
+    O.flush_to(op);
+    if (laneid() == 0) O.put(op, token);
+    WAVE_SYNC();
+    put_ext(O, op + 1, ext_len(lit), lit >= 15 ? (lit - 15) % 255 : 0);
 }
 
 template <bool U16, bool ST>
 __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8_t* __restrict__ d, uint32_t cap,
                                 uint32_t* __restrict__ Traw, uint8_t* __restrict__ S, uint32_t* __restrict__ ringE,
-                                uint64_t* acc) {
+                                uint8_t* __restrict__ outRing, uint64_t* acc) {
     const uint32_t L = laneid();
     uint64_t ts = STAMP_T();
     const uint32_t bound = n + n / 255 + 16;
@@ -218,8 +273,9 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
         uint4* T4 = reinterpret_cast<uint4*>(Traw);
         for (uint32_t i = L; i < 1024; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
     }
-    SrcView V{s, n, ringE, 0};
+    SrcView V{s, n, ringE, 0, 0, 0, 0};
     V.init();
+    OutView O{d, outRing, 0};
 
     const uint32_t mflimitP1 = n - kMfLimit + 1;
     const uint32_t matchlimit = n - kLastLiterals;
@@ -308,19 +364,23 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
             const uint32_t maxb = wasTest ? 0u : min(ip - anchor, cd);
             const uint32_t lim = matchlimit - (ip + kMinMatch);
             V.cover(min(ip + kMinMatch + 256, n));
+            // round-0 operands (the cd side is the global round trip)
+            bool beq = false;
+            if (L + 1 <= maxb) beq = V.rd1(ip - L - 1) == V.rd1(cd - L - 1);
+            uint32_t eqb = 0;
+            if (4 * L < lim) {
+                const uint32_t x = V.rd4(ip + kMinMatch + 4 * L) ^ V.rd4(cd + kMinMatch + 4 * L);
+                eqb = x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u;
+                eqb = min(eqb, lim - 4 * L);
+            }
+            // while those loads fly: stage the literals assuming no catch-up
+            const uint32_t lit0 = ip - anchor;
+            const bool early = lit0 <= 256 && op + 1 + ext_len(lit0) + lit0 + 64 <= O.flushed + kOutRing;
+            if (early) stage_lits(V, O, anchor, 0, lit0, op + 1 + ext_len(lit0), false, 0);
+            STAMP_ADD(3, ts);
             uint32_t back = 0, mc = 0;
             bool backDone = maxb == 0, cntDone = false;
-            while (!(backDone && cntDone)) {
-                bool beq = false;
-                uint32_t eqb = 0;
-                const uint32_t kk = back + L + 1;
-                if (!backDone && kk <= maxb) beq = V.rd1(ip - kk) == V.rd1(cd - kk);
-                const uint32_t rel = mc + 4 * L;
-                if (!cntDone && rel < lim) {
-                    const uint32_t x = V.rd4(ip + kMinMatch + rel) ^ V.rd4(cd + kMinMatch + rel);
-                    eqb = x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u;
-                    eqb = min(eqb, lim - rel);
-                }
+            for (;;) {
                 if (!backDone) {
                     const uint64_t fm = ballot(!beq);
                     if (fm) { back += (uint32_t)(__ffsll((long long)fm) - 1); backDone = true; }
@@ -336,25 +396,47 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
                         mc += 256;
                     }
                 }
+                if (backDone && cntDone) break;
+                beq = false;
+                eqb = 0;
+                const uint32_t kk = back + L + 1;
+                if (!backDone && kk <= maxb) beq = V.rd1(ip - kk) == V.rd1(cd - kk);
+                const uint32_t rel = mc + 4 * L;
+                if (!cntDone && rel < lim) {
+                    const uint32_t x = V.rd4(ip + kMinMatch + rel) ^ V.rd4(cd + kMinMatch + rel);
+                    eqb = x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u;
+                    eqb = min(eqb, lim - rel);
+                }
             }
-            STAMP_ADD(3, ts);
-            const uint32_t ipm = ip - back;          // caught-up match start
-            const uint32_t mcf = mc + back;          // LZ4_count from ipm + 4
-            const uint32_t lit = ipm - anchor;
             STAMP_ADD(4, ts);
+            const uint32_t mcf = mc + back;          // LZ4_count from the caught-up start + 4
+            const uint32_t lit = lit0 - back;
+            const uint32_t litExt = ext_len(lit);
+            const uint32_t mlExt = ext_len(mcf);
             if (limited) {
                 if (!wasTest && op + 1 + lit + 8 + lit / 255 > cap) return 0;
-                const uint32_t litExt = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
                 if (op + 1 + litExt + lit + 2 + 6 + (mcf + 240) / 255 > cap) return 0;
             }
-            emit_seq(V, d, op, anchor, lit, true, ip - cd, mcf);
-            {
-                const uint32_t litExt = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
-                const uint32_t mlExt = mcf >= 15 ? (mcf - 15) / 255 + 1 : 0;
-                op += 1 + litExt + lit + 2 + mlExt;
+            const uint32_t litPos = op + 1 + litExt;
+            if (!early || litExt != ext_len(lit0)) {
+                put_head(O, op, lit, mcf < 15 ? mcf : 15);
+                WAVE_SYNC();
+                stage_lits(V, O, anchor, 0, lit, litPos, true, litPos);
+            } else {
+                put_head(O, op, lit, mcf < 15 ? mcf : 15);
             }
+            {   // offset + match-length bytes
+                const uint32_t off = ip - cd, tpos = litPos + lit;
+                O.flush_to(tpos);
+                if (L < 2) O.put(tpos + L, L == 0 ? (off & 255) : (off >> 8));
+                WAVE_SYNC();
+                put_ext(O, tpos + 2, mlExt, mcf >= 15 ? (mcf - 15) % 255 : 0);
+            }
+            op = litPos + lit + 2 + mlExt;
+            WAVE_SYNC();
+            O.flush_to(op);
             STAMP_ADD(5, ts);
-            const uint32_t ipe = ip + kMinMatch + mc;  // = ipm + mcf + 4
+            const uint32_t ipe = ip + kMinMatch + mc;  // = caught-up start + mcf + 4
             anchor = ipe;
             if (ipe >= mflimitP1) goto last_literals;
             W = Win{1, 1, ipe - 2, ipe, ipe + 1, 0};
@@ -363,17 +445,21 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
 last_literals : {
     const uint32_t run = n - anchor;
     if (limited && op + run + 1 + (run + 240) / 255 > cap) return 0;
-    emit_seq(V, d, op, anchor, run, false, 0, 0);
-    const uint32_t ext = run >= 15 ? (run - 15) / 255 + 1 : 0;
-    op += 1 + ext + run;
+    put_head(O, op, run, 0);
+    const uint32_t litPos = op + 1 + ext_len(run);
+    WAVE_SYNC();
+    stage_lits(V, O, anchor, 0, run, litPos, true, litPos);
+    op = litPos + run;
+    O.finish(op);
 }
     return (int32_t)op;
 }
 
-#define ENCODE_LDS                                                        \
-    __shared__ __attribute__((aligned(16))) uint32_t T[4096];   /* 16 KiB */ \
-    __shared__ __attribute__((aligned(16))) uint32_t R[kRingE / 4]; /* 2 KiB */ \
-    __shared__ __attribute__((aligned(16))) uint8_t S[kDedup];  /* 1 KiB */
+#define ENCODE_LDS                                                               \
+    __shared__ __attribute__((aligned(16))) uint32_t T[4096];        /* 16 KiB */ \
+    __shared__ __attribute__((aligned(16))) uint32_t R[kRingE / 4];  /* 2 KiB */  \
+    __shared__ __attribute__((aligned(16))) uint8_t OR_[kOutRing];   /* 1 KiB */  \
+    __shared__ __attribute__((aligned(16))) uint8_t S[kDedup];       /* 1 KiB */
 
 __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, uint64_t srcSize, uint32_t blockSize,
                                                uint8_t* __restrict__ slots, uint64_t slotStride,
@@ -386,8 +472,8 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
     const uint8_t* s = src + off;
     uint8_t* d = slots + (uint64_t)b * slotStride;
     int32_t r;
-    if (n < (uint32_t)kLimit64K) r = encode_block<true, false>(s, n, d, cap, T, S, R, nullptr);
-    else r = encode_block<false, false>(s, n, d, cap, T, S, R, nullptr);
+    if (n < (uint32_t)kLimit64K) r = encode_block<true, false>(s, n, d, cap, T, S, R, OR_, nullptr);
+    else r = encode_block<false, false>(s, n, d, cap, T, S, R, OR_, nullptr);
     if (laneid() == 0) csize[b] = r;
 }
 
@@ -402,8 +488,10 @@ __global__ void __launch_bounds__(64) k_encode_stats(const uint8_t* __restrict__
     const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
     uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int32_t r;
-    if (n < (uint32_t)kLimit64K) r = encode_block<true, true>(src + off, n, slots + b * slotStride, n, T, S, R, acc);
-    else r = encode_block<false, true>(src + off, n, slots + b * slotStride, n, T, S, R, acc);
+    if (n < (uint32_t)kLimit64K)
+        r = encode_block<true, true>(src + off, n, slots + b * slotStride, n, T, S, R, OR_, acc);
+    else
+        r = encode_block<false, true>(src + off, n, slots + b * slotStride, n, T, S, R, OR_, acc);
     if (laneid() == 0) {
         csize[b] = r;
         for (int i = 0; i < 8; ++i) stats[b * 8 + i] = acc[i];
