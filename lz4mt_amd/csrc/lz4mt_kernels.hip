@@ -28,6 +28,27 @@ namespace lz4mt {
 // ---------------------------------------------------------------------------
 #define WAVE_SYNC() __builtin_amdgcn_wave_barrier()
 
+// Address-space-typed pointers.  Every global (1) and LDS (3) access goes
+// through these so the compiler emits global_* / ds_* instructions: a
+// generic pointer (e.g. an LDS array kept in a struct) becomes flat_*,
+// which counts against both vmcnt and lgkmcnt and serialises the wave.
+typedef const __attribute__((address_space(1))) uint8_t g_cu8;
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+typedef const __attribute__((address_space(1))) uint32_t g_cu32;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(1))) v4u g_cu4;
+typedef __attribute__((address_space(1))) v4u g_u4;
+typedef __attribute__((address_space(1))) v2u g_u2;
+typedef __attribute__((address_space(3))) uint8_t l_u8;
+typedef __attribute__((address_space(3))) uint16_t l_u16;
+typedef __attribute__((address_space(3))) uint32_t l_u32;
+typedef __attribute__((address_space(3))) v4u l_u4;
+typedef __attribute__((address_space(3))) v2u l_u2;
+__device__ __forceinline__ g_cu8* gptr(const uint8_t* p) { return (g_cu8*)p; }
+__device__ __forceinline__ g_u8* gptr(uint8_t* p) { return (g_u8*)p; }
+
 __device__ __forceinline__ uint32_t laneid() { return __lane_id(); }
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int lane) {
@@ -42,10 +63,9 @@ __device__ __forceinline__ uint64_t mask_le(uint32_t L) { return (L >= 63) ? ~0u
 // Little-endian 32-bit read at an arbitrary byte address.  Only the aligned
 // dwords that hold requested bytes are touched, so it never reads a dword
 // that lies wholly past the last requested byte.
-__device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-    const uint32_t sh = (uint32_t)(a & 3);
+__device__ __forceinline__ uint32_t ld32u(g_cu8* p) {
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+    g_cu32* q = (g_cu32*)(p - sh);
     const uint32_t lo = q[0];
     const uint32_t hi = sh ? q[1] : 0u;
     return __builtin_amdgcn_alignbyte(hi, lo, sh);
@@ -113,9 +133,9 @@ constexpr uint32_t kOutRing = 1024;               // LDS staging of the compress
 constexpr uint32_t kOutFlush = 512;               // flush granule (64 lanes x 8 B)
 
 struct SrcView {
-    const uint8_t* s;
+    g_cu8* s;
     uint32_t n;
-    uint32_t* ring;   // kRingE bytes
+    l_u32* ring;      // kRingE bytes
     uint32_t B;
     uint32_t pfPos;   // position of the prefetched chunk in (pa, pb)
     uint32_t pa, pb;
@@ -123,8 +143,8 @@ struct SrcView {
     __device__ __forceinline__ void fetch(uint32_t c, uint32_t& a, uint32_t& b) const {
         const uint32_t pos = c + 8 * laneid();
         a = 0; b = 0;
-        if (pos < n) a = *reinterpret_cast<const uint32_t*>(s + pos);
-        if (pos + 4 < n) b = *reinterpret_cast<const uint32_t*>(s + pos + 4);
+        if (pos < n) a = *(g_cu32*)(s + pos);
+        if (pos + 4 < n) b = *(g_cu32*)(s + pos + 4);
     }
     __device__ __forceinline__ void store(uint32_t c, uint32_t a, uint32_t b) {
         const uint32_t w = (c >> 2) + 2 * laneid();
@@ -184,8 +204,8 @@ struct SrcView {
 // flushed with 8-byte stores.  Global stores are rare, so the vmcnt waits of
 // the candidate loads do not queue behind byte stores.
 struct OutView {
-    uint8_t* d;       // block slot (8-byte aligned)
-    uint8_t* ring;    // kOutRing bytes
+    g_u8* d;          // block slot (8-byte aligned)
+    l_u8* ring;       // kOutRing bytes
     uint32_t flushed;
 
     __device__ __forceinline__ void put(uint32_t pos, uint32_t v) { ring[pos & (kOutRing - 1)] = (uint8_t)v; }
@@ -193,8 +213,8 @@ struct OutView {
         while (flushed + kOutFlush <= upto) {
             WAVE_SYNC();
             const uint32_t o = flushed + 8 * laneid();
-            const uint2 v = *reinterpret_cast<const uint2*>(ring + (o & (kOutRing - 1)));
-            *reinterpret_cast<uint2*>(d + o) = v;
+            const v2u v = *(l_u2*)(ring + (o & (kOutRing - 1)));
+            *(g_u2*)(d + o) = v;
             flushed += kOutFlush;
         }
     }
@@ -256,9 +276,9 @@ __device__ __forceinline__ void put_head(OutView& O, uint32_t op, uint32_t lit, 
 }
 
 template <bool U16, bool ST>
-__device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8_t* __restrict__ d, uint32_t cap,
-                                uint32_t* __restrict__ Traw, uint8_t* __restrict__ S, uint32_t* __restrict__ ringE,
-                                uint8_t* __restrict__ outRing, uint64_t* acc) {
+__device__ int32_t encode_block(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
+                                l_u32* __restrict__ Traw, l_u8* __restrict__ S, l_u32* __restrict__ ringE,
+                                l_u8* __restrict__ outRing, uint64_t* acc) {
     const uint32_t L = laneid();
     uint64_t ts = STAMP_T();
     const uint32_t bound = n + n / 255 + 16;
@@ -268,10 +288,10 @@ __device__ int32_t encode_block(const uint8_t* __restrict__ s, uint32_t n, uint8
         if (L == 0) d[0] = 0;
         return 1;
     }
-    uint16_t* T16 = reinterpret_cast<uint16_t*>(Traw);
+    l_u16* T16 = (l_u16*)Traw;
     {
-        uint4* T4 = reinterpret_cast<uint4*>(Traw);
-        for (uint32_t i = L; i < 1024; i += 64) T4[i] = make_uint4(0, 0, 0, 0);
+        l_u4* T4 = (l_u4*)Traw;
+        for (uint32_t i = L; i < 1024; i += 64) T4[i] = (v4u){0, 0, 0, 0};
     }
     SrcView V{s, n, ringE, 0, 0, 0, 0};
     V.init();
@@ -469,11 +489,15 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
     const uint64_t off = (uint64_t)b * blockSize;
     const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
     const uint32_t cap = (capOverride == 0xFFFFFFFFu) ? n : capOverride;   // lz4mt: cap = n
-    const uint8_t* s = src + off;
-    uint8_t* d = slots + (uint64_t)b * slotStride;
+    g_cu8* s = gptr(src) + off;
+    g_u8* d = gptr(slots) + (uint64_t)b * slotStride;
+    l_u32* Tl = (l_u32*)T;
+    l_u8* Sl = (l_u8*)S;
+    l_u32* Rl = (l_u32*)R;
+    l_u8* Ol = (l_u8*)OR_;
     int32_t r;
-    if (n < (uint32_t)kLimit64K) r = encode_block<true, false>(s, n, d, cap, T, S, R, OR_, nullptr);
-    else r = encode_block<false, false>(s, n, d, cap, T, S, R, OR_, nullptr);
+    if (n < (uint32_t)kLimit64K) r = encode_block<true, false>(s, n, d, cap, Tl, Sl, Rl, Ol, nullptr);
+    else r = encode_block<false, false>(s, n, d, cap, Tl, Sl, Rl, Ol, nullptr);
     if (laneid() == 0) csize[b] = r;
 }
 
@@ -488,10 +512,12 @@ __global__ void __launch_bounds__(64) k_encode_stats(const uint8_t* __restrict__
     const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
     uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int32_t r;
+    g_cu8* s = gptr(src) + off;
+    g_u8* d = gptr(slots) + b * slotStride;
     if (n < (uint32_t)kLimit64K)
-        r = encode_block<true, true>(src + off, n, slots + b * slotStride, n, T, S, R, OR_, acc);
+        r = encode_block<true, true>(s, n, d, n, (l_u32*)T, (l_u8*)S, (l_u32*)R, (l_u8*)OR_, acc);
     else
-        r = encode_block<false, true>(src + off, n, slots + b * slotStride, n, T, S, R, OR_, acc);
+        r = encode_block<false, true>(s, n, d, n, (l_u32*)T, (l_u8*)S, (l_u32*)R, (l_u8*)OR_, acc);
     if (laneid() == 0) {
         csize[b] = r;
         for (int i = 0; i < 8; ++i) stats[b * 8 + i] = acc[i];
@@ -517,12 +543,12 @@ template <bool ST>
 struct Dec {
     uint64_t* acc;
     uint64_t ts;
-    const uint8_t* src;   // compressed block
+    g_cu8* src;           // compressed block
     int64_t len;
-    uint8_t* dst;         // block's output slot (16-B aligned)
+    g_u8* dst;            // block's output slot (16-B aligned)
     int64_t physcap;      // bytes of the slot that exist
-    uint8_t* ring;
-    uint8_t* win;
+    l_u8* ring;
+    l_u8* win;
     int64_t wlo;          // block-relative position of win[0]
     int64_t flushed;      // [0, flushed) stored to dst
     int64_t completed;    // [0, completed) known complete in memory
@@ -536,15 +562,15 @@ struct Dec {
 #pragma unroll
         for (int h = 0; h < kInWin / 1024; ++h) {
             const uintptr_t a = base + (uintptr_t)(h * 1024 + 16 * L);
-            const uint32_t* q = reinterpret_cast<const uint32_t*>(a);
-            uint4 v = make_uint4(0, 0, 0, 0);   // dword-granular: never past the block's last dword
-            if (a + 12 < end) v = *reinterpret_cast<const uint4*>(a);
+            g_cu32* q = (g_cu32*)(src + (a - reinterpret_cast<uintptr_t>(src)));
+            v4u v = {0, 0, 0, 0};   // dword-granular: never past the block's last dword
+            if (a + 12 < end) v = *(g_cu4*)q;
             else {
                 if (a < end) v.x = q[0];
                 if (a + 4 < end) v.y = q[1];
                 if (a + 8 < end) v.z = q[2];
             }
-            *reinterpret_cast<uint4*>(win + h * 1024 + 16 * L) = v;
+            *(l_u4*)(win + h * 1024 + 16 * L) = v;
         }
         WAVE_SYNC();
     }
@@ -557,9 +583,9 @@ struct Dec {
     __device__ __forceinline__ void flush_to(int64_t upto) {
         const uint32_t L = laneid();
         while (flushed + kFlush <= upto) {
-            const uint4 v = *reinterpret_cast<const uint4*>(ring + ((flushed & (kRing - 1)) + 16 * L));
+            const v4u v = *(l_u4*)(ring + ((flushed & (kRing - 1)) + 16 * L));
             const int64_t o = flushed + 16 * L;
-            if (o + 16 <= physcap) *reinterpret_cast<uint4*>(dst + o) = v;
+            if (o + 16 <= physcap) *(g_u4*)(dst + o) = v;
             flushed += kFlush;
         }
     }
@@ -761,10 +787,10 @@ output_error:
 }
 
 // raw (incompressible) block: src at any alignment -> dst 16-B aligned
-__device__ void copy_raw(const uint8_t* src, uint8_t* dst, int64_t n) {
+__device__ void copy_raw(g_cu8* src, g_u8* dst, int64_t n) {
     const uint32_t L = laneid();
     const int64_t nd = n >> 2;   // whole destination dwords
-    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
+    g_u32* d32 = (g_u32*)dst;
     for (int64_t base = 0; base < nd; base += 64 * 4) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -788,17 +814,17 @@ __global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ frame
     int32_t res;
     if (r.bits & 0x80000000u) {
         if (len > physcap) res = kDecodeOutputTooSmall;
-        else { copy_raw(frame + r.offset, out + slot, len); res = (int32_t)len; }
+        else { copy_raw(gptr(frame) + r.offset, gptr(out) + slot, len); res = (int32_t)len; }
     } else {
         Dec<false> D;
         D.acc = nullptr;
         D.ts = 0;
-        D.src = frame + r.offset;
+        D.src = gptr(frame) + r.offset;
         D.len = len;
-        D.dst = out + slot;
+        D.dst = gptr(out) + slot;
         D.physcap = physcap;
-        D.ring = ring;
-        D.win = win;
+        D.ring = (l_u8*)ring;
+        D.win = (l_u8*)win;
         D.wlo = INT64_MIN / 4;
         D.flushed = 0;
         D.completed = 0;
@@ -821,12 +847,12 @@ __global__ void __launch_bounds__(64) k_decode_stats(const uint8_t* __restrict__
     Dec<true> D;
     D.acc = acc;
     D.ts = t0;
-    D.src = frame + r.offset;
+    D.src = gptr(frame) + r.offset;
     D.len = r.bits & 0x7FFFFFFFu;
-    D.dst = out + slot;
+    D.dst = gptr(out) + slot;
     D.physcap = (int64_t)min<uint64_t>(blockMax, outCap - slot);
-    D.ring = ring;
-    D.win = win;
+    D.ring = (l_u8*)ring;
+    D.win = (l_u8*)win;
     D.wlo = INT64_MIN / 4;
     D.flushed = 0;
     D.completed = 0;
@@ -867,13 +893,12 @@ __device__ __forceinline__ uint32_t xround(uint32_t acc, uint32_t w) { return ro
 // One wavefront hashes one byte range: the range streams through LDS in
 // 1 KiB chunks (64 lanes x 16 B, loaded one chunk ahead), lanes 0..3 run
 // the four accumulator chains (v1..v4 of XXH32) over each chunk.
-__device__ __forceinline__ uint4 load16u(const uint8_t* p) {   // 16 bytes at any alignment
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-    const uint32_t sh = (uint32_t)(a & 3);
+__device__ __forceinline__ v4u load16u(g_cu8* p) {   // 16 bytes at any alignment
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+    g_cu32* q = (g_cu32*)(p - sh);
     const uint32_t a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
     const uint32_t a4 = sh ? q[4] : 0u;
-    uint4 v;
+    v4u v;
     v.x = __builtin_amdgcn_alignbyte(a1, a0, sh);
     v.y = __builtin_amdgcn_alignbyte(a2, a1, sh);
     v.z = __builtin_amdgcn_alignbyte(a3, a2, sh);
@@ -881,22 +906,22 @@ __device__ __forceinline__ uint4 load16u(const uint8_t* p) {   // 16 bytes at an
     return v;
 }
 
-__device__ uint32_t xxh32_wave(const uint8_t* p, uint64_t len, uint32_t* __restrict__ buf /* 512 dwords */) {
+__device__ uint32_t xxh32_wave(g_cu8* p, uint64_t len, l_u32* __restrict__ buf /* 512 dwords */) {
     const uint32_t L = laneid();
     uint32_t v = (L == 0) ? kP1 + kP2 : (L == 1) ? kP2 : (L == 2) ? 0u : (uint32_t)(0u - kP1);
     const uint64_t ns = len >> 4;            // whole 16-byte stripes
     const uint64_t nch = (ns + 63) >> 6;     // 1 KiB chunks
-    uint4 r = make_uint4(0, 0, 0, 0);
+    v4u r = {0, 0, 0, 0};
     if (nch && (uint64_t)L < ns) r = load16u(p + 16 * L);
     uint32_t cur = 0;
     for (uint64_t ch = 0; ch < nch; ++ch) {
-        reinterpret_cast<uint4*>(buf + cur * 256)[L] = r;
+        ((l_u4*)(buf + cur * 256))[L] = r;
         const uint64_t nxt = (ch + 1) * 64 + L;
         if (ch + 1 < nch && nxt < ns) r = load16u(p + 16 * nxt);
         WAVE_SYNC();
         if (L < 4) {
             const uint32_t m = (uint32_t)min<uint64_t>(64, ns - ch * 64);
-            const uint32_t* cb = buf + cur * 256 + L;
+            const l_u32* cb = buf + cur * 256 + L;
             uint32_t i = 0;
             for (; i + 8 <= m; i += 8) {
                 uint32_t w[8];
@@ -929,7 +954,7 @@ __global__ void __launch_bounds__(64) k_xxh32_stored(const uint8_t* __restrict__
     const uint64_t off = (uint64_t)b * blockSize;
     const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
     const int32_t cs = csize[b];
-    const uint32_t h = xxh32_wave(cs > 0 ? slots + off : src + off, cs > 0 ? (uint64_t)cs : n, buf);
+    const uint32_t h = xxh32_wave(cs > 0 ? gptr(slots) + off : gptr(src) + off, cs > 0 ? (uint64_t)cs : n, (l_u32*)buf);
     if (laneid() == 0) digest[b] = h;
 }
 
@@ -939,7 +964,7 @@ __global__ void __launch_bounds__(64) k_xxh32_frame_blocks(const uint8_t* __rest
     __shared__ __attribute__((aligned(16))) uint32_t buf[512];
     const uint32_t b = blockIdx.x;
     const BlockRec r = recs[b];
-    const uint32_t h = xxh32_wave(frame + r.offset, r.bits & 0x7FFFFFFFu, buf);
+    const uint32_t h = xxh32_wave(gptr(frame) + r.offset, r.bits & 0x7FFFFFFFu, (l_u32*)buf);
     if (laneid() == 0) digest[b] = h;
 }
 
@@ -947,7 +972,7 @@ __global__ void __launch_bounds__(64) k_xxh32_frame_blocks(const uint8_t* __rest
 __global__ void __launch_bounds__(64) k_xxh32_stream(const uint8_t* __restrict__ p, uint64_t len,
                                                      uint32_t* __restrict__ digest) {
     __shared__ __attribute__((aligned(16))) uint32_t buf[512];
-    const uint32_t h = xxh32_wave(p, len, buf);
+    const uint32_t h = xxh32_wave(gptr(p), len, (l_u32*)buf);
     if (laneid() == 0) *digest = h;
 }
 
@@ -1012,11 +1037,11 @@ __global__ void __launch_bounds__(256) k_frame_assemble(const uint8_t* __restric
     const uint64_t off = (uint64_t)b * blockSize;
     const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
     const int32_t cs = csize[b];
-    const uint8_t* sp = cs > 0 ? slots + off : src + off;   // 16-B aligned
+    g_cu8* sp = cs > 0 ? gptr(slots) + off : gptr(src) + off;   // 16-B aligned
     const uint64_t L = cs > 0 ? (uint64_t)cs : n;
     const uint32_t bits = cs > 0 ? (uint32_t)cs : (n | 0x80000000u);
-    uint8_t* rec = frame + hdrLen + recOff[b];
-    uint8_t* D = rec + 4;
+    g_u8* rec = gptr(frame) + hdrLen + recOff[b];
+    g_u8* D = rec + 4;
     if (t < 4) rec[t] = (uint8_t)(bits >> (8 * t));
     if (blockChecksum && t >= 4 && t < 8) D[L + (t - 4)] = (uint8_t)(bsum[b] >> (8 * (t - 4)));
     const uintptr_t Da = reinterpret_cast<uintptr_t>(D);
@@ -1033,16 +1058,16 @@ __global__ void __launch_bounds__(256) k_frame_assemble(const uint8_t* __restric
     const uint64_t nchunks = (E0 - A0) >> 4;
     for (uint64_t j = t; j < nchunks; j += 256) {
         const uint64_t so = head + 16 * j;                 // source byte offset of this chunk
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(sp + (so & ~3ull));
+        g_cu32* q = (g_cu32*)(sp + (so & ~3ull));
         const uint32_t s3 = (uint32_t)(so & 3);
         const uint32_t a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
         const uint32_t a4 = s3 ? q[4] : 0u;
-        uint4 v;
+        v4u v;
         v.x = __builtin_amdgcn_alignbyte(a1, a0, s3);
         v.y = __builtin_amdgcn_alignbyte(a2, a1, s3);
         v.z = __builtin_amdgcn_alignbyte(a3, a2, s3);
         v.w = __builtin_amdgcn_alignbyte(a4, a3, s3);
-        *reinterpret_cast<uint4*>(A0 + 16 * j) = v;
+        *(g_u4*)(D + (A0 - Da) + 16 * j) = v;
     }
 }
 
