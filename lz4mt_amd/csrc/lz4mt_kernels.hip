@@ -550,6 +550,8 @@ struct Dec {
     l_u8* ring;
     l_u8* win;
     int64_t wlo;          // block-relative position of win[0]
+    int64_t labase;       // block position of the register lookahead's byte 0
+    uint32_t la;          // lookahead: lane L holds bytes [labase + 4L, labase + 4L + 4)
     int64_t flushed;      // [0, flushed) stored to dst
     int64_t completed;    // [0, completed) known complete in memory
 
@@ -574,10 +576,22 @@ struct Dec {
         }
         WAVE_SYNC();
     }
+    // 256-byte register lookahead of the token stream: the serial parser
+    // extracts bytes with v_readlane (no LDS round trip per byte)
+    __device__ __forceinline__ void refill_la(int64_t i) {
+        if (i < wlo || i + 256 > wlo + kInWin) refill(i);
+        labase = wlo + ((i - wlo) & ~int64_t(3));
+        la = *(l_u32*)(win + (labase - wlo) + 4 * laneid());
+    }
     __device__ __forceinline__ uint32_t in8(int64_t i) {
         if (i < 0 || i >= len) return 0;
-        if (i < wlo || i >= wlo + kInWin) refill(i);
-        return win[i - wlo];
+        int64_t k = i - labase;
+        if (k < 0 || k >= 256) {
+            refill_la(i);
+            k = i - labase;
+        }
+        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)la, (int)(k >> 2));
+        return (w >> ((uint32_t)(k & 3) * 8)) & 255u;
     }
     // flush every complete kFlush chunk below `upto`
     __device__ __forceinline__ void flush_to(int64_t upto) {
@@ -641,6 +655,29 @@ struct Dec {
         }
         STAMP_ADD((int64_t)offset > kRing ? 3 : 2, ts);
     }
+    // literal [ipl, ipl+lit) -> [opl, opl+lit), then a match of mlen bytes at
+    // opl+lit with `off`.  When the whole sequence fits one wave step and the
+    // match source lies wholly before the sequence, it is ONE LDS read (lanes
+    // pick the input window or the history ring) and ONE LDS write.
+    __device__ __forceinline__ void copy_seq(int64_t ipl, int64_t opl, int64_t lit, uint32_t off, int64_t mlen) {
+        const int64_t tot = lit + mlen;
+        if (tot <= 64 && (int64_t)off >= tot && (int64_t)off <= kRing - 128 && ipl >= wlo &&
+            ipl + lit <= wlo + kInWin) {
+            STAMP_ADD(0, ts);
+            if (ST) acc[6] += 1;
+            flush_to(opl);
+            const int64_t x = laneid();
+            uint32_t v = 0;
+            if (x < lit) v = win[ipl + x - wlo];
+            else if (x < tot) v = ring[(opl + x - off) & (kRing - 1)];
+            if (x < tot) ring[(opl + x) & (kRing - 1)] = (uint8_t)v;
+            WAVE_SYNC();
+            STAMP_ADD(2, ts);
+            return;
+        }
+        if (lit) copy_lit(ipl, opl, lit);
+        copy_match(opl + lit, off, mlen);
+    }
     // read_variable_length(); returns 0 ok, -1 initial error, -2 loop error
     __device__ __forceinline__ int rvl(int64_t& ip, int64_t lencheck, bool loopCheck, bool initialCheck,
                                        int64_t& length) {
@@ -664,6 +701,7 @@ __device__ int32_t decode_block(Dec<ST>& D, int64_t cap) {
     const int64_t iend = D.len, oend = cap;
     const int64_t shortiend = iend - 16, shortoend = oend - 32;
     int64_t ip = 0, op = 0, cpy = 0, match = 0, length = 0, ext = 0;
+    int64_t plIp = 0, plOp = 0, plLen = 0;   // literal run deferred to its sequence's match copy
     uint32_t token = 0, offset = 0;
     int e;
 
@@ -688,7 +726,7 @@ __device__ int32_t decode_block(Dec<ST>& D, int64_t cap) {
             if (ip > iend - 17) goto safe_literal_copy;
         }
         PHYS_CHECK(cpy);
-        D.copy_lit(ip, op, length);
+        plIp = ip; plOp = op; plLen = length;
         ip += length;
         op = cpy;
         offset = D.in8(ip) | (D.in8(ip + 1) << 8);
@@ -707,7 +745,7 @@ __device__ int32_t decode_block(Dec<ST>& D, int64_t cap) {
             if (op + length >= oend - 64) goto safe_match_copy;
             if (match >= 0 && offset >= 8) {
                 PHYS_CHECK(op + length);
-                D.copy_match(op, offset, length);
+                D.copy_seq(plIp, plOp, plLen, offset, length);
                 op += length;
                 continue;
             }
@@ -715,7 +753,7 @@ __device__ int32_t decode_block(Dec<ST>& D, int64_t cap) {
         if (match < 0) goto output_error;
         cpy = op + length;
         PHYS_CHECK(cpy);
-        D.copy_match(op, offset, length);
+        D.copy_seq(plIp, plOp, plLen, offset, length);
         op = cpy;
     }
 
@@ -725,7 +763,7 @@ safe_decode:
         length = token >> 4;
         if (length != 15 && ip < shortiend && op <= shortoend) {
             PHYS_CHECK(op + length);
-            D.copy_lit(ip, op, length);
+            plIp = ip; plOp = op; plLen = length;
             op += length;
             ip += length;
             length = token & 15;
@@ -734,7 +772,7 @@ safe_decode:
             match = op - (int64_t)offset;
             if (length != 15 && offset >= 8 && match >= 0) {
                 PHYS_CHECK(op + length + kMinMatch);
-                D.copy_match(op, offset, length + kMinMatch);
+                D.copy_seq(plIp, plOp, plLen, offset, length + kMinMatch);
                 op += length + kMinMatch;
                 continue;
             }
@@ -756,7 +794,7 @@ safe_decode:
             break;
         }
         PHYS_CHECK(cpy);
-        D.copy_lit(ip, op, length);
+        plIp = ip; plOp = op; plLen = length;
         ip += length;
         op = cpy;
         offset = D.in8(ip) | (D.in8(ip + 1) << 8);
@@ -775,7 +813,7 @@ safe_decode:
         cpy = op + length;
         if (cpy > oend - kLastLiterals) goto output_error;
         PHYS_CHECK(cpy);
-        D.copy_match(op, offset, length);
+        D.copy_seq(plIp, plOp, plLen, offset, length);
         op = cpy;
     }
 #undef PHYS_CHECK
@@ -826,6 +864,8 @@ __global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ frame
         D.ring = (l_u8*)ring;
         D.win = (l_u8*)win;
         D.wlo = INT64_MIN / 4;
+        D.labase = INT64_MIN / 4;
+        D.la = 0;
         D.flushed = 0;
         D.completed = 0;
         res = decode_block(D, (int64_t)blockMax);
@@ -854,6 +894,8 @@ __global__ void __launch_bounds__(64) k_decode_stats(const uint8_t* __restrict__
     D.ring = (l_u8*)ring;
     D.win = (l_u8*)win;
     D.wlo = INT64_MIN / 4;
+    D.labase = INT64_MIN / 4;
+    D.la = 0;
     D.flushed = 0;
     D.completed = 0;
     const int32_t res = decode_block(D, (int64_t)blockMax);
