@@ -533,6 +533,26 @@ hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSiz
 }
 
 // ---------------------------------------------------------------------------
+// Wave-wide inclusive prefix sum and max (DPP row shifts + 3 cross-row adds)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    const uint32_t r0 = rdlane(v, 15), r1 = rdlane(v, 31), r2 = rdlane(v, 47);
+    const uint32_t row = laneid() >> 4;
+    return v + (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));
+    return max(max(rdlane(v, 15), rdlane(v, 31)), max(rdlane(v, 47), rdlane(v, 63)));
+}
+
+// ---------------------------------------------------------------------------
 // Decoder
 // ---------------------------------------------------------------------------
 constexpr int32_t kRing = 16384;   // LDS history ring (bytes)
@@ -678,6 +698,170 @@ struct Dec {
         if (lit) copy_lit(ipl, opl, lit);
         copy_match(opl + lit, off, mlen);
     }
+    // ---------------------------------------------------------------------
+    // Batch fast path.  Called at the top of the 1.9.3 fast loop.  Consumes
+    // the longest run of sequences (<= 64) that the fast loop would process
+    // on its normal path -- no error, no detour to safe_literal_copy /
+    // safe_match_copy, one-byte length extensions, offset != 0 -- so the
+    // serial state machine resumes at the same loop top with identical
+    // state.  Returns the number of sequences consumed (0: run serially).
+    //   1. next-token delta for 256 candidate positions (4 per lane)
+    //   2. serial hop over the packed deltas (v_readlane), one lane per sequence
+    //   3. lane-parallel field decode, DPP prefix sum of output lengths
+    //   4. lane-parallel check of the fast-loop conditions, cut at the first miss
+    //   5. copies: literals, far matches (HBM, independent), near matches in
+    //      dependency rounds (frontier = first unfinished sequence)
+    // ---------------------------------------------------------------------
+    __device__ __forceinline__ int decode_batch(int64_t& ip, int64_t& op, int64_t iend, int64_t oend) {
+        if (ip + 1024 > iend || op + 8192 > oend) return 0;
+        if (ip < wlo || ip + 768 > wlo + kInWin) refill(ip);
+        const uint32_t L = laneid();
+        const int64_t w0 = ip - wlo;
+        // 1. candidate deltas
+        uint32_t packed = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t x = w0 + 4 * L + e;
+            const uint32_t t = win[x];
+            uint32_t lit = t >> 4, ext1 = 0;
+            bool cx = false;
+            if (lit == 15) { const uint32_t b = win[x + 1]; cx = b == 255; lit += b; ext1 = 1; }
+            uint32_t ext2 = 0;
+            if ((t & 15) == 15) { const uint32_t b = win[x + 1 + ext1 + lit + 2]; cx = cx || b == 255; ext2 = 1; }
+            const uint32_t d = 1 + ext1 + lit + 2 + ext2;
+            packed |= ((cx || lit > 64 || d > 255) ? 0u : d) << (8 * e);
+        }
+        // 2. hop
+        uint32_t startRel = 0, cnt = 0, cur = 0;
+        while (cnt < 64 && cur < 256) {
+            const uint32_t wv = rdlane(packed, (int)(cur >> 2));
+            const uint32_t d = (wv >> ((cur & 3) * 8)) & 255u;
+            if (d == 0) break;
+            if (L == cnt) startRel = cur;
+            cur += d;
+            ++cnt;
+        }
+        if (cnt == 0) return 0;
+        // 3. fields
+        const bool act = L < cnt;
+        const int64_t sw = w0 + startRel;   // window index of the token
+        uint32_t tok = 0, lit = 0, ext1 = 0, off = 0, mlen = 0, ext2 = 0;
+        if (act) {
+            tok = win[sw];
+            lit = tok >> 4;
+            if (lit == 15) { lit += win[sw + 1]; ext1 = 1; }
+            const int64_t ow = sw + 1 + ext1 + lit;
+            off = win[ow] | ((uint32_t)win[ow + 1] << 8);
+            mlen = (tok & 15) + kMinMatch;
+            if ((tok & 15) == 15) { mlen += win[ow + 2]; ext2 = 1; }
+        }
+        const uint32_t olen = act ? lit + mlen : 0u;
+        const uint32_t incl = wave_scan_incl(olen);
+        const int64_t oj = op + (int64_t)(incl - olen);   // sequence output start
+        const int64_t ipT = ip + startRel + 1;            // just after the token
+        const int64_t lp = ipT + ext1;                    // literal start
+        const int64_t om = oj + lit;                      // match output start
+        // 4. fast-loop conditions (lz4 1.9.3, see decode_block)
+        bool ok = act && off != 0 && lit <= 64 && mlen <= 128 && (int64_t)incl <= 4096;
+        if ((tok >> 4) == 15) ok = ok && ipT < iend - 15 && ipT + 1 < iend - 15 && !(oj + lit > oend - 32) &&
+                                   !(lp + lit > iend - 32);
+        else ok = ok && !(ipT > iend - 17);
+        ok = ok && om - (int64_t)off >= 0;
+        if ((tok & 15) == 15) ok = ok && lp + lit + 3 < iend - kLastLiterals + 1;
+        ok = ok && om + mlen < oend - 64;
+        const uint64_t bad = ballot(act && !ok);
+        const uint32_t nb = bad ? (uint32_t)(__ffsll((long long)bad) - 1) : cnt;
+        if (nb == 0) return 0;
+        const bool in = L < nb;
+        STAMP_ADD(0, ts);
+        if (ST) acc[6] += nb;
+        // 5. copies.  Ring invariant: after flush_to(op) everything below op
+        // that may still be read from the ring lies in [op - kRing + 4096, op).
+        flush_to(op);
+        WAVE_SYNC();
+        {   // literals (independent: window -> ring), 4 bytes per step
+            const uint32_t maxLit = wave_max(in ? lit : 0u);
+            const int64_t lw = lp - wlo;
+            for (uint32_t k = 0; k < maxLit; k += 4) {
+                uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+                if (in && k < lit) b0 = win[lw + k];
+                if (in && k + 1 < lit) b1 = win[lw + k + 1];
+                if (in && k + 2 < lit) b2 = win[lw + k + 2];
+                if (in && k + 3 < lit) b3 = win[lw + k + 3];
+                if (in && k < lit) ring[(oj + k) & (kRing - 1)] = (uint8_t)b0;
+                if (in && k + 1 < lit) ring[(oj + k + 1) & (kRing - 1)] = (uint8_t)b1;
+                if (in && k + 2 < lit) ring[(oj + k + 2) & (kRing - 1)] = (uint8_t)b2;
+                if (in && k + 3 < lit) ring[(oj + k + 3) & (kRing - 1)] = (uint8_t)b3;
+            }
+        }
+        STAMP_ADD(1, ts);
+        const int64_t src = om - (int64_t)off;
+        const int64_t ringLo = op + 4096 - kRing;     // oldest position safely in the ring
+        const bool far = in && src < ringLo;          // then src + mlen < op: wholly older data
+        const uint64_t farMask = ballot(far);
+        if (farMask) {   // HBM sources: all loads independent, issued together
+            if (completed < ringLo) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                completed = flushed;
+            }
+            if (far) {
+                const uint32_t sh = (uint32_t)(src & 3);
+                g_cu32* q = (g_cu32*)(dst + (src - sh));
+                const uint32_t nw = (sh + mlen + 3) >> 2;   // dwords covering [src, src+mlen)
+                uint32_t wv[33];
+#pragma unroll
+                for (int i = 0; i < 33; ++i) wv[i] = (uint32_t)i < nw ? q[i] : 0u;
+#pragma unroll
+                for (int i = 0; i < 33; ++i) {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const int64_t k = 4 * i + b - (int64_t)sh;   // output byte index
+                        if (k >= 0 && k < (int64_t)mlen) ring[(om + k) & (kRing - 1)] = (uint8_t)(wv[i] >> (8 * b));
+                    }
+                }
+            }
+        }
+        STAMP_ADD(3, ts);
+        uint64_t undone = ballot(in && !far);
+        const int64_t srcHi = min(src + (int64_t)mlen, om);
+        while (undone) {
+            WAVE_SYNC();
+            const int u = __ffsll((long long)undone) - 1;
+            const int64_t F = op + (int64_t)rdlane((uint32_t)(om - op), u);   // all output below F is final
+            const bool ready = ((undone >> L) & 1) && srcHi <= F;
+            const uint64_t rm = ballot(ready);
+            const uint32_t maxM = wave_max(ready ? mlen : 0u);
+            const bool wide = ballot(ready && off < 4) == 0;
+            if (wide) {
+                for (uint32_t k = 0; k < maxM; k += 4) {
+                    uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+                    if (ready && k < mlen) b0 = ring[(src + k) & (kRing - 1)];
+                    if (ready && k + 1 < mlen) b1 = ring[(src + k + 1) & (kRing - 1)];
+                    if (ready && k + 2 < mlen) b2 = ring[(src + k + 2) & (kRing - 1)];
+                    if (ready && k + 3 < mlen) b3 = ring[(src + k + 3) & (kRing - 1)];
+                    if (ready && k < mlen) ring[(om + k) & (kRing - 1)] = (uint8_t)b0;
+                    if (ready && k + 1 < mlen) ring[(om + k + 1) & (kRing - 1)] = (uint8_t)b1;
+                    if (ready && k + 2 < mlen) ring[(om + k + 2) & (kRing - 1)] = (uint8_t)b2;
+                    if (ready && k + 3 < mlen) ring[(om + k + 3) & (kRing - 1)] = (uint8_t)b3;
+                    WAVE_SYNC();
+                }
+            } else {
+                for (uint32_t k = 0; k < maxM; ++k) {
+                    if (ready && k < mlen) ring[(om + k) & (kRing - 1)] = ring[(src + k) & (kRing - 1)];
+                    WAVE_SYNC();
+                }
+            }
+            undone &= ~rm;
+        }
+        WAVE_SYNC();
+        STAMP_ADD(2, ts);
+        // advance past the last consumed sequence
+        const uint32_t last = nb - 1;
+        ip = ip + (int64_t)rdlane(startRel, (int)last) + 1 + rdlane(ext1, (int)last) + rdlane(lit, (int)last) + 2 +
+             rdlane(ext2, (int)last);
+        op = op + (int64_t)rdlane(incl, (int)last);
+        return (int)nb;
+    }
     // read_variable_length(); returns 0 ok, -1 initial error, -2 loop error
     __device__ __forceinline__ int rvl(int64_t& ip, int64_t lencheck, bool loopCheck, bool initialCheck,
                                        int64_t& length) {
@@ -713,6 +897,7 @@ __device__ int32_t decode_block(Dec<ST>& D, int64_t cap) {
 
     if (oend - op < 64) goto safe_decode;
     for (;;) {
+        if (D.decode_batch(ip, op, iend, oend)) continue;
         token = D.in8(ip++);
         length = token >> 4;
         if (length == 15) {
