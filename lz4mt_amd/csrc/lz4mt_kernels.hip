@@ -713,23 +713,22 @@ struct Dec {
     //      dependency rounds (frontier = first unfinished sequence)
     // ---------------------------------------------------------------------
     __device__ __forceinline__ int decode_batch(int64_t& ip, int64_t& op, int64_t iend, int64_t oend) {
-        if (ip + 1024 > iend || op + 8192 > oend) return 0;
-        if (ip < wlo || ip + 768 > wlo + kInWin) refill(ip);
+        if (ip + 1280 > iend || op + 8192 > oend) return 0;
+        if (ip < wlo || ip + 1024 > wlo + kInWin) refill(ip);
         const uint32_t L = laneid();
-        const int64_t w0 = ip - wlo;
-        // 1. candidate deltas
+        const uint32_t w0 = (uint32_t)(ip - wlo);
+        // 1. candidate deltas, branch-free (every address stays inside the window)
         uint32_t packed = 0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const int64_t x = w0 + 4 * L + e;
-            const uint32_t t = win[x];
-            uint32_t lit = t >> 4, ext1 = 0;
-            bool cx = false;
-            if (lit == 15) { const uint32_t b = win[x + 1]; cx = b == 255; lit += b; ext1 = 1; }
-            uint32_t ext2 = 0;
-            if ((t & 15) == 15) { const uint32_t b = win[x + 1 + ext1 + lit + 2]; cx = cx || b == 255; ext2 = 1; }
-            const uint32_t d = 1 + ext1 + lit + 2 + ext2;
-            packed |= ((cx || lit > 64 || d > 255) ? 0u : d) << (8 * e);
+            const uint32_t x = w0 + 4 * L + e;
+            const uint32_t t = win[x], b1 = win[x + 1];
+            const bool l15 = (t >> 4) == 15, m15 = (t & 15) == 15;
+            const uint32_t lit = (t >> 4) + (l15 ? b1 : 0u);
+            const uint32_t b2 = win[x + 3 + (l15 ? 1u : 0u) + lit];
+            const bool cx = (l15 && b1 == 255) || (m15 && b2 == 255) || lit > 64;
+            const uint32_t d = 3 + (l15 ? 1u : 0u) + lit + (m15 ? 1u : 0u);
+            packed |= (cx ? 0u : d) << (8 * e);
         }
         // 2. hop
         uint32_t startRel = 0, cnt = 0, cur = 0;
@@ -737,37 +736,36 @@ struct Dec {
             const uint32_t wv = rdlane(packed, (int)(cur >> 2));
             const uint32_t d = (wv >> ((cur & 3) * 8)) & 255u;
             if (d == 0) break;
-            if (L == cnt) startRel = cur;
+            startRel = (L == cnt) ? cur : startRel;
             cur += d;
             ++cnt;
         }
         if (cnt == 0) return 0;
-        // 3. fields
+        if (ST) acc[4] += 1;
+        // 3. fields (lane j = sequence j), branch-free
         const bool act = L < cnt;
-        const int64_t sw = w0 + startRel;   // window index of the token
-        uint32_t tok = 0, lit = 0, ext1 = 0, off = 0, mlen = 0, ext2 = 0;
-        if (act) {
-            tok = win[sw];
-            lit = tok >> 4;
-            if (lit == 15) { lit += win[sw + 1]; ext1 = 1; }
-            const int64_t ow = sw + 1 + ext1 + lit;
-            off = win[ow] | ((uint32_t)win[ow + 1] << 8);
-            mlen = (tok & 15) + kMinMatch;
-            if ((tok & 15) == 15) { mlen += win[ow + 2]; ext2 = 1; }
-        }
+        const uint32_t sw = w0 + (act ? startRel : 0u);
+        const uint32_t tok = win[sw], b1 = win[sw + 1];
+        const bool l15 = (tok >> 4) == 15, m15 = (tok & 15) == 15;
+        const uint32_t e1 = l15 ? 1u : 0u;
+        const uint32_t lit = (tok >> 4) + (l15 ? b1 : 0u);
+        const uint32_t ow = sw + 1 + e1 + lit;
+        const uint32_t off = win[ow] | ((uint32_t)win[ow + 1] << 8);
+        const uint32_t b2 = win[ow + 2];
+        const uint32_t e2 = m15 ? 1u : 0u;
+        const uint32_t mlen = (tok & 15) + kMinMatch + (m15 ? b2 : 0u);
         const uint32_t olen = act ? lit + mlen : 0u;
         const uint32_t incl = wave_scan_incl(olen);
         const int64_t oj = op + (int64_t)(incl - olen);   // sequence output start
         const int64_t ipT = ip + startRel + 1;            // just after the token
-        const int64_t lp = ipT + ext1;                    // literal start
+        const int64_t lp = ipT + e1;                      // literal start
         const int64_t om = oj + lit;                      // match output start
         // 4. fast-loop conditions (lz4 1.9.3, see decode_block)
-        bool ok = act && off != 0 && lit <= 64 && mlen <= 128 && (int64_t)incl <= 4096;
-        if ((tok >> 4) == 15) ok = ok && ipT < iend - 15 && ipT + 1 < iend - 15 && !(oj + lit > oend - 32) &&
-                                   !(lp + lit > iend - 32);
-        else ok = ok && !(ipT > iend - 17);
-        ok = ok && om - (int64_t)off >= 0;
-        if ((tok & 15) == 15) ok = ok && lp + lit + 3 < iend - kLastLiterals + 1;
+        bool ok = act && off != 0 && lit + mlen <= 128 && incl <= 4096;
+        ok = ok && (l15 ? (ipT < iend - 15 && ipT + 1 < iend - 15 && oj + lit <= oend - 32 && lp + lit <= iend - 32)
+                        : ipT <= iend - 17);
+        ok = ok && om >= (int64_t)off;
+        ok = ok && (!m15 || lp + lit + 3 < iend - kLastLiterals + 1);
         ok = ok && om + mlen < oend - 64;
         const uint64_t bad = ballot(act && !ok);
         const uint32_t nb = bad ? (uint32_t)(__ffsll((long long)bad) - 1) : cnt;
@@ -775,91 +773,80 @@ struct Dec {
         const bool in = L < nb;
         STAMP_ADD(0, ts);
         if (ST) acc[6] += nb;
-        // 5. copies.  Ring invariant: after flush_to(op) everything below op
-        // that may still be read from the ring lies in [op - kRing + 4096, op).
         flush_to(op);
-        WAVE_SYNC();
-        {   // literals (independent: window -> ring), 4 bytes per step
-            const uint32_t maxLit = wave_max(in ? lit : 0u);
-            const int64_t lw = lp - wlo;
-            for (uint32_t k = 0; k < maxLit; k += 4) {
-                uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
-                if (in && k < lit) b0 = win[lw + k];
-                if (in && k + 1 < lit) b1 = win[lw + k + 1];
-                if (in && k + 2 < lit) b2 = win[lw + k + 2];
-                if (in && k + 3 < lit) b3 = win[lw + k + 3];
-                if (in && k < lit) ring[(oj + k) & (kRing - 1)] = (uint8_t)b0;
-                if (in && k + 1 < lit) ring[(oj + k + 1) & (kRing - 1)] = (uint8_t)b1;
-                if (in && k + 2 < lit) ring[(oj + k + 2) & (kRing - 1)] = (uint8_t)b2;
-                if (in && k + 3 < lit) ring[(oj + k + 3) & (kRing - 1)] = (uint8_t)b3;
-            }
-        }
-        STAMP_ADD(1, ts);
+        // 5a. far matches (source older than the ring keeps): their output
+        // equals their source, so fetch it from HBM (independent loads) and
+        // drop it straight into the ring at the match's output position.
         const int64_t src = om - (int64_t)off;
-        const int64_t ringLo = op + 4096 - kRing;     // oldest position safely in the ring
-        const bool far = in && src < ringLo;          // then src + mlen < op: wholly older data
-        const uint64_t farMask = ballot(far);
-        if (farMask) {   // HBM sources: all loads independent, issued together
+        const int64_t ringLo = op + 4096 - kRing;
+        const bool far = in && src < ringLo;
+        if (ballot(far)) {
             if (completed < ringLo) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 completed = flushed;
             }
+            if (ST) acc[7] += __popcll(ballot(far));
             if (far) {
-                const uint32_t sh = (uint32_t)(src & 3);
-                g_cu32* q = (g_cu32*)(dst + (src - sh));
-                const uint32_t nw = (sh + mlen + 3) >> 2;   // dwords covering [src, src+mlen)
-                uint32_t wv[33];
+                // dst dword t covers ring positions A + 4t, A = om & ~3; its bytes
+                // come from src + (A + 4t - om) = S0 + 4t, S0 = src - (om & 3)
+                const int64_t A = om & ~int64_t(3);
+                const int64_t S0 = src - (om & 3);
+                const uint32_t r = (uint32_t)(S0 & 3);
+                g_cu32* q = (g_cu32*)(dst + (S0 - r));
+                const uint32_t nd = (uint32_t)((om + mlen - A + 3) >> 2);   // dst dwords, <= 33
+                uint32_t wv[34];
 #pragma unroll
-                for (int i = 0; i < 33; ++i) wv[i] = (uint32_t)i < nw ? q[i] : 0u;
+                for (int i = 0; i < 34; ++i)   // never below the slot start (block 0 starts the buffer)
+                    wv[i] = ((uint32_t)i <= nd && S0 - (int64_t)r + 4 * i >= 0) ? q[i] : 0u;
 #pragma unroll
-                for (int i = 0; i < 33; ++i) {
+                for (int t = 0; t < 33; ++t) {
+                    if ((uint32_t)t < nd) {
+                        const uint32_t v = __builtin_amdgcn_alignbyte(wv[t + 1], wv[t], r);
+                        const int64_t pos = A + 4 * t;
+                        if (pos >= om) {   // whole dword at or after the match start
+                            *(l_u32*)(ring + (pos & (kRing - 1))) = v;
+                        } else {           // first dword: keep bytes below om
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        const int64_t k = 4 * i + b - (int64_t)sh;   // output byte index
-                        if (k >= 0 && k < (int64_t)mlen) ring[(om + k) & (kRing - 1)] = (uint8_t)(wv[i] >> (8 * b));
+                            for (int bb = 0; bb < 4; ++bb)
+                                if (pos + bb >= om) ring[(pos + bb) & (kRing - 1)] = (uint8_t)(v >> (8 * bb));
+                        }
                     }
                 }
             }
         }
-        STAMP_ADD(3, ts);
-        uint64_t undone = ballot(in && !far);
-        const int64_t srcHi = min(src + (int64_t)mlen, om);
-        while (undone) {
-            WAVE_SYNC();
-            const int u = __ffsll((long long)undone) - 1;
-            const int64_t F = op + (int64_t)rdlane((uint32_t)(om - op), u);   // all output below F is final
-            const bool ready = ((undone >> L) & 1) && srcHi <= F;
-            const uint64_t rm = ballot(ready);
-            const uint32_t maxM = wave_max(ready ? mlen : 0u);
-            const bool wide = ballot(ready && off < 4) == 0;
-            if (wide) {
-                for (uint32_t k = 0; k < maxM; k += 4) {
-                    uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
-                    if (ready && k < mlen) b0 = ring[(src + k) & (kRing - 1)];
-                    if (ready && k + 1 < mlen) b1 = ring[(src + k + 1) & (kRing - 1)];
-                    if (ready && k + 2 < mlen) b2 = ring[(src + k + 2) & (kRing - 1)];
-                    if (ready && k + 3 < mlen) b3 = ring[(src + k + 3) & (kRing - 1)];
-                    if (ready && k < mlen) ring[(om + k) & (kRing - 1)] = (uint8_t)b0;
-                    if (ready && k + 1 < mlen) ring[(om + k + 1) & (kRing - 1)] = (uint8_t)b1;
-                    if (ready && k + 2 < mlen) ring[(om + k + 2) & (kRing - 1)] = (uint8_t)b2;
-                    if (ready && k + 3 < mlen) ring[(om + k + 3) & (kRing - 1)] = (uint8_t)b3;
-                    WAVE_SYNC();
-                }
-            } else {
-                for (uint32_t k = 0; k < maxM; ++k) {
-                    if (ready && k < mlen) ring[(om + k) & (kRing - 1)] = ring[(src + k) & (kRing - 1)];
-                    WAVE_SYNC();
-                }
-            }
-            undone &= ~rm;
-        }
         WAVE_SYNC();
+        STAMP_ADD(3, ts);
+        // 5b. sequences in order, whole wave per sequence: ONE LDS read (lanes
+        // pick window or ring; a far match's bytes are already in place) and
+        // ONE LDS write.  Overlapping matches (off < len) use k mod off.
+        const uint32_t lwin = (uint32_t)(lp - wlo);
+        for (uint32_t j = 0; j < nb; ++j) {
+            const uint32_t jlit = rdlane(lit, (int)j), jml = rdlane(mlen, (int)j), joff = rdlane(off, (int)j);
+            const uint32_t jlw = rdlane(lwin, (int)j);
+            const uint32_t jo = rdlane((uint32_t)(oj - op), (int)j);
+            const bool jfar = (ballot(far) >> j) & 1;
+            const uint32_t jtot = jlit + (jfar ? 0u : jml);
+            const uint32_t magic = joff < 64 ? (65536u + joff - 1) / joff : 0u;
+            for (uint32_t base = 0; base < jtot; base += 64) {
+                const uint32_t x = base + L;
+                uint32_t v = 0;
+                if (x < jtot) {
+                    if (x < jlit) v = win[jlw + x];
+                    else {
+                        const uint32_t k = x - jlit;
+                        const uint32_t kk = (joff >= 64 || k < joff) ? k : k - ((k * magic) >> 16) * joff;
+                        v = ring[(op + jo + jlit - joff + kk) & (kRing - 1)];
+                    }
+                    ring[(op + jo + x) & (kRing - 1)] = (uint8_t)v;
+                }
+                WAVE_SYNC();
+            }
+        }
         STAMP_ADD(2, ts);
         // advance past the last consumed sequence
-        const uint32_t last = nb - 1;
-        ip = ip + (int64_t)rdlane(startRel, (int)last) + 1 + rdlane(ext1, (int)last) + rdlane(lit, (int)last) + 2 +
-             rdlane(ext2, (int)last);
-        op = op + (int64_t)rdlane(incl, (int)last);
+        const int last = (int)nb - 1;
+        ip = ip + (int64_t)rdlane(startRel, last) + 1 + rdlane(e1, last) + rdlane(lit, last) + 2 + rdlane(e2, last);
+        op = op + (int64_t)rdlane(incl, last);
         return (int)nb;
     }
     // read_variable_length(); returns 0 ok, -1 initial error, -2 loop error
