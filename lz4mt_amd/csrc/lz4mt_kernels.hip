@@ -826,20 +826,33 @@ struct Dec {
             const uint32_t jo = rdlane((uint32_t)(oj - op), (int)j);
             const bool jfar = (ballot(far) >> j) & 1;
             const uint32_t jtot = jlit + (jfar ? 0u : jml);
-            const uint32_t magic = joff < 64 ? (65536u + joff - 1) / joff : 0u;
-            for (uint32_t base = 0; base < jtot; base += 64) {
-                const uint32_t x = base + L;
-                uint32_t v = 0;
-                if (x < jtot) {
-                    if (x < jlit) v = win[jlw + x];
-                    else {
-                        const uint32_t k = x - jlit;
-                        const uint32_t kk = (joff >= 64 || k < joff) ? k : k - ((k * magic) >> 16) * joff;
-                        v = ring[(op + jo + jlit - joff + kk) & (kRing - 1)];
+            const int64_t jo64 = op + jo;
+            if (jfar || joff >= jtot) {   // source wholly before the sequence: one fused pass
+                for (uint32_t base = 0; base < jtot; base += 64) {
+                    const uint32_t x = base + L;
+                    if (x < jtot) {
+                        const uint32_t v = x < jlit ? (uint32_t)win[jlw + x]
+                                                    : (uint32_t)ring[(jo64 + x - joff) & (kRing - 1)];
+                        ring[(jo64 + x) & (kRing - 1)] = (uint8_t)v;
                     }
-                    ring[(op + jo + x) & (kRing - 1)] = (uint8_t)v;
+                    WAVE_SYNC();
                 }
-                WAVE_SYNC();
+            } else {   // source overlaps the sequence itself: literal first, then the match (k mod off)
+                for (uint32_t base = 0; base < jlit; base += 64) {
+                    const uint32_t x = base + L;
+                    if (x < jlit) ring[(jo64 + x) & (kRing - 1)] = win[jlw + x];
+                    WAVE_SYNC();
+                }
+                const uint32_t magic = joff < 64 ? (65536u + joff - 1) / joff : 0u;
+                const int64_t jom = jo64 + jlit;
+                for (uint32_t base = 0; base < jml; base += 64) {
+                    const uint32_t k = base + L;
+                    if (k < jml) {
+                        const uint32_t kk = (joff >= 64 || k < joff) ? k : k - ((k * magic) >> 16) * joff;
+                        ring[(jom + k) & (kRing - 1)] = ring[(jom - joff + kk) & (kRing - 1)];
+                    }
+                    WAVE_SYNC();
+                }
             }
         }
         STAMP_ADD(2, ts);
