@@ -803,12 +803,13 @@ struct Dec {
                     if ((uint32_t)t < nd) {
                         const uint32_t v = __builtin_amdgcn_alignbyte(wv[t + 1], wv[t], r);
                         const int64_t pos = A + 4 * t;
-                        if (pos >= om) {   // whole dword at or after the match start
+                        if (pos >= om && pos + 4 <= om + mlen) {   // whole dword inside the match
                             *(l_u32*)(ring + (pos & (kRing - 1))) = v;
-                        } else {           // first dword: keep bytes below om
+                        } else {   // edge dword: only [om, om+mlen) (a neighbour's far bytes may sit beside it)
 #pragma unroll
                             for (int bb = 0; bb < 4; ++bb)
-                                if (pos + bb >= om) ring[(pos + bb) & (kRing - 1)] = (uint8_t)(v >> (8 * bb));
+                                if (pos + bb >= om && pos + bb < om + mlen)
+                                    ring[(pos + bb) & (kRing - 1)] = (uint8_t)(v >> (8 * bb));
                         }
                     }
                 }
