@@ -28,6 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import lz4mt_amd as L  # noqa: E402
+from lz4mt_amd import dist as D  # noqa: E402
 
 GiB = float(1 << 30)
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -106,7 +107,6 @@ def main():
     ws = L.compress_workspace(n, sd, device=dev)
     out = torch.empty(n, dtype=torch.uint8, device=dev)
     fsz = torch.zeros(2, dtype=torch.int64, device=dev)
-    gathered = None
 
     def compress():
         r = L.lib.lz4mtHipCompressFrameAsync(
@@ -116,18 +116,13 @@ def main():
         if r != 0:
             raise L.Lz4MtError(r, "compress")
 
+    stitched = {"len": 0}
+
     def gather_to_root(flen):
-        nonlocal gathered
-        sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-        dist.all_gather(sizes, fsz[:1])
-        mx = int(max(int(s.item()) for s in sizes))
-        if rank == 0:
-            if gathered is None or gathered.numel() < world * mx:
-                gathered = torch.empty(world * mx, dtype=torch.uint8, device=dev)
-            parts = [gathered[i * mx:(i + 1) * mx] for i in range(world)]
-            dist.gather(frame_buf[:mx], parts, dst=0)
-        else:
-            dist.gather(frame_buf[:mx], None, dst=0)
+        # one frame for the whole 8N GiB stream on rank 0 (lz4mt_amd/dist.py)
+        full = D.gather_frame(frame_buf, flen, dst=0)
+        if full is not None:
+            stitched["len"] = full.numel()
 
     def decompress(flen):
         osz = ctypes.c_uint64(0)
@@ -213,7 +208,8 @@ def main():
                        "bytes_per_gpu": n, "block_bytes": bm, "parallelism": f"block-sharded x{world}"
                                                                                 + (", RCCL gather" if world > 1 else "")},
             "compress_GiBps": round(comp_gibps, 3), "decompress_GiBps": round(decomp_gibps, 3),
-            "ratio": round(n / frame_len, 4), "frame_bytes": frame_len, "roundtrip_ok": ok,
+            "ratio": round(n / frame_len, 4), "frame_bytes": frame_len,
+            "stitched_frame_bytes": stitched["len"] if world > 1 else frame_len, "roundtrip_ok": ok,
             "roofline": roof, "decode_roofline": dec_roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

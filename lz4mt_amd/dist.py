@@ -1,0 +1,168 @@
+"""Block-sharded multi-GPU frames.
+
+lz4mt frames with independent blocks (FLG bit 5, reference
+src/lz4mt.cpp:914-918) are a header, a run of self-delimiting block records
+(u32 size word | payload | [u32 block XXH32]) and an EOS word
+(src/lz4mt.cpp:418-428, 923-925).  A record depends only on its own block,
+so a stream cut at block boundaries can be compressed shard by shard on
+different GPUs and the record runs concatenated: the result is byte-for-byte
+the frame one process would write for the whole stream.  The one thing that
+does not shard is the stream (content) checksum, a single serial XXH32 chain
+(SURVEY.md §0.5), so sharded frames require FLG.2 = 0 (``-Sx``).
+
+One process per GPU (torch.distributed; backend "nccl" is RCCL on ROCm,
+"gloo" for CPU tests).  Compress: each rank encodes its contiguous block
+range locally, then the compressed record runs are gathered to the root (the
+only exchange step of the path).  Decompress: the host walks the size words
+(O(blocks)) and hands each rank a sub-frame of whole records -- no
+collective on the data path.
+"""
+import struct
+
+import torch
+import torch.distributed as dist
+
+MAGIC = 0x184D2204
+SKIPPABLE_MIN, SKIPPABLE_MAX = 0x184D2A50, 0x184D2A5F
+EOS = b"\x00\x00\x00\x00"
+
+
+def block_bytes(block_max_id):
+    """getBlockSize (reference src/lz4mt.cpp:34-37)."""
+    if not 4 <= block_max_id <= 7:
+        raise ValueError(f"block maximum size id {block_max_id} not in [4, 7]")
+    return 1 << (8 + 2 * block_max_id)
+
+
+def shard_blocks(n_total, bm, world, rank):
+    """Contiguous block range of ``rank``: returns (byte offset, byte length, first block, block count).
+
+    Blocks [0, nb) are split as evenly as possible; the last (short) block
+    goes to the last rank that owns blocks.
+    """
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad world/rank")
+    nb = (n_total + bm - 1) // bm
+    per, rem = divmod(nb, world)
+    first = rank * per + min(rank, rem)
+    count = per + (1 if rank < rem else 0)
+    off = min(first * bm, n_total)
+    end = min((first + count) * bm, n_total)
+    return off, end - off, first, count
+
+
+def header_length(flg):
+    """Frame header bytes after the magic word: FLG, BD, [u64 size], [u32 dict], HC (src/lz4mt.cpp:335-369)."""
+    return 3 + (8 if flg & 0x08 else 0) + (4 if flg & 0x01 else 0)
+
+
+def _frame_layout(head):
+    """(header length incl. magic, FLG) from the first bytes of a frame."""
+    if len(head) < 6 or struct.unpack_from("<I", head, 0)[0] != MAGIC:
+        raise ValueError("not an lz4mt frame (magic)")
+    flg = head[4]
+    if not flg & 0x20:
+        raise ValueError("block-dependent frames (-BD) do not shard")
+    if flg & 0x04:
+        raise ValueError("a stream checksum (FLG.2) is one serial chain and cannot be sharded; use -Sx")
+    return 4 + header_length(flg), flg
+
+
+def frame_records(frame, frame_len=None):
+    """(header length, records length) of a single -Sx frame held in a uint8 tensor or bytes."""
+    frame_len = len(frame) if frame_len is None else int(frame_len)
+    head = bytes(frame[:20].cpu().numpy().tobytes()) if isinstance(frame, torch.Tensor) else bytes(frame[:20])
+    hdr, _ = _frame_layout(head)
+    rec = frame_len - hdr - 4
+    if rec < 0:
+        raise ValueError("frame shorter than header + EOS")
+    return hdr, rec
+
+
+def gather_frame(frame, frame_len, dst=0, group=None):
+    """Gathers every rank's shard frame into ONE frame on ``dst``.
+
+    ``frame`` is this rank's uint8 tensor (device tensor under RCCL, CPU under
+    gloo) holding a complete -Sx frame of ``frame_len`` bytes.  Ranks must
+    hold consecutive block ranges in rank order (``shard_blocks``) and equal
+    frame headers.  Returns the stitched frame on ``dst`` (header of rank 0,
+    record runs in rank order, EOS) and None elsewhere.
+
+    Exchange: one all_gather of the record-run lengths (8 B per rank), then
+    grouped point-to-point sends of each rank's record run straight into its
+    final place in the root's frame (no padding, no staging copy).  This is
+    the path's only collective; it is bound by the root's inbound xGMI links.
+    """
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    hdr, rec = frame_records(frame, frame_len)
+    dev = frame.device
+    sizes = torch.tensor([rec], dtype=torch.int64, device=dev)
+    all_sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(all_sizes, sizes, group=group)
+    lens = [int(s.item()) for s in all_sizes]
+    peer = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+    if rank == dst:
+        out = torch.empty(hdr + sum(lens) + 4, dtype=torch.uint8, device=dev)
+        out[:hdr] = frame[:hdr]
+        ops, pos = [], hdr
+        for r, n in enumerate(lens):
+            if r == rank:
+                out[pos:pos + n] = frame[hdr:hdr + n]
+            elif n:
+                ops.append(dist.P2POp(dist.irecv, out[pos:pos + n], peer(r), group))
+            pos += n
+        out[pos:pos + 4] = 0
+        for w in (dist.batch_isend_irecv(ops) if ops else []):
+            w.wait()
+        return out
+    if rec:
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, frame[hdr:hdr + rec], peer(dst), group)]):
+            w.wait()
+    return None
+
+
+def walk_records(frame, block_checksum=None):
+    """Host walk of the size words of one -Sx frame (bytes): returns (header length, [(start, end), ...], end).
+
+    Mirrors the block loop of decompress() (src/lz4mt.cpp:685-727): a size
+    word of 0 ends the frame; bit 31 marks a raw block; a checksum word
+    follows the payload when FLG.4 is set.
+    """
+    frame = bytes(frame)
+    hdr, flg = _frame_layout(frame[:20])
+    bck = bool(flg & 0x10) if block_checksum is None else block_checksum
+    recs, pos = [], hdr
+    while True:
+        if pos + 4 > len(frame):
+            raise ValueError("truncated frame (no EOS)")
+        w = struct.unpack_from("<I", frame, pos)[0]
+        if w == 0:
+            return hdr, recs, pos + 4
+        end = pos + 4 + (w & 0x7FFFFFFF) + (4 if bck else 0)
+        if end > len(frame):
+            raise ValueError("truncated block record")
+        recs.append((pos, end))
+        pos = end
+
+
+def split_frame(frame, world):
+    """Splits one -Sx frame (bytes) into ``world`` frames of contiguous whole records.
+
+    Each piece is a valid frame (same header, its records, EOS) that decodes
+    to the matching slice of the original content; piece r holds the block
+    range ``shard_blocks`` assigns to rank r.  This is the host side of the
+    decompress scatter.
+    """
+    frame = bytes(frame)
+    hdr, recs, _ = walk_records(frame)
+    head = frame[:hdr]
+    nb = len(recs)
+    out = []
+    for r in range(world):
+        per, rem = divmod(nb, world)
+        first = r * per + min(r, rem)
+        count = per + (1 if r < rem else 0)
+        body = frame[recs[first][0]:recs[first + count - 1][1]] if count else b""
+        out.append(head + body + EOS)
+    return out

@@ -1,0 +1,112 @@
+"""Multi-process (gloo, world_size 2) tests of the block-sharded frame path
+(lz4mt_amd/dist.py).  CPU only: each rank compresses its
+block range with the oracle (the checker), the record runs are gathered
+over torch.distributed, and the stitched frame must equal the oracle's frame
+of the whole stream byte for byte."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from lz4mt_amd import dist as D
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n, block_id, bck, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data = oracle.gen_synthetic(n, 42)
+        bm = D.block_bytes(block_id)
+        off, ln, _, _ = D.shard_blocks(n, bm, world, rank)
+        p = oracle.params(block_id, stream_checksum=False, block_checksum=bck)
+        local = oracle.compress_frame(data[off:off + ln], p)
+        t = torch.frombuffer(bytearray(local + b"\xAA" * 13), dtype=torch.uint8)   # slack past the frame end
+        full = D.gather_frame(t, len(local))
+        if rank == 0:
+            q.put(bytes(full.numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, n, block_id, bck):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, block_id, bck, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return got
+
+
+@pytest.mark.parametrize("n,block_id,bck", [(17 * 65536 + 12345, 4, True), (3 * 262144, 5, False)])
+def test_gather_stitches_whole_stream_frame(n, block_id, bck):
+    got = _run(2, n, block_id, bck)
+    want = oracle.compress_frame(oracle.gen_synthetic(n, 42), oracle.params(block_id, False, bck))
+    assert got == want
+
+
+def test_gather_more_ranks_than_blocks():
+    # 3 ranks, 2 blocks: one rank owns an empty shard (a header + EOS frame)
+    n = 65536 + 100
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 3, port, n, 4, True, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == oracle.compress_frame(oracle.gen_synthetic(n, 42), oracle.params(4, False, True))
+
+
+def test_shard_plan_covers_stream():
+    for n, bm, world in [(0, 65536, 2), (1, 65536, 3), (10 * 65536, 65536, 4), (10 * 65536 + 7, 65536, 8),
+                         (8 << 30, 4 << 20, 8)]:
+        pos = 0
+        for r in range(world):
+            off, ln, first, count = D.shard_blocks(n, bm, world, r)
+            assert off == pos and (off % bm == 0 or off == n)
+            assert ln <= count * bm
+            pos += ln
+        assert pos == n
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5])
+def test_split_frame_decodes_to_slices(world):
+    n = 9 * 65536 + 333
+    data = oracle.gen_synthetic(n, 7)
+    frame = oracle.compress_frame(data, oracle.params(4, False, True))
+    parts = D.split_frame(frame, world)
+    out = b""
+    for r, part in enumerate(parts):
+        rc, dec = oracle.decompress_frame(part, n + 65536)
+        assert rc == 0
+        off, ln, _, _ = D.shard_blocks(n, 65536, world, r)
+        assert dec == data[off:off + ln]
+        out += dec
+    assert out == data
+    # and the pieces stitch back into the original frame
+    hdr, _, _ = D.walk_records(frame)
+    assert frame[:hdr] + b"".join(p[hdr:-4] for p in parts) + D.EOS == frame
+
+
+def test_stream_checksum_frames_refuse_to_shard():
+    frame = oracle.compress_frame(oracle.gen_synthetic(70000, 1), oracle.params(4, True, False))
+    with pytest.raises(ValueError, match="serial"):
+        D.split_frame(frame, 2)
