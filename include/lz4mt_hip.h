@@ -93,10 +93,12 @@ int lz4mtHipGetTimings(float* ms4);
 /* ---- 4. diagnostics ----------------------------------------------------- */
 /* Runs s_memtime-stamped twins of the encode / decode kernels (never the
  * product launch) and sums per-phase shader cycles over all blocks.
- * encode: [hash, table+dedup, verify+table writes, catch-up, count, emit,
- * windows, loop overhead]; decode: [parse, literal copy, ring match copy,
- * HBM match copy, -, total, matches, HBM matches]. */
-int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* stats8, void* stream);
+ * encode (16 slots): [hash, table+dedup, candidate check, round issue,
+ * literal staging, round wait, table writes, count, emit, loop overhead,
+ * windows, tag aliases, tag-candidate winners, -, -, -];
+ * decode (8 slots): [parse, literal copy, ring match copy, HBM match copy,
+ * batches, total, matches, HBM matches]. */
+int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* stats16, void* stream);
 int lz4mtHipDebugDecodeStats(const void* d_frame, uint64_t frameSize, uint64_t* stats8, void* stream);
 
 #ifdef __cplusplus

@@ -530,7 +530,7 @@ extern "C" int lz4mtHipGetTimings(float* ms4) {
 // ===========================================================================
 // 4. diagnostics: phase cycle counts of the encode / decode kernels
 // ===========================================================================
-extern "C" int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* stats8,
+extern "C" int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* stats16,
                                         void* stream) {
     if (!have_device() || blockSize == 0) return -1;
     const hipStream_t st = static_cast<hipStream_t>(stream);
@@ -541,15 +541,15 @@ extern "C" int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t 
     int rc = -1;
     if (hipMalloc(reinterpret_cast<void**>(&slots), nb * blockSize + 64) == hipSuccess &&
         hipMalloc(reinterpret_cast<void**>(&cs), nb * 4 + 4) == hipSuccess &&
-        hipMalloc(reinterpret_cast<void**>(&dst), nb * 64 + 64) == hipSuccess &&
+        hipMalloc(reinterpret_cast<void**>(&dst), nb * 128 + 64) == hipSuccess &&
         launch_encode_stats(static_cast<const uint8_t*>(d_src), n, blockSize, (uint32_t)nb, slots, cs, dst, st) ==
             hipSuccess) {
-        std::vector<uint64_t> h(nb * 8);
-        if (hipMemcpyAsync(h.data(), dst, nb * 64, hipMemcpyDeviceToHost, st) == hipSuccess &&
+        std::vector<uint64_t> h(nb * 16);
+        if (hipMemcpyAsync(h.data(), dst, nb * 128, hipMemcpyDeviceToHost, st) == hipSuccess &&
             hipStreamSynchronize(st) == hipSuccess) {
-            for (int i = 0; i < 8; ++i) stats8[i] = 0;
+            for (int i = 0; i < 16; ++i) stats16[i] = 0;
             for (uint64_t b = 0; b < nb; ++b)
-                for (int i = 0; i < 8; ++i) stats8[i] += h[b * 8 + i];
+                for (int i = 0; i < 16; ++i) stats16[i] += h[b * 16 + i];
             rc = 0;
         }
     }

@@ -106,6 +106,17 @@ __device__ __forceinline__ uint32_t lz4_hash(uint32_t w0, uint32_t w1) {
     return (uint32_t)(((v << 24) * 889523592379ull) >> 52);
 }
 
+// u32-table entries (blocks >= 65547 B, at most 4 MiB = 2^22 positions) keep
+// the position in the low 22 bits and a 10-bit tag of the 4 bytes AT that
+// position in the high bits.  LZ4 accepts a candidate only if those 4 bytes
+// equal the probe's, so a tag mismatch proves "no match" without touching
+// memory; only tag-equal candidates outside the LDS ring cost a global load
+// (then folded into the count round trip).  Exact: every accepted match is
+// still confirmed by a full 4-byte compare.
+constexpr uint32_t kPosBits = 22;
+constexpr uint32_t kPosMask = (1u << kPosBits) - 1u;
+__device__ __forceinline__ uint32_t cand_tag(uint32_t w0) { return (w0 * 0x85EBCA77u) >> kPosBits; }
+
 // One window of up to 64 probes.  Lane roles: [INSERT][TEST] SEARCH...
 //   INSERT: table insertion only (position 0 at block start, ip-2 after a match)
 //   TEST:   LZ4's "test next position" probe right after a match
@@ -275,7 +286,7 @@ __device__ __forceinline__ void put_head(OutView& O, uint32_t op, uint32_t lit, 
     put_ext(O, op + 1, ext_len(lit), lit >= 15 ? (lit - 15) % 255 : 0);
 }
 
-template <bool U16, bool ST>
+template <bool U16, bool TAG, bool ST>
 __device__ int32_t encode_block(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
                                 l_u32* __restrict__ Traw, l_u8* __restrict__ S, l_u32* __restrict__ ringE,
                                 l_u8* __restrict__ outRing, uint64_t* acc) {
@@ -290,8 +301,11 @@ __device__ int32_t encode_block(g_cu8* __restrict__ s, uint32_t n, g_u8* __restr
     }
     l_u16* T16 = (l_u16*)Traw;
     {
+        // a fresh entry is position 0 -- a real candidate in LZ4 1.9.3 --
+        // so tagged tables start with the tag of the bytes at 0
+        const uint32_t t0 = TAG ? (cand_tag(ld32u(s)) << kPosBits) : 0u;
         l_u4* T4 = (l_u4*)Traw;
-        for (uint32_t i = L; i < 1024; i += 64) T4[i] = (v4u){0, 0, 0, 0};
+        for (uint32_t i = L; i < 1024; i += 64) T4[i] = (v4u){t0, t0, t0, t0};
     }
     SrcView V{s, n, ringE, 0, 0, 0, 0};
     V.init();
@@ -306,8 +320,8 @@ __device__ int32_t encode_block(g_cu8* __restrict__ s, uint32_t n, g_u8* __restr
         Win W{1, 0, 0, 0, 1, 0};  // T[h(0)] = 0; search from ip = 1
         for (;;) {
             // ---------------- one probe window ----------------
-            if (ST) acc[6] += 1;
-            STAMP_ADD(7, ts);
+            if (ST) acc[10] += 1;
+            STAMP_ADD(9, ts);
             const uint32_t ns = W.hasIns + W.hasTest;
             const bool isIns = L < W.hasIns;
             const bool isTest = !isIns && L < ns;
@@ -326,6 +340,7 @@ __device__ int32_t encode_block(g_cu8* __restrict__ s, uint32_t n, g_u8* __restr
                 if (!U16) w1 = V.rd4(p + 4);
             }
             const uint32_t h = live ? lz4_hash<U16>(w0, w1) : 0u;
+            const uint32_t mytag = TAG ? cand_tag(w0) : 0u;
             STAMP_ADD(0, ts);
             // duplicate-hash detection inside the window (aliasing of the
             // scratch index only costs an extra group iteration)
@@ -347,26 +362,82 @@ __device__ int32_t encode_block(g_cu8* __restrict__ s, uint32_t n, g_u8* __restr
                 }
                 pending &= ~m;
             }
-            const uint32_t cand = pred >= 0 ? W.pos((uint32_t)pred) : told;
+            const uint32_t cand = pred >= 0 ? W.pos((uint32_t)pred) : (TAG ? (told & kPosMask) : told);
             STAMP_ADD(1, ts);
-            bool ok = false;
+            // ok: verified match (4-byte compare); maybe: tag-equal table
+            // candidate outside the ring, confirmed in the count round trip
+            bool ok = false, maybe = false;
             if (live && !isIns && !term) {
                 const bool distok = U16 || (cand + kDistMax >= p);
-                if (distok) ok = (V.rd4(cand) == w0);
+                if (distok) {
+                    if (TAG && pred < 0 && !V.in_ring(cand, 4)) maybe = (told >> kPosBits) == mytag;
+                    else ok = (V.rd4(cand) == w0);
+                }
             }
-            const uint64_t sm = ballot(live && (term || ok));
-            const int w = sm ? __ffsll((long long)sm) - 1 : 64;
-            const bool wTerm = (w < 64) && ((ballot(term) >> w) & 1);
+            uint64_t sm = ballot(live && (term || ok || maybe));
+            const uint64_t mm = ballot(maybe), tmk = ballot(term);
+            STAMP_ADD(2, ts);
+            // resolve the first stop; a tag-equal lane issues the count round
+            // (with its 4-byte check) and drops out if the check fails
+            int w;
+            uint32_t ip = 0, cd = 0, maxb = 0, lim = 0, lit0 = 0;
+            bool wasTest = false, early = false, beq = false;
+            uint32_t eqb = 0;
+            for (;;) {
+                w = sm ? __ffsll((long long)sm) - 1 : 64;
+                if (w == 64 || ((tmk >> w) & 1)) break;
+                ip = rdlane(p, w);
+                cd = rdlane(cand, w);
+                wasTest = (ballot(isTest) >> w) & 1;
+                // Catch-up and forward count in one round: with back = catch-up
+                // length, LZ4_count from the caught-up position equals
+                // back + count from ip+4 (the skipped bytes are known equal).
+                maxb = wasTest ? 0u : min(ip - anchor, cd);
+                lim = matchlimit - (ip + kMinMatch);
+                V.cover(min(ip + kMinMatch + 256, n));
+                // round-0 operands (the cd side is the global round trip)
+                const bool needV = (mm >> w) & 1;
+                uint32_t vx = 0;
+                if (needV && L == 0) vx = ld32u(s + cd) ^ rdlane(w0, w);
+                beq = false;
+                if (L + 1 <= maxb) beq = V.rd1(ip - L - 1) == V.rd1(cd - L - 1);
+                eqb = 0;
+                if (4 * L < lim) {
+                    const uint32_t x = V.rd4(ip + kMinMatch + 4 * L) ^ V.rd4(cd + kMinMatch + 4 * L);
+                    eqb = x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u;
+                    eqb = min(eqb, lim - 4 * L);
+                }
+                STAMP_ADD(3, ts);
+                if (ST) acc[12] += (mm >> w) & 1;
+                // while those loads fly: stage the literals assuming no catch-up
+                lit0 = ip - anchor;
+                early = lit0 <= 256 && op + 1 + ext_len(lit0) + lit0 + 64 <= O.flushed + kOutRing;
+                if (early) stage_lits(V, O, anchor, 0, lit0, op + 1 + ext_len(lit0), false, 0);
+                STAMP_ADD(4, ts);
+                if (needV && (ballot(L == 0 && vx != 0) & 1)) {   // tag alias: not a match
+                    if (ST) acc[11] += 1;
+                    sm &= ~(1ull << w);
+                    STAMP_ADD(5, ts);
+                    continue;
+                }
+                if (ST) {   // round trip of the count loads (waited here)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                STAMP_ADD(5, ts);
+                break;
+            }
+            const bool wTerm = (w < 64) && ((tmk >> w) & 1);
             const int wlim = (w == 64) ? 63 : (wTerm ? w - 1 : w);
             // table writes: last member of each hash group among lanes <= wlim
             if (wlim >= 0 && live && (int)L <= wlim) {
                 const uint64_t later = gmask & ~mask_le(L) & mask_le((uint32_t)wlim);
                 if (!later) {
-                    if (U16) T16[h] = (uint16_t)p; else Traw[h] = p;
+                    if (U16) T16[h] = (uint16_t)p;
+                    else Traw[h] = TAG ? (p | (mytag << kPosBits)) : p;
                 }
             }
             WAVE_SYNC();
-            STAMP_ADD(2, ts);
+            STAMP_ADD(6, ts);
             if (w == 64) {  // no stop: continue the search
                 W.k0 += 64 - ns;
                 W.hasIns = 0; W.hasTest = 0;
@@ -375,29 +446,6 @@ __device__ int32_t encode_block(g_cu8* __restrict__ s, uint32_t n, g_u8* __restr
             if (wTerm) goto last_literals;
 
             // ---------------- match found ----------------
-            const uint32_t ip = rdlane(p, w);
-            const uint32_t cd = rdlane(cand, w);
-            const bool wasTest = (ballot(isTest) >> w) & 1;
-            // Catch-up and forward count in one round: with back = catch-up
-            // length, LZ4_count from the caught-up position equals
-            // back + count from ip+4 (the skipped bytes are known equal).
-            const uint32_t maxb = wasTest ? 0u : min(ip - anchor, cd);
-            const uint32_t lim = matchlimit - (ip + kMinMatch);
-            V.cover(min(ip + kMinMatch + 256, n));
-            // round-0 operands (the cd side is the global round trip)
-            bool beq = false;
-            if (L + 1 <= maxb) beq = V.rd1(ip - L - 1) == V.rd1(cd - L - 1);
-            uint32_t eqb = 0;
-            if (4 * L < lim) {
-                const uint32_t x = V.rd4(ip + kMinMatch + 4 * L) ^ V.rd4(cd + kMinMatch + 4 * L);
-                eqb = x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u;
-                eqb = min(eqb, lim - 4 * L);
-            }
-            // while those loads fly: stage the literals assuming no catch-up
-            const uint32_t lit0 = ip - anchor;
-            const bool early = lit0 <= 256 && op + 1 + ext_len(lit0) + lit0 + 64 <= O.flushed + kOutRing;
-            if (early) stage_lits(V, O, anchor, 0, lit0, op + 1 + ext_len(lit0), false, 0);
-            STAMP_ADD(3, ts);
             uint32_t back = 0, mc = 0;
             bool backDone = maxb == 0, cntDone = false;
             for (;;) {
@@ -428,7 +476,7 @@ __device__ int32_t encode_block(g_cu8* __restrict__ s, uint32_t n, g_u8* __restr
                     eqb = min(eqb, lim - rel);
                 }
             }
-            STAMP_ADD(4, ts);
+            STAMP_ADD(7, ts);
             const uint32_t mcf = mc + back;          // LZ4_count from the caught-up start + 4
             const uint32_t lit = lit0 - back;
             const uint32_t litExt = ext_len(lit);
@@ -455,7 +503,7 @@ __device__ int32_t encode_block(g_cu8* __restrict__ s, uint32_t n, g_u8* __restr
             op = litPos + lit + 2 + mlExt;
             WAVE_SYNC();
             O.flush_to(op);
-            STAMP_ADD(5, ts);
+            STAMP_ADD(8, ts);
             const uint32_t ipe = ip + kMinMatch + mc;  // = caught-up start + mcf + 4
             anchor = ipe;
             if (ipe >= mflimitP1) goto last_literals;
@@ -475,11 +523,291 @@ last_literals : {
     return (int32_t)op;
 }
 
+// ---------------------------------------------------------------------------
+// Lean encoder for the frame path: tagged u32 table, 65547 <= n <= 4 MiB.
+// Same parse and bytes as encode_block (LZ4 1.9.3); the
+// window is organised around ONE global round trip:
+//   hash inputs   unaligned ds_read_b64 from a mirrored 2 KiB source ring
+//                 (global loads when the window spans more than 1 KiB)
+//   candidates    in-window predecessor: its bytes via ds_bpermute (exact);
+//                 table entry: distance + 10-bit tag filter
+//   round trip    verify word, both sides of the forward count, catch-up
+//                 bytes and the literal bytes, all issued together
+//   emit          coalesced byte stores straight into the block slot
+// ---------------------------------------------------------------------------
+typedef const __attribute__((address_space(1))) uint32_t __attribute__((aligned(1))) g_cu32u;
+typedef const __attribute__((address_space(1))) uint64_t __attribute__((aligned(1))) g_cu64u;
+typedef __attribute__((address_space(3))) uint64_t __attribute__((aligned(1))) l_u64u;
+typedef __attribute__((address_space(3))) uint64_t l_u64;
+
+constexpr uint32_t kSR = 2048;        // source ring bytes
+constexpr uint32_t kSRMirror = 64;    // ring[kSR .. kSR+64) mirrors ring[0 .. 64)
+
+__device__ __forceinline__ uint32_t gld4u(g_cu8* p) { return *(g_cu32u*)p; }
+__device__ __forceinline__ uint64_t gld8u(g_cu8* p) { return *(g_cu64u*)p; }
+
+struct SrcRing {
+    g_cu8* s;
+    uint32_t n;
+    l_u8* r;          // kSR + kSRMirror bytes
+    uint32_t B;       // ring holds src[B, B + kSR), B a multiple of 512
+    uint32_t pfPos;   // chunk prefetched into pf
+    uint64_t pf;
+
+    __device__ __forceinline__ uint64_t fetch(uint32_t c) const {
+        const uint32_t pos = c + 8 * laneid();
+        if (pos + 8 <= n) return gld8u(s + pos);
+        uint64_t v = 0;
+        for (uint32_t i = 0; i < 8; ++i)
+            if (pos + i < n) v |= (uint64_t)s[pos + i] << (8 * i);
+        return v;
+    }
+    __device__ __forceinline__ void store(uint32_t c, uint64_t v) {
+        const uint32_t o = (c & (kSR - 1)) + 8 * laneid();
+        *(l_u64*)(r + o) = v;
+        if (o < kSRMirror) *(l_u64*)(r + kSR + o) = v;
+    }
+    __device__ __forceinline__ void init() {
+        B = 0;
+        for (uint32_t c = 0; c < kSR; c += 512) store(c, fetch(c));
+        pfPos = kSR;
+        pf = fetch(pfPos);
+        WAVE_SYNC();
+    }
+    // make [lo, hi) readable (requires hi - lo <= 1024 and lo >= B)
+    __device__ __forceinline__ void cover(uint32_t hi) {
+        if (hi <= B + kSR) return;
+        const uint32_t nb = (hi - kSR + 511) & ~511u;
+        WAVE_SYNC();
+        for (uint32_t c = (nb > B + kSR ? nb : B + kSR); c < nb + kSR; c += 512) store(c, c == pfPos ? pf : fetch(c));
+        B = nb;
+        pfPos = B + kSR;
+        pf = fetch(pfPos);   // next advance's chunk, in flight
+        WAVE_SYNC();
+    }
+    __device__ __forceinline__ uint64_t rd8(uint32_t pos) const { return *(l_u64u*)(r + (pos & (kSR - 1))); }
+};
+
+template <bool ST>
+__device__ int32_t encode_block_t(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
+                                  l_u32* __restrict__ T, l_u8* __restrict__ S, l_u8* __restrict__ R, uint64_t* acc) {
+    const uint32_t L = laneid();
+    uint64_t ts = STAMP_T();
+    const uint32_t bound = n + n / 255 + 16;
+    const bool limited = cap < bound;
+    {
+        const uint32_t t0 = cand_tag(gld4u(s)) << kPosBits;   // fresh entry = position 0 (a real candidate)
+        for (uint32_t i = L; i < 1024; i += 64) ((l_u4*)T)[i] = (v4u){t0, t0, t0, t0};
+    }
+    SrcRing V{s, n, R, 0, 0, 0};
+    V.init();
+    const uint32_t mflimitP1 = n - kMfLimit + 1;
+    const uint32_t matchlimit = n - kLastLiterals;
+    uint32_t anchor = 0, op = 0;
+    Win W{1, 0, 0, 0, 1, 0};   // T[h(0)] = 0; search from ip = 1
+    for (;;) {
+        if (ST) acc[10] += 1;
+        STAMP_ADD(9, ts);
+        const uint32_t ns = W.hasIns + W.hasTest;
+        const bool isIns = L < W.hasIns;
+        const bool isSearch = L >= ns;
+        const uint32_t k = W.k0 + (L - ns);
+        const uint32_t p = W.pos(L);
+        const bool live = !isSearch || p <= mflimitP1;
+        const bool term = isSearch && live && (p + probe_step(k) > mflimitP1);
+        // hash inputs: bytes [p, p+8)
+        const uint32_t lo = W.pos(0);
+        const uint32_t plast = W.pos(63);
+        const uint32_t hi = (plast < mflimitP1 ? plast : mflimitP1) + 8;
+        uint64_t v8 = 0;
+        if (hi - lo <= 1024) {
+            V.cover(hi);
+            v8 = V.rd8(p);
+        } else if (live) {
+            v8 = gld8u(s + p);
+        }
+        const uint32_t w0 = (uint32_t)v8;
+        const uint32_t h = live ? lz4_hash<false>(w0, (uint32_t)(v8 >> 32)) : 0u;
+        const uint32_t mytag = cand_tag(w0);
+        STAMP_ADD(0, ts);
+        S[h & (kDedup - 1)] = (uint8_t)L;
+        const uint32_t told = T[h];
+        WAVE_SYNC();
+        const uint32_t sv = S[h & (kDedup - 1)];
+        uint64_t pending = ballot(live && sv != L);
+        int pred = -1;
+        uint64_t gmask = 1ull << L;
+        while (pending) {   // one iteration per group of equal hashes
+            const int leader = __ffsll((long long)pending) - 1;
+            const uint32_t key = rdlane(h, leader);
+            const uint64_t m = ballot(live && h == key);
+            if ((m >> L) & 1) {
+                gmask = m;
+                const uint64_t below = m & ((1ull << L) - 1ull);
+                pred = below ? 63 - __clzll((long long)below) : -1;
+            }
+            pending &= ~m;
+        }
+        const uint32_t pw = (uint32_t)__builtin_amdgcn_ds_bpermute((pred < 0 ? 0 : pred) * 4, (int)w0);
+        const uint32_t cand = pred >= 0 ? W.pos((uint32_t)pred) : (told & kPosMask);
+        STAMP_ADD(1, ts);
+        bool ok = false, maybe = false;
+        if (live && !isIns && !term && cand + kDistMax >= p) {
+            if (pred >= 0) ok = pw == w0;
+            else maybe = (told >> kPosBits) == mytag;
+        }
+        uint64_t sm = ballot(live && (term || ok || maybe));
+        const uint64_t mm = ballot(maybe), tmk = ballot(term);
+        STAMP_ADD(2, ts);
+        // first stop; a tag-equal lane is confirmed inside the round trip
+        int w;
+        uint32_t ip = 0, cd = 0, maxb = 0, lim = 0, lit0 = 0, cw = 0, iw = 0, lb = 0;
+        bool wasTest = false, beq = false;
+        for (;;) {
+            w = sm ? __ffsll((long long)sm) - 1 : 64;
+            if (w == 64 || ((tmk >> w) & 1)) break;
+            ip = rdlane(p, w);
+            cd = rdlane(cand, w);
+            wasTest = (uint32_t)w >= W.hasIns && (uint32_t)w < ns;
+            maxb = wasTest ? 0u : min(ip - anchor, cd);
+            lim = matchlimit - (ip + kMinMatch);
+            lit0 = ip - anchor;
+            // lane 0: the 4 bytes at cd (verify); lanes >= 1: count words
+            const uint32_t rel = 4 * L - 4;
+            cw = (L == 0 || rel < lim) ? gld4u(s + cd + 4 * L) : 0u;
+            iw = (L != 0 && rel < lim) ? gld4u(s + ip + 4 * L) : 0u;
+            beq = false;
+            if (L + 1 <= maxb) beq = s[ip - L - 1] == s[cd - L - 1];
+            lb = L < lit0 ? (uint32_t)s[anchor + L] : 0u;
+            STAMP_ADD(3, ts);
+            if (((mm >> w) & 1) && (ballot(L == 0 && cw != rdlane(w0, w)) & 1)) {   // tag alias
+                if (ST) acc[11] += 1;
+                sm &= ~(1ull << w);
+                continue;
+            }
+            if (ST) acc[12] += (mm >> w) & 1;
+            break;
+        }
+        STAMP_ADD(5, ts);
+        const bool wTerm = (w < 64) && ((tmk >> w) & 1);
+        const int wlim = (w == 64) ? 63 : (wTerm ? w - 1 : w);
+        // table writes: last member of each hash group among lanes <= wlim
+        if (wlim >= 0 && live && (int)L <= wlim) {
+            const uint64_t later = gmask & ~mask_le(L) & mask_le((uint32_t)wlim);
+            if (!later) T[h] = p | (mytag << kPosBits);
+        }
+        WAVE_SYNC();
+        STAMP_ADD(6, ts);
+        if (w == 64) {   // no stop: continue the search
+            W.k0 += 64 - ns;
+            W.hasIns = 0; W.hasTest = 0;
+            continue;
+        }
+        if (wTerm) break;
+
+        // ---- catch-up and forward count (LZ4_count from the caught-up start
+        // + 4 = back + count from ip + 4; the skipped bytes are known equal)
+        uint32_t back = 0;
+        if (maxb) {
+            for (;;) {
+                const uint64_t fm = ballot(!beq);
+                if (fm) { back += (uint32_t)(__ffsll((long long)fm) - 1); break; }
+                back += 64;
+                if (back >= maxb) { back = maxb; break; }
+                const uint32_t kk = back + L + 1;
+                beq = kk <= maxb && s[ip - kk] == s[cd - kk];
+            }
+        }
+        uint32_t mc;
+        {
+            uint32_t e = 0;
+            if (L != 0 && 4 * L - 4 < lim) {
+                const uint32_t x = cw ^ iw;
+                e = min(x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u, lim - (4 * L - 4));
+            }
+            const uint64_t nf = ballot(L != 0 && e < 4);
+            if (nf) {
+                const int f = __ffsll((long long)nf) - 1;
+                mc = 4 * (uint32_t)(f - 1) + rdlane(e, f);
+            } else {
+                mc = 252;
+                for (;;) {   // long match: 256 bytes per round
+                    const uint32_t r2 = mc + 4 * L;
+                    e = 0;
+                    if (r2 < lim) {
+                        const uint32_t x = gld4u(s + ip + kMinMatch + r2) ^ gld4u(s + cd + kMinMatch + r2);
+                        e = min(x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u, lim - r2);
+                    }
+                    const uint64_t nf2 = ballot(e < 4);
+                    if (nf2) {
+                        const int f = __ffsll((long long)nf2) - 1;
+                        mc += 4 * (uint32_t)f + rdlane(e, f);
+                        break;
+                    }
+                    mc += 256;
+                }
+            }
+        }
+        STAMP_ADD(7, ts);
+        // ---- emit: token | lit ext | literals | offset | ml ext
+        const uint32_t mcf = mc + back;
+        const uint32_t lit = lit0 - back;
+        const uint32_t litExt = ext_len(lit), mlExt = ext_len(mcf);
+        if (limited) {
+            if (!wasTest && op + 1 + lit + 8 + lit / 255 > cap) return 0;
+            if (op + 1 + litExt + lit + 2 + 6 + (mcf + 240) / 255 > cap) return 0;
+        }
+        {
+            const uint32_t off = ip - cd;
+            const uint32_t token = ((lit < 15 ? lit : 15) << 4) | (mcf < 15 ? mcf : 15);
+            const uint32_t litRem = lit >= 15 ? (lit - 15) % 255 : 0u;
+            const uint32_t mlRem = mcf >= 15 ? (mcf - 15) % 255 : 0u;
+            const uint32_t a1 = 1 + litExt, a2 = a1 + lit, total = a2 + 2 + mlExt;
+            for (uint32_t base = 0; base < total; base += 64) {
+                const uint32_t x = base + L;
+                const uint32_t j = x - a1;   // literal index (wraps when x < a1)
+                const uint32_t lbx = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((j & 63) * 4), (int)lb);
+                if (x < total) {
+                    uint32_t v;
+                    if (x == 0) v = token;
+                    else if (x < a1) v = x < litExt ? 255u : litRem;
+                    else if (x < a2) v = j < 64 ? lbx : (uint32_t)s[anchor + j];
+                    else if (x == a2) v = off & 255u;
+                    else if (x == a2 + 1) v = off >> 8;
+                    else v = x + 1 < total ? 255u : mlRem;
+                    d[op + x] = (uint8_t)v;
+                }
+            }
+            op += total;
+        }
+        STAMP_ADD(8, ts);
+        const uint32_t ipe = ip + kMinMatch + mc;
+        anchor = ipe;
+        if (ipe >= mflimitP1) break;
+        W = Win{1, 1, ipe - 2, ipe, ipe + 1, 0};
+    }
+    // ---- last literals
+    {
+        const uint32_t run = n - anchor;
+        if (limited && op + run + 1 + (run + 240) / 255 > cap) return 0;
+        const uint32_t ext = ext_len(run), rem = run >= 15 ? (run - 15) % 255 : 0u;
+        if (L == 0) d[op] = (uint8_t)((run < 15 ? run : 15) << 4);
+        for (uint32_t x = L; x < ext; x += 64) d[op + 1 + x] = (uint8_t)(x + 1 < ext ? 255u : rem);
+        op += 1 + ext;
+        for (uint32_t x = L; x < run; x += 64) d[op + x] = s[anchor + x];
+        op += run;
+    }
+    return (int32_t)op;
+}
+
+// 20 KiB per wave (8 waves per CU): table + dedup scratch + 3 KiB shared by
+// the paths (encode_block: 2 KiB source ring + 1 KiB output ring;
+// encode_block_t: 2 KiB + 64 B mirrored source ring)
 #define ENCODE_LDS                                                               \
     __shared__ __attribute__((aligned(16))) uint32_t T[4096];        /* 16 KiB */ \
-    __shared__ __attribute__((aligned(16))) uint32_t R[kRingE / 4];  /* 2 KiB */  \
-    __shared__ __attribute__((aligned(16))) uint8_t OR_[kOutRing];   /* 1 KiB */  \
+    __shared__ __attribute__((aligned(16))) uint32_t X[768];         /* 3 KiB */  \
     __shared__ __attribute__((aligned(16))) uint8_t S[kDedup];       /* 1 KiB */
+static_assert(kSR + kSRMirror <= 3072, "ring exceeds the shared scratch");
 
 __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, uint64_t srcSize, uint32_t blockSize,
                                                uint8_t* __restrict__ slots, uint64_t slotStride,
@@ -493,15 +821,18 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
     g_u8* d = gptr(slots) + (uint64_t)b * slotStride;
     l_u32* Tl = (l_u32*)T;
     l_u8* Sl = (l_u8*)S;
-    l_u32* Rl = (l_u32*)R;
-    l_u8* Ol = (l_u8*)OR_;
+    l_u8* Xl = (l_u8*)X;
     int32_t r;
-    if (n < (uint32_t)kLimit64K) r = encode_block<true, false>(s, n, d, cap, Tl, Sl, Rl, Ol, nullptr);
-    else r = encode_block<false, false>(s, n, d, cap, Tl, Sl, Rl, Ol, nullptr);
+    if (n < (uint32_t)kLimit64K)
+        r = encode_block<true, false, false>(s, n, d, cap, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
+    else if (n <= (1u << kPosBits))
+        r = encode_block_t<false>(s, n, d, cap, Tl, Sl, Xl, nullptr);
+    else
+        r = encode_block<false, false, false>(s, n, d, cap, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
     if (laneid() == 0) csize[b] = r;
 }
 
-// diagnostic twin of k_encode: per-block phase cycle counts in stats[b*8 .. +8]
+// diagnostic twin of k_encode: per-block phase cycle counts in stats[b*16 .. +16]
 __global__ void __launch_bounds__(64) k_encode_stats(const uint8_t* __restrict__ src, uint64_t srcSize,
                                                      uint32_t blockSize, uint8_t* __restrict__ slots,
                                                      uint64_t slotStride, int32_t* __restrict__ csize,
@@ -510,17 +841,20 @@ __global__ void __launch_bounds__(64) k_encode_stats(const uint8_t* __restrict__
     const uint32_t b = blockIdx.x;
     const uint64_t off = (uint64_t)b * blockSize;
     const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
-    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t acc[16] = {0};
     int32_t r;
     g_cu8* s = gptr(src) + off;
     g_u8* d = gptr(slots) + b * slotStride;
+    l_u8* Xl = (l_u8*)X;
     if (n < (uint32_t)kLimit64K)
-        r = encode_block<true, true>(s, n, d, n, (l_u32*)T, (l_u8*)S, (l_u32*)R, (l_u8*)OR_, acc);
+        r = encode_block<true, false, true>(s, n, d, n, (l_u32*)T, (l_u8*)S, (l_u32*)Xl, Xl + kRingE, acc);
+    else if (n <= (1u << kPosBits))
+        r = encode_block_t<true>(s, n, d, n, (l_u32*)T, (l_u8*)S, Xl, acc);
     else
-        r = encode_block<false, true>(s, n, d, n, (l_u32*)T, (l_u8*)S, (l_u32*)R, (l_u8*)OR_, acc);
+        r = encode_block<false, false, true>(s, n, d, n, (l_u32*)T, (l_u8*)S, (l_u32*)Xl, Xl + kRingE, acc);
     if (laneid() == 0) {
         csize[b] = r;
-        for (int i = 0; i < 8; ++i) stats[b * 8 + i] = acc[i];
+        for (int i = 0; i < 16; ++i) stats[b * 16 + i] = acc[i];
     }
 }
 

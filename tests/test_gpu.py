@@ -75,6 +75,41 @@ def test_block_compress_fuzz_vs_oracle():
             assert L.compress_block(d, cap) == oracle.compress_block(d, cap), (t, n, cap)
 
 
+def _mixed(n, seed):
+    # synthetic text, random runs (long literal runs > 64), zero runs and
+    # repeats (matches longer than one 256-byte count round), near/far offsets
+    rnd = random.Random(seed)
+    syn = oracle.gen_synthetic(1 << 20, seed)
+    out, size = [], 0
+    while size < n:
+        k = rnd.randrange(5)
+        if k == 0:
+            a = rnd.randrange(len(syn) - 5000)
+            piece = syn[a:a + rnd.randrange(100, 5000)]
+        elif k == 1:
+            piece = oracle.gen_random(rnd.randrange(65, 700), rnd.randrange(1 << 30))
+        elif k == 2:
+            piece = bytes(rnd.randrange(1, 3000))
+        elif k == 3 and out:
+            prev = b"".join(out[-8:])
+            a = rnd.randrange(len(prev))
+            piece = prev[a:a + rnd.randrange(4, 2000)]
+        else:
+            piece = bytes([rnd.randrange(256)]) * rnd.randrange(1, 400)
+        out.append(piece)
+        size += len(piece)
+    return b"".join(out)[:n]
+
+
+@pytest.mark.parametrize("n", [65547, 300_000, (4 << 20) - 1, 4 << 20, (4 << 20) + 1, 5 << 20])
+def test_block_compress_mixed_vs_oracle(n):
+    # both u32 encoder paths: tagged (n <= 4 MiB) and untagged (larger
+    # blocks, reachable only through the block operator)
+    d = _mixed(n, n)
+    for cap in (n, n - 1, n + n // 255 + 16, n // 3):
+        assert L.compress_block(d, cap) == oracle.compress_block(d, cap), (n, cap)
+
+
 def test_block_decompress_golden(golden, decode_blob):
     for v in golden["decode"]:
         blk = decode_blob[v["off"]:v["off"] + v["len"]]

@@ -18,17 +18,21 @@ bm = 1 << (8 + 2 * bid)
 n = int(gib * (1 << 30)) // bm * bm
 src = L.gen_synthetic(n)
 torch.cuda.synchronize()
-st = (ctypes.c_uint64 * 8)()
+st16 = (ctypes.c_uint64 * 16)()
 t = time.time()
-assert L.lib.lz4mtHipDebugEncodeStats(ctypes.c_void_p(src.data_ptr()), n, bm, st, None) == 0
+assert L.lib.lz4mtHipDebugEncodeStats(ctypes.c_void_p(src.data_ptr()), n, bm, st16, None) == 0
 wall = time.time() - t
-e = list(st)
+e = list(st16)
 nb = n // bm
-names = ["hash", "table+dedup", "verify+twrite", "catchup", "count", "emit", "windows", "loop-ovh"]
-tot = sum(e[:6]) + e[7]
-print(f"ENCODE {gib} GiB B{bid}: wall {wall*1e3:.1f} ms, blocks {nb}, windows {e[6]}, cycles/block {tot/nb:.3e}")
-for i in (0, 1, 2, 3, 4, 5, 7):
-    print(f"  {names[i]:14s} {e[i]/tot*100:5.1f}%  {e[i]/max(e[6],1):8.1f} cyc/window")
+names = ["hash", "table+dedup", "cand check", "round issue", "lit staging", "round wait", "table writes",
+         "count", "emit", "loop-ovh"]
+tot = sum(e[:10])
+win = max(e[10], 1)
+print(f"ENCODE {gib} GiB B{bid}: wall {wall*1e3:.1f} ms, blocks {nb}, windows {e[10]}, cycles/block {tot/nb:.3e}, "
+      f"tag aliases {e[11]}, tag-candidate winners {e[12]}")
+for i in range(10):
+    print(f"  {names[i]:14s} {e[i]/tot*100:5.1f}%  {e[i]/win:8.1f} cyc/window")
+st = (ctypes.c_uint64 * 8)()
 sd = L.make_sd(bid, False, True)
 fr = L.compress_frame(src, sd)
 torch.cuda.synchronize()
@@ -36,7 +40,7 @@ t = time.time()
 assert L.lib.lz4mtHipDebugDecodeStats(ctypes.c_void_p(fr.data_ptr()), fr.numel(), st, None) == 0
 wall = time.time() - t
 d = list(st)
-print(f"DECODE: wall {wall*1e3:.1f} ms (incl. walk+alloc), total cycles/block {d[5]/nb:.3e}, matches {d[6]}, "
+print(f"DECODE: wall {wall*1e3:.1f} ms (incl. walk+alloc), total cycles/block {d[5]/nb:.3e}, batches {d[4]}, matches {d[6]}, "
       f"HBM matches {d[7]} ({d[7]/max(d[6],1)*100:.1f}%)")
 dn = ["parse", "literal copy", "ring match", "HBM match"]
 for i in range(4):
