@@ -96,10 +96,11 @@ int lz4mtHipGetTimings(float* ms4);
  * encode (16 slots): [hash, table+dedup, candidate check, round issue,
  * literal staging, round wait, table writes, count, emit, loop overhead,
  * windows, tag aliases, tag-candidate winners, -, -, -];
- * decode (8 slots): [parse, literal copy, ring match copy, HBM match copy,
- * batches, total, matches, HBM matches]. */
+ * decode (16 slots): [batch parse, serial literal copy, serial match copy
+ * / batch dependent copies, batch group + far copies, batches, total,
+ * matches, far matches, batch sequences, serial-path sequences, -...]. */
 int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* stats16, void* stream);
-int lz4mtHipDebugDecodeStats(const void* d_frame, uint64_t frameSize, uint64_t* stats8, void* stream);
+int lz4mtHipDebugDecodeStats(const void* d_frame, uint64_t frameSize, uint64_t* stats16, void* stream);
 
 #ifdef __cplusplus
 }

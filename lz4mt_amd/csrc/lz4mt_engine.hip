@@ -557,7 +557,7 @@ extern "C" int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t 
     return rc;
 }
 
-extern "C" int lz4mtHipDebugDecodeStats(const void* d_frame, uint64_t frameSize, uint64_t* stats8, void* stream) {
+extern "C" int lz4mtHipDebugDecodeStats(const void* d_frame, uint64_t frameSize, uint64_t* stats16, void* stream) {
     if (!have_device()) return -1;
     const hipStream_t st = static_cast<hipStream_t>(stream);
     const uint8_t* f = static_cast<const uint8_t*>(d_frame);
@@ -577,14 +577,14 @@ extern "C" int lz4mtHipDebugDecodeStats(const void* d_frame, uint64_t frameSize,
     int rc = -1;
     const uint64_t nb = wi.nBlocks;
     if (hipMalloc(reinterpret_cast<void**>(&out), nb * bm + 64) == hipSuccess &&
-        hipMalloc(reinterpret_cast<void**>(&dst), nb * 64 + 64) == hipSuccess &&
+        hipMalloc(reinterpret_cast<void**>(&dst), nb * 128 + 64) == hipSuccess &&
         launch_decode_stats(f, B.recs, (uint32_t)nb, bm, out, nb * bm, B.dsize, dst, st) == hipSuccess) {
-        std::vector<uint64_t> hs(nb * 8);
-        if (hipMemcpyAsync(hs.data(), dst, nb * 64, hipMemcpyDeviceToHost, st) == hipSuccess &&
+        std::vector<uint64_t> hs(nb * 16);
+        if (hipMemcpyAsync(hs.data(), dst, nb * 128, hipMemcpyDeviceToHost, st) == hipSuccess &&
             hipStreamSynchronize(st) == hipSuccess) {
-            for (int i = 0; i < 8; ++i) stats8[i] = 0;
+            for (int i = 0; i < 16; ++i) stats16[i] = 0;
             for (uint64_t b = 0; b < nb; ++b)
-                for (int i = 0; i < 8; ++i) stats8[i] += hs[b * 8 + i];
+                for (int i = 0; i < 16; ++i) stats16[i] += hs[b * 16 + i];
             rc = 0;
         }
     }

@@ -538,6 +538,7 @@ last_literals : {
 typedef const __attribute__((address_space(1))) uint32_t __attribute__((aligned(1))) g_cu32u;
 typedef const __attribute__((address_space(1))) uint64_t __attribute__((aligned(1))) g_cu64u;
 typedef __attribute__((address_space(3))) uint64_t __attribute__((aligned(1))) l_u64u;
+typedef __attribute__((address_space(3))) uint32_t __attribute__((aligned(1))) l_u32u;
 typedef __attribute__((address_space(3))) uint64_t l_u64;
 
 constexpr uint32_t kSR = 2048;        // source ring bytes
@@ -1092,30 +1093,36 @@ struct Dec {
     // safe_match_copy, one-byte length extensions, offset != 0 -- so the
     // serial state machine resumes at the same loop top with identical
     // state.  Returns the number of sequences consumed (0: run serially).
+    // Positions are 32-bit block-relative here (blocks are < 2^31 bytes).
     //   1. next-token delta for 256 candidate positions (4 per lane)
     //   2. serial hop over the packed deltas (v_readlane), one lane per sequence
     //   3. lane-parallel field decode, DPP prefix sum of output lengths
     //   4. lane-parallel check of the fast-loop conditions, cut at the first miss
-    //   5. copies: literals, far matches (HBM, independent), near matches in
-    //      dependency rounds (frontier = first unfinished sequence)
+    //   5. copies: far-match loads issued first (HBM, lane per byte); literal
+    //      runs and matches whose source lies before the batch, 8 sequences
+    //      per group (all reads, then all writes); far bytes into the ring;
+    //      matches sourcing the batch's own output last, in order
     // ---------------------------------------------------------------------
-    __device__ __forceinline__ int decode_batch(int64_t& ip, int64_t& op, int64_t iend, int64_t oend) {
-        if (ip + 1280 > iend || op + 8192 > oend) return 0;
-        if (ip < wlo || ip + 1024 > wlo + kInWin) refill(ip);
+    __device__ __forceinline__ int decode_batch(int64_t& ip64, int64_t& op64, int64_t iend64, int64_t oend64) {
+        if (ip64 + 1280 > iend64 || op64 + 8192 > oend64) return 0;
+        if (ip64 < wlo || ip64 + 1024 > wlo + kInWin) refill(ip64);
         const uint32_t L = laneid();
-        const uint32_t w0 = (uint32_t)(ip - wlo);
+        const int32_t ip = (int32_t)ip64, op = (int32_t)op64, iend = (int32_t)iend64, oend = (int32_t)oend64;
+        const uint32_t w0 = (uint32_t)(ip64 - wlo);
         // 1. candidate deltas, branch-free (every address stays inside the window)
         uint32_t packed = 0;
+        {
+            const uint64_t q = *(l_u64u*)(win + w0 + 4 * L);   // bytes [4L, 4L+8) of the scan
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const uint32_t x = w0 + 4 * L + e;
-            const uint32_t t = win[x], b1 = win[x + 1];
-            const bool l15 = (t >> 4) == 15, m15 = (t & 15) == 15;
-            const uint32_t lit = (t >> 4) + (l15 ? b1 : 0u);
-            const uint32_t b2 = win[x + 3 + (l15 ? 1u : 0u) + lit];
-            const bool cx = (l15 && b1 == 255) || (m15 && b2 == 255) || lit > 64;
-            const uint32_t d = 3 + (l15 ? 1u : 0u) + lit + (m15 ? 1u : 0u);
-            packed |= (cx ? 0u : d) << (8 * e);
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t t = (uint32_t)(q >> (8 * e)) & 255u, b1 = (uint32_t)(q >> (8 * e + 8)) & 255u;
+                const bool l15 = (t >> 4) == 15, m15 = (t & 15) == 15;
+                const uint32_t lit = (t >> 4) + (l15 ? b1 : 0u);
+                const uint32_t b2 = win[w0 + 4 * L + e + 3 + (l15 ? 1u : 0u) + lit];
+                const bool cx = (l15 && b1 == 255) || (m15 && b2 == 255) || lit > 64;
+                const uint32_t d = 3 + (l15 ? 1u : 0u) + lit + (m15 ? 1u : 0u);
+                packed |= (cx ? 0u : d) << (8 * e);
+            }
         }
         // 2. hop
         uint32_t startRel = 0, cnt = 0, cur = 0;
@@ -1137,117 +1144,149 @@ struct Dec {
         const uint32_t e1 = l15 ? 1u : 0u;
         const uint32_t lit = (tok >> 4) + (l15 ? b1 : 0u);
         const uint32_t ow = sw + 1 + e1 + lit;
-        const uint32_t off = win[ow] | ((uint32_t)win[ow + 1] << 8);
-        const uint32_t b2 = win[ow + 2];
+        const uint32_t ob = *(l_u32u*)(win + ow);   // offset lo, hi, match-length byte
+        const uint32_t off = ob & 0xFFFFu;
+        const uint32_t b2 = (ob >> 16) & 255u;
         const uint32_t e2 = m15 ? 1u : 0u;
         const uint32_t mlen = (tok & 15) + kMinMatch + (m15 ? b2 : 0u);
         const uint32_t olen = act ? lit + mlen : 0u;
         const uint32_t incl = wave_scan_incl(olen);
-        const int64_t oj = op + (int64_t)(incl - olen);   // sequence output start
-        const int64_t ipT = ip + startRel + 1;            // just after the token
-        const int64_t lp = ipT + e1;                      // literal start
-        const int64_t om = oj + lit;                      // match output start
+        const int32_t oj = op + (int32_t)(incl - olen);      // sequence output start
+        const int32_t ipT = ip + (int32_t)startRel + 1;      // just after the token
+        const int32_t lp = ipT + (int32_t)e1;                // literal start
+        const int32_t om = oj + (int32_t)lit;                // match output start
         // 4. fast-loop conditions (lz4 1.9.3, see decode_block)
         bool ok = act && off != 0 && lit + mlen <= 128 && incl <= 4096;
-        ok = ok && (l15 ? (ipT < iend - 15 && ipT + 1 < iend - 15 && oj + lit <= oend - 32 && lp + lit <= iend - 32)
+        ok = ok && (l15 ? (ipT < iend - 15 && ipT + 1 < iend - 15 && oj + (int32_t)lit <= oend - 32 &&
+                           lp + (int32_t)lit <= iend - 32)
                         : ipT <= iend - 17);
-        ok = ok && om >= (int64_t)off;
-        ok = ok && (!m15 || lp + lit + 3 < iend - kLastLiterals + 1);
-        ok = ok && om + mlen < oend - 64;
+        ok = ok && om >= (int32_t)off;
+        ok = ok && (!m15 || lp + (int32_t)lit + 3 < iend - kLastLiterals + 1);
+        ok = ok && om + (int32_t)mlen < oend - 64;
         const uint64_t bad = ballot(act && !ok);
         const uint32_t nb = bad ? (uint32_t)(__ffsll((long long)bad) - 1) : cnt;
         if (nb == 0) return 0;
         const bool in = L < nb;
         STAMP_ADD(0, ts);
-        if (ST) acc[6] += nb;
-        flush_to(op);
-        // 5a. far matches (source older than the ring keeps): their output
-        // equals their source, so fetch it from HBM (independent loads) and
-        // drop it straight into the ring at the match's output position.
-        const int64_t src = om - (int64_t)off;
-        const int64_t ringLo = op + 4096 - kRing;
+        if (ST) { acc[6] += nb; acc[8] += nb; }
+        flush_to(op64);
+        // 5. classes: far (source older than the ring keeps), dep (source
+        // reaches into this batch's output), else independent
+        const int32_t src = om - (int32_t)off;
+        const int32_t ringLo = op + 4096 - kRing;
         const bool far = in && src < ringLo;
-        if (ballot(far)) {
-            if (completed < ringLo) {
+        const bool dep = in && !far && src + (int32_t)mlen > op;
+        const uint64_t farM = ballot(far), depM = ballot(dep);
+        // 5a. far loads (up to 8 sequences, lane per byte), in flight during 5b
+        uint32_t fv[8], fv2[8];
+        uint64_t farLeft = farM;
+        if (farM) {
+            if (completed < (int64_t)ringLo) {   // their bytes were stored to dst: make sure the stores landed
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 completed = flushed;
             }
-            if (ST) acc[7] += __popcll(ballot(far));
-            if (far) {
-                // dst dword t covers ring positions A + 4t, A = om & ~3; its bytes
-                // come from src + (A + 4t - om) = S0 + 4t, S0 = src - (om & 3)
-                const int64_t A = om & ~int64_t(3);
-                const int64_t S0 = src - (om & 3);
-                const uint32_t r = (uint32_t)(S0 & 3);
-                g_cu32* q = (g_cu32*)(dst + (S0 - r));
-                const uint32_t nd = (uint32_t)((om + mlen - A + 3) >> 2);   // dst dwords, <= 33
-                uint32_t wv[34];
+            if (ST) acc[7] += __popcll(farM);
 #pragma unroll
-                for (int i = 0; i < 34; ++i)   // never below the slot start (block 0 starts the buffer)
-                    wv[i] = ((uint32_t)i <= nd && S0 - (int64_t)r + 4 * i >= 0) ? q[i] : 0u;
+            for (int g = 0; g < 8; ++g) {
+                fv[g] = 0; fv2[g] = 0;
+                if (farLeft) {
+                    const int j = __ffsll((long long)farLeft) - 1;
+                    const uint32_t js = (uint32_t)rdlane((uint32_t)src, j), jm = rdlane(mlen, j);
+                    fv[g] = L < jm ? (uint32_t)dst[js + L] : 0u;
+                    if (jm > 64) fv2[g] = L + 64 < jm ? (uint32_t)dst[js + 64 + L] : 0u;
+                }
+                farLeft &= farLeft ? farLeft - 1 : 0ull;
+            }
+        }
+        // 5b. literal runs of every sequence + independent matches, 8 per group
+        const uint32_t tot = lit + ((in && !far && !dep) ? mlen : 0u);
+        const uint32_t pA = lit | (tot << 8) | ((uint32_t)(lp - (int32_t)wlo) << 16);     // lw < 2048
+        const uint32_t pB = (uint32_t)(oj - op) | (((uint32_t)src & (kRing - 1)) << 16);   // ojrel < 4096
+        l_u8* const winp = win;
+        l_u8* const ringp = ring;
+        for (uint32_t j0 = 0; j0 < nb; j0 += 8) {
+            uint32_t v[8], v2[8], wa[8];
 #pragma unroll
-                for (int t = 0; t < 33; ++t) {
-                    if ((uint32_t)t < nd) {
-                        const uint32_t v = __builtin_amdgcn_alignbyte(wv[t + 1], wv[t], r);
-                        const int64_t pos = A + 4 * t;
-                        if (pos >= om && pos + 4 <= om + mlen) {   // whole dword inside the match
-                            *(l_u32*)(ring + (pos & (kRing - 1))) = v;
-                        } else {   // edge dword: only [om, om+mlen) (a neighbour's far bytes may sit beside it)
-#pragma unroll
-                            for (int bb = 0; bb < 4; ++bb)
-                                if (pos + bb >= om && pos + bb < om + mlen)
-                                    ring[(pos + bb) & (kRing - 1)] = (uint8_t)(v >> (8 * bb));
-                        }
+            for (int g = 0; g < 8; ++g) {
+                const uint32_t j = j0 + g;
+                v[g] = 0; v2[g] = 0; wa[g] = 0;
+                if (j < nb) {
+                    const uint32_t A = rdlane(pA, (int)j), Bv = rdlane(pB, (int)j);
+                    const uint32_t jl = A & 255u, jt = (A >> 8) & 255u, jlw = A >> 16;
+                    const uint32_t jo = (uint32_t)op + (Bv & 0xFFFFu), js = Bv >> 16;
+                    wa[g] = jo;
+                    const uint32_t x = L;
+                    l_u8* ra = x < jl ? winp + jlw + x : ringp + ((js + x - jl) & (kRing - 1));
+                    v[g] = x < jt ? (uint32_t)*ra : 0u;
+                    if (jt > 64) {
+                        const uint32_t x2 = L + 64;
+                        l_u8* rb = x2 < jl ? winp + jlw + x2 : ringp + ((js + x2 - jl) & (kRing - 1));
+                        v2[g] = x2 < jt ? (uint32_t)*rb : 0u;
                     }
                 }
             }
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const uint32_t j = j0 + g;
+                if (j < nb) {
+                    const uint32_t jt = rdlane((pA >> 8) & 255u, (int)j);
+                    const uint32_t jo = (uint32_t)op + (rdlane(pB, (int)j) & 0xFFFFu);
+                    if (L < jt) ring[(jo + L) & (kRing - 1)] = (uint8_t)v[g];
+                    if (L + 64 < jt) ring[(jo + 64 + L) & (kRing - 1)] = (uint8_t)v2[g];
+                }
+            }
+        }
+        // 5c. far bytes into the ring at the match outputs
+        if (farM) {
+            farLeft = farM;
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                if (farLeft) {
+                    const int j = __ffsll((long long)farLeft) - 1;
+                    const uint32_t jo = (uint32_t)rdlane((uint32_t)om, j), jm = rdlane(mlen, j);
+                    if (L < jm) ring[(jo + L) & (kRing - 1)] = (uint8_t)fv[g];
+                    if (L + 64 < jm) ring[(jo + 64 + L) & (kRing - 1)] = (uint8_t)fv2[g];
+                }
+                farLeft &= farLeft ? farLeft - 1 : 0ull;
+            }
+            while (farLeft) {   // more than 8 far matches: one at a time
+                const int j = __ffsll((long long)farLeft) - 1;
+                const uint32_t js = (uint32_t)rdlane((uint32_t)src, j), jm = rdlane(mlen, j);
+                const uint32_t jo = (uint32_t)rdlane((uint32_t)om, j);
+                const uint32_t a0 = L < jm ? (uint32_t)dst[js + L] : 0u;
+                const uint32_t a1 = L + 64 < jm ? (uint32_t)dst[js + 64 + L] : 0u;
+                if (L < jm) ring[(jo + L) & (kRing - 1)] = (uint8_t)a0;
+                if (L + 64 < jm) ring[(jo + 64 + L) & (kRing - 1)] = (uint8_t)a1;
+                farLeft &= farLeft - 1;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            completed = flushed;
         }
         WAVE_SYNC();
         STAMP_ADD(3, ts);
-        // 5b. sequences in order, whole wave per sequence: ONE LDS read (lanes
-        // pick window or ring; a far match's bytes are already in place) and
-        // ONE LDS write.  Overlapping matches (off < len) use k mod off.
-        const uint32_t lwin = (uint32_t)(lp - wlo);
-        for (uint32_t j = 0; j < nb; ++j) {
-            const uint32_t jlit = rdlane(lit, (int)j), jml = rdlane(mlen, (int)j), joff = rdlane(off, (int)j);
-            const uint32_t jlw = rdlane(lwin, (int)j);
-            const uint32_t jo = rdlane((uint32_t)(oj - op), (int)j);
-            const bool jfar = (ballot(far) >> j) & 1;
-            const uint32_t jtot = jlit + (jfar ? 0u : jml);
-            const int64_t jo64 = op + jo;
-            if (jfar || joff >= jtot) {   // source wholly before the sequence: one fused pass
-                for (uint32_t base = 0; base < jtot; base += 64) {
-                    const uint32_t x = base + L;
-                    if (x < jtot) {
-                        const uint32_t v = x < jlit ? (uint32_t)win[jlw + x]
-                                                    : (uint32_t)ring[(jo64 + x - joff) & (kRing - 1)];
-                        ring[(jo64 + x) & (kRing - 1)] = (uint8_t)v;
-                    }
-                    WAVE_SYNC();
+        // 5d. matches sourcing this batch's output, in order (k mod off when
+        // the source overlaps the match itself)
+        uint64_t depLeft = depM;
+        while (depLeft) {
+            const int j = __ffsll((long long)depLeft) - 1;
+            depLeft &= depLeft - 1;
+            const uint32_t jm = rdlane(mlen, j), joff = rdlane(off, j);
+            const uint32_t jom = (uint32_t)rdlane((uint32_t)om, j);
+            const uint32_t magic = joff < 64 ? (65536u + joff - 1) / joff : 0u;
+            for (uint32_t base = 0; base < jm; base += 64) {
+                const uint32_t k = base + L;
+                if (k < jm) {
+                    const uint32_t kk = (joff >= 64 || k < joff) ? k : k - ((k * magic) >> 16) * joff;
+                    ring[(jom + k) & (kRing - 1)] = ring[(jom - joff + kk) & (kRing - 1)];
                 }
-            } else {   // source overlaps the sequence itself: literal first, then the match (k mod off)
-                for (uint32_t base = 0; base < jlit; base += 64) {
-                    const uint32_t x = base + L;
-                    if (x < jlit) ring[(jo64 + x) & (kRing - 1)] = win[jlw + x];
-                    WAVE_SYNC();
-                }
-                const uint32_t magic = joff < 64 ? (65536u + joff - 1) / joff : 0u;
-                const int64_t jom = jo64 + jlit;
-                for (uint32_t base = 0; base < jml; base += 64) {
-                    const uint32_t k = base + L;
-                    if (k < jml) {
-                        const uint32_t kk = (joff >= 64 || k < joff) ? k : k - ((k * magic) >> 16) * joff;
-                        ring[(jom + k) & (kRing - 1)] = ring[(jom - joff + kk) & (kRing - 1)];
-                    }
-                    WAVE_SYNC();
-                }
+                WAVE_SYNC();
             }
         }
         STAMP_ADD(2, ts);
         // advance past the last consumed sequence
         const int last = (int)nb - 1;
-        ip = ip + (int64_t)rdlane(startRel, last) + 1 + rdlane(e1, last) + rdlane(lit, last) + 2 + rdlane(e2, last);
-        op = op + (int64_t)rdlane(incl, last);
+        ip64 = ip64 + (int64_t)rdlane(startRel, last) + 1 + rdlane(e1, last) + rdlane(lit, last) + 2 + rdlane(e2, last);
+        op64 = op64 + (int64_t)rdlane(incl, last);
         return (int)nb;
     }
     // read_variable_length(); returns 0 ok, -1 initial error, -2 loop error
@@ -1286,6 +1325,7 @@ __device__ int32_t decode_block(Dec<ST>& D, int64_t cap) {
     if (oend - op < 64) goto safe_decode;
     for (;;) {
         if (D.decode_batch(ip, op, iend, oend)) continue;
+        if (ST) D.acc[9] += 1;
         token = D.in8(ip++);
         length = token >> 4;
         if (length == 15) {
@@ -1455,7 +1495,7 @@ __global__ void __launch_bounds__(64) k_decode_stats(const uint8_t* __restrict__
     const uint32_t b = blockIdx.x;
     const BlockRec r = recs[b];
     const uint64_t slot = (uint64_t)b * blockMax;
-    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t acc[16] = {0};
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     Dec<true> D;
     D.acc = acc;
@@ -1475,7 +1515,7 @@ __global__ void __launch_bounds__(64) k_decode_stats(const uint8_t* __restrict__
     acc[5] = __builtin_amdgcn_s_memtime() - t0;
     if (laneid() == 0) {
         dsize[b] = res;
-        for (int i = 0; i < 8; ++i) stats[b * 8 + i] = acc[i];
+        for (int i = 0; i < 16; ++i) stats[b * 16 + i] = acc[i];
     }
 }
 

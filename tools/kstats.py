@@ -32,16 +32,16 @@ print(f"ENCODE {gib} GiB B{bid}: wall {wall*1e3:.1f} ms, blocks {nb}, windows {e
       f"tag aliases {e[11]}, tag-candidate winners {e[12]}")
 for i in range(10):
     print(f"  {names[i]:14s} {e[i]/tot*100:5.1f}%  {e[i]/win:8.1f} cyc/window")
-st = (ctypes.c_uint64 * 8)()
 sd = L.make_sd(bid, False, True)
 fr = L.compress_frame(src, sd)
 torch.cuda.synchronize()
+dst16 = (ctypes.c_uint64 * 16)()
 t = time.time()
-assert L.lib.lz4mtHipDebugDecodeStats(ctypes.c_void_p(fr.data_ptr()), fr.numel(), st, None) == 0
+assert L.lib.lz4mtHipDebugDecodeStats(ctypes.c_void_p(fr.data_ptr()), fr.numel(), dst16, None) == 0
 wall = time.time() - t
-d = list(st)
-print(f"DECODE: wall {wall*1e3:.1f} ms (incl. walk+alloc), total cycles/block {d[5]/nb:.3e}, batches {d[4]}, matches {d[6]}, "
-      f"HBM matches {d[7]} ({d[7]/max(d[6],1)*100:.1f}%)")
-dn = ["parse", "literal copy", "ring match", "HBM match"]
+d = list(dst16)
+print(f"DECODE: wall {wall*1e3:.1f} ms (incl. walk+alloc), total cycles/block {d[5]/nb:.3e}, batches {d[4]}, "
+      f"sequences {d[6]} (batch {d[8]}, serial {d[9]}), far {d[7]} ({d[7]/max(d[6],1)*100:.1f}%)")
+dn = ["batch parse", "serial lit copy", "dep/serial match", "group+far copy"]
 for i in range(4):
-    print(f"  {dn[i]:14s} {d[i]/d[5]*100:5.1f}%  {d[i]/max(d[6],1):8.1f} cyc/match")
+    print(f"  {dn[i]:16s} {d[i]/d[5]*100:5.1f}%  {d[i]/max(d[6],1):8.1f} cyc/seq")
