@@ -539,6 +539,7 @@ typedef const __attribute__((address_space(1))) uint32_t __attribute__((aligned(
 typedef const __attribute__((address_space(1))) uint64_t __attribute__((aligned(1))) g_cu64u;
 typedef __attribute__((address_space(3))) uint64_t __attribute__((aligned(1))) l_u64u;
 typedef __attribute__((address_space(3))) uint32_t __attribute__((aligned(1))) l_u32u;
+typedef __attribute__((address_space(3))) uint16_t __attribute__((aligned(1))) l_u16u;
 typedef __attribute__((address_space(3))) uint64_t l_u64;
 
 constexpr uint32_t kSR = 2048;        // source ring bytes
@@ -1094,52 +1095,61 @@ struct Dec {
     // serial state machine resumes at the same loop top with identical
     // state.  Returns the number of sequences consumed (0: run serially).
     // Positions are 32-bit block-relative here (blocks are < 2^31 bytes).
-    //   1. next-token delta for 256 candidate positions (4 per lane)
+    //   1. next-token delta for 512 candidate positions (8 per lane, one
+    //      LDS round trip; the match-length byte is checked in step 3)
     //   2. serial hop over the packed deltas (v_readlane), one lane per sequence
     //   3. lane-parallel field decode, DPP prefix sum of output lengths
     //   4. lane-parallel check of the fast-loop conditions, cut at the first miss
     //   5. copies: far-match loads issued first (HBM, lane per byte); literal
-    //      runs and matches whose source lies before the batch, 8 sequences
-    //      per group (all reads, then all writes); far bytes into the ring;
-    //      matches sourcing the batch's own output last, in order
+    //      runs and short matches whose source lies before the batch, 8
+    //      sequences per group (all reads, then all writes); far bytes into
+    //      the ring; then, in order, matches sourcing the batch's own output
+    //      and matches longer than one group slot (128 B)
     // ---------------------------------------------------------------------
     __device__ __forceinline__ int decode_batch(int64_t& ip64, int64_t& op64, int64_t iend64, int64_t oend64) {
         if (ip64 + 1280 > iend64 || op64 + 8192 > oend64) return 0;
+        STAMP_ADD(0, ts);
         if (ip64 < wlo || ip64 + 1024 > wlo + kInWin) refill(ip64);
+        STAMP_ADD(10, ts);
         const uint32_t L = laneid();
         const int32_t ip = (int32_t)ip64, op = (int32_t)op64, iend = (int32_t)iend64, oend = (int32_t)oend64;
         const uint32_t w0 = (uint32_t)(ip64 - wlo);
-        // 1. candidate deltas, branch-free (every address stays inside the window)
-        uint32_t packed = 0;
+        // 1. candidate deltas for positions 8L .. 8L+7 (bytes 8L .. 8L+8)
+        uint32_t pk0 = 0, pk1 = 0;
         {
-            const uint64_t q = *(l_u64u*)(win + w0 + 4 * L);   // bytes [4L, 4L+8) of the scan
+            const uint64_t q = *(l_u64u*)(win + w0 + 8 * L);
+            const uint32_t q8 = win[w0 + 8 * L + 8];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t t = (uint32_t)(q >> (8 * e)) & 255u, b1 = (uint32_t)(q >> (8 * e + 8)) & 255u;
-                const bool l15 = (t >> 4) == 15, m15 = (t & 15) == 15;
+            for (int e = 0; e < 8; ++e) {
+                const uint32_t t = (uint32_t)(q >> (8 * e)) & 255u;
+                const uint32_t b1 = e < 7 ? (uint32_t)(q >> (8 * e + 8)) & 255u : q8;
+                const bool l15 = (t >> 4) == 15;
                 const uint32_t lit = (t >> 4) + (l15 ? b1 : 0u);
-                const uint32_t b2 = win[w0 + 4 * L + e + 3 + (l15 ? 1u : 0u) + lit];
-                const bool cx = (l15 && b1 == 255) || (m15 && b2 == 255) || lit > 64;
-                const uint32_t d = 3 + (l15 ? 1u : 0u) + lit + (m15 ? 1u : 0u);
-                packed |= (cx ? 0u : d) << (8 * e);
+                const uint32_t d = 3 + (l15 ? 1u : 0u) + lit + ((t & 15) == 15 ? 1u : 0u);
+                const bool cx = (l15 && b1 == 255) || d > 255;   // deltas are bytes
+                if (e < 4) pk0 |= (cx ? 0u : d) << (8 * e);
+                else pk1 |= (cx ? 0u : d) << (8 * (e - 4));
             }
         }
-        // 2. hop
+        STAMP_ADD(11, ts);
+        // 2. hop (bottom-tested: one backward branch per sequence)
         uint32_t startRel = 0, cnt = 0, cur = 0;
-        while (cnt < 64 && cur < 256) {
-            const uint32_t wv = rdlane(packed, (int)(cur >> 2));
-            const uint32_t d = (wv >> ((cur & 3) * 8)) & 255u;
+        do {
+            const uint32_t ln = cur >> 3;
+            const uint32_t wa0 = rdlane(pk0, (int)ln), wa1 = rdlane(pk1, (int)ln);
+            const uint32_t d = (((cur & 4) ? wa1 : wa0) >> ((cur & 3) << 3)) & 255u;
             if (d == 0) break;
             startRel = (L == cnt) ? cur : startRel;
             cur += d;
-            ++cnt;
-        }
+        } while (++cnt < 64 && cur < 512);
+        STAMP_ADD(12, ts);
         if (cnt == 0) return 0;
         if (ST) acc[4] += 1;
         // 3. fields (lane j = sequence j), branch-free
         const bool act = L < cnt;
         const uint32_t sw = w0 + (act ? startRel : 0u);
-        const uint32_t tok = win[sw], b1 = win[sw + 1];
+        const uint32_t tb = *(l_u16u*)(win + sw);   // token, first literal-length byte
+        const uint32_t tok = tb & 255u, b1 = tb >> 8;
         const bool l15 = (tok >> 4) == 15, m15 = (tok & 15) == 15;
         const uint32_t e1 = l15 ? 1u : 0u;
         const uint32_t lit = (tok >> 4) + (l15 ? b1 : 0u);
@@ -1155,28 +1165,32 @@ struct Dec {
         const int32_t ipT = ip + (int32_t)startRel + 1;      // just after the token
         const int32_t lp = ipT + (int32_t)e1;                // literal start
         const int32_t om = oj + (int32_t)lit;                // match output start
+        const int32_t src = om - (int32_t)off;
+        const int32_t ringLo = op + 4096 - kRing;
         // 4. fast-loop conditions (lz4 1.9.3, see decode_block)
-        bool ok = act && off != 0 && lit + mlen <= 128 && incl <= 4096;
+        bool ok = act && off != 0 && !(m15 && b2 == 255) && incl <= 4096;
         ok = ok && (l15 ? (ipT < iend - 15 && ipT + 1 < iend - 15 && oj + (int32_t)lit <= oend - 32 &&
                            lp + (int32_t)lit <= iend - 32)
                         : ipT <= iend - 17);
         ok = ok && om >= (int32_t)off;
         ok = ok && (!m15 || lp + (int32_t)lit + 3 < iend - kLastLiterals + 1);
         ok = ok && om + (int32_t)mlen < oend - 64;
+        ok = ok && !(src < ringLo && mlen > 128);   // far loads carry at most 128 bytes
         const uint64_t bad = ballot(act && !ok);
         const uint32_t nb = bad ? (uint32_t)(__ffsll((long long)bad) - 1) : cnt;
+        STAMP_ADD(13, ts);
         if (nb == 0) return 0;
         const bool in = L < nb;
-        STAMP_ADD(0, ts);
         if (ST) { acc[6] += nb; acc[8] += nb; }
         flush_to(op64);
-        // 5. classes: far (source older than the ring keeps), dep (source
-        // reaches into this batch's output), else independent
-        const int32_t src = om - (int32_t)off;
-        const int32_t ringLo = op + 4096 - kRing;
+        STAMP_ADD(14, ts);
+        // 5. classes: far (source older than the ring keeps), ordered (source
+        // reaches into this batch's output, or longer than a group slot),
+        // else copied in groups
         const bool far = in && src < ringLo;
-        const bool dep = in && !far && src + (int32_t)mlen > op;
-        const uint64_t farM = ballot(far), depM = ballot(dep);
+        const bool longLit = in && lit > 64;
+        const bool ord = in && !far && (longLit || src + (int32_t)mlen > op || lit + mlen > 128);
+        const uint64_t farM = ballot(far), ordM = ballot(ord);
         // 5a. far loads (up to 8 sequences, lane per byte), in flight during 5b
         uint32_t fv[8], fv2[8];
         uint64_t farLeft = farM;
@@ -1198,26 +1212,27 @@ struct Dec {
                 farLeft &= farLeft ? farLeft - 1 : 0ull;
             }
         }
-        // 5b. literal runs of every sequence + independent matches, 8 per group
-        const uint32_t tot = lit + ((in && !far && !dep) ? mlen : 0u);
+        STAMP_ADD(15, ts);
+        // 5b. literal runs of every sequence + grouped matches, 8 per group
+        const uint32_t tot = longLit ? 0u : lit + ((in && !far && !ord) ? mlen : 0u);
         const uint32_t pA = lit | (tot << 8) | ((uint32_t)(lp - (int32_t)wlo) << 16);     // lw < 2048
         const uint32_t pB = (uint32_t)(oj - op) | (((uint32_t)src & (kRing - 1)) << 16);   // ojrel < 4096
         l_u8* const winp = win;
         l_u8* const ringp = ring;
         for (uint32_t j0 = 0; j0 < nb; j0 += 8) {
-            uint32_t v[8], v2[8], wa[8];
+            uint32_t v[8], v2[8], wa[8], jtv[8];
 #pragma unroll
             for (int g = 0; g < 8; ++g) {
                 const uint32_t j = j0 + g;
-                v[g] = 0; v2[g] = 0; wa[g] = 0;
+                v[g] = 0; v2[g] = 0; wa[g] = 0; jtv[g] = 0;
                 if (j < nb) {
                     const uint32_t A = rdlane(pA, (int)j), Bv = rdlane(pB, (int)j);
                     const uint32_t jl = A & 255u, jt = (A >> 8) & 255u, jlw = A >> 16;
                     const uint32_t jo = (uint32_t)op + (Bv & 0xFFFFu), js = Bv >> 16;
-                    wa[g] = jo;
-                    const uint32_t x = L;
-                    l_u8* ra = x < jl ? winp + jlw + x : ringp + ((js + x - jl) & (kRing - 1));
-                    v[g] = x < jt ? (uint32_t)*ra : 0u;
+                    jtv[g] = jt;
+                    wa[g] = jo + L;
+                    l_u8* ra = L < jl ? winp + jlw + L : ringp + ((js + L - jl) & (kRing - 1));
+                    v[g] = L < jt ? (uint32_t)*ra : 0u;
                     if (jt > 64) {
                         const uint32_t x2 = L + 64;
                         l_u8* rb = x2 < jl ? winp + jlw + x2 : ringp + ((js + x2 - jl) & (kRing - 1));
@@ -1227,13 +1242,22 @@ struct Dec {
             }
 #pragma unroll
             for (int g = 0; g < 8; ++g) {
-                const uint32_t j = j0 + g;
-                if (j < nb) {
-                    const uint32_t jt = rdlane((pA >> 8) & 255u, (int)j);
-                    const uint32_t jo = (uint32_t)op + (rdlane(pB, (int)j) & 0xFFFFu);
-                    if (L < jt) ring[(jo + L) & (kRing - 1)] = (uint8_t)v[g];
-                    if (L + 64 < jt) ring[(jo + 64 + L) & (kRing - 1)] = (uint8_t)v2[g];
+                if (j0 + g < nb) {
+                    if (L < jtv[g]) ring[wa[g] & (kRing - 1)] = (uint8_t)v[g];
+                    if (L + 64 < jtv[g]) ring[(wa[g] + 64) & (kRing - 1)] = (uint8_t)v2[g];
                 }
+            }
+        }
+        // 5b'. literal runs longer than 64 bytes (whole wave, 64 per step)
+        uint64_t llLeft = ballot(longLit);
+        while (llLeft) {
+            const int j = __ffsll((long long)llLeft) - 1;
+            llLeft &= llLeft - 1;
+            const uint32_t A = rdlane(pA, j), jo = (uint32_t)op + (rdlane(pB, j) & 0xFFFFu);
+            const uint32_t jl = A & 255u, jlw = A >> 16;
+            for (uint32_t base = 0; base < jl; base += 64) {
+                const uint32_t x = base + L;
+                if (x < jl) ring[(jo + x) & (kRing - 1)] = win[jlw + x];
             }
         }
         // 5c. far bytes into the ring at the match outputs
@@ -1264,12 +1288,11 @@ struct Dec {
         }
         WAVE_SYNC();
         STAMP_ADD(3, ts);
-        // 5d. matches sourcing this batch's output, in order (k mod off when
-        // the source overlaps the match itself)
-        uint64_t depLeft = depM;
-        while (depLeft) {
-            const int j = __ffsll((long long)depLeft) - 1;
-            depLeft &= depLeft - 1;
+        // 5d. ordered matches (k mod off when the source overlaps the match)
+        uint64_t ordLeft = ordM;
+        while (ordLeft) {
+            const int j = __ffsll((long long)ordLeft) - 1;
+            ordLeft &= ordLeft - 1;
             const uint32_t jm = rdlane(mlen, j), joff = rdlane(off, j);
             const uint32_t jom = (uint32_t)rdlane((uint32_t)om, j);
             const uint32_t magic = joff < 64 ? (65536u + joff - 1) / joff : 0u;
