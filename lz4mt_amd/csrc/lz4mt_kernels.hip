@@ -1219,35 +1219,41 @@ struct Dec {
         const uint32_t pB = (uint32_t)(oj - op) | (((uint32_t)src & (kRing - 1)) << 16);   // ojrel < 4096
         l_u8* const winp = win;
         l_u8* const ringp = ring;
+        l_u8* const dummy = win + kInWin;   // 128 scratch bytes: target of masked-off lane writes
+        const uint64_t bigM = ballot(tot > 64);
         for (uint32_t j0 = 0; j0 < nb; j0 += 8) {
-            uint32_t v[8], v2[8], wa[8], jtv[8];
+            uint32_t v[8];
+            l_u8* wp[8];
+            const bool big = ((bigM >> j0) & 0xFFull) != 0;
 #pragma unroll
             for (int g = 0; g < 8; ++g) {
-                const uint32_t j = j0 + g;
-                v[g] = 0; v2[g] = 0; wa[g] = 0; jtv[g] = 0;
-                if (j < nb) {
-                    const uint32_t A = rdlane(pA, (int)j), Bv = rdlane(pB, (int)j);
-                    const uint32_t jl = A & 255u, jt = (A >> 8) & 255u, jlw = A >> 16;
-                    const uint32_t jo = (uint32_t)op + (Bv & 0xFFFFu), js = Bv >> 16;
-                    jtv[g] = jt;
-                    wa[g] = jo + L;
-                    l_u8* ra = L < jl ? winp + jlw + L : ringp + ((js + L - jl) & (kRing - 1));
-                    v[g] = L < jt ? (uint32_t)*ra : 0u;
-                    if (jt > 64) {
-                        const uint32_t x2 = L + 64;
-                        l_u8* rb = x2 < jl ? winp + jlw + x2 : ringp + ((js + x2 - jl) & (kRing - 1));
-                        v2[g] = x2 < jt ? (uint32_t)*rb : 0u;
-                    }
-                }
+                const uint32_t j = min(j0 + g, 63u);
+                const uint32_t A = rdlane(pA, (int)j), Bv = rdlane(pB, (int)j);
+                const uint32_t jl = A & 255u, jt = (j0 + g < nb) ? (A >> 8) & 255u : 0u, jlw = A >> 16;
+                const uint32_t jo = (uint32_t)op + (Bv & 0xFFFFu), js = Bv >> 16;
+                l_u8* ra = L < jl ? winp + jlw + L : ringp + ((js + L - jl) & (kRing - 1));
+                v[g] = *ra;
+                wp[g] = L < jt ? ringp + ((jo + L) & (kRing - 1)) : dummy + L;
             }
 #pragma unroll
-            for (int g = 0; g < 8; ++g) {
-                if (j0 + g < nb) {
-                    if (L < jtv[g]) ring[wa[g] & (kRing - 1)] = (uint8_t)v[g];
-                    if (L + 64 < jtv[g]) ring[(wa[g] + 64) & (kRing - 1)] = (uint8_t)v2[g];
+            for (int g = 0; g < 8; ++g) *wp[g] = (uint8_t)v[g];
+            if (big) {   // second 64-byte half of sequences longer than 64 bytes
+#pragma unroll
+                for (int g = 0; g < 8; ++g) {
+                    const uint32_t j = min(j0 + g, 63u);
+                    const uint32_t A = rdlane(pA, (int)j), Bv = rdlane(pB, (int)j);
+                    const uint32_t jl = A & 255u, jt = (j0 + g < nb) ? (A >> 8) & 255u : 0u, jlw = A >> 16;
+                    const uint32_t jo = (uint32_t)op + (Bv & 0xFFFFu), js = Bv >> 16;
+                    const uint32_t x = L + 64;
+                    l_u8* ra = x < jl ? winp + jlw + x : ringp + ((js + x - jl) & (kRing - 1));
+                    v[g] = *ra;
+                    wp[g] = x < jt ? ringp + ((jo + x) & (kRing - 1)) : dummy + 64 + L;
                 }
+#pragma unroll
+                for (int g = 0; g < 8; ++g) *wp[g] = (uint8_t)v[g];
             }
         }
+        STAMP_ADD(1, ts);
         // 5b'. literal runs longer than 64 bytes (whole wave, 64 per step)
         uint64_t llLeft = ballot(longLit);
         while (llLeft) {
@@ -1268,8 +1274,8 @@ struct Dec {
                 if (farLeft) {
                     const int j = __ffsll((long long)farLeft) - 1;
                     const uint32_t jo = (uint32_t)rdlane((uint32_t)om, j), jm = rdlane(mlen, j);
-                    if (L < jm) ring[(jo + L) & (kRing - 1)] = (uint8_t)fv[g];
-                    if (L + 64 < jm) ring[(jo + 64 + L) & (kRing - 1)] = (uint8_t)fv2[g];
+                    *(L < jm ? ringp + ((jo + L) & (kRing - 1)) : dummy + L) = (uint8_t)fv[g];
+                    if (jm > 64) *(L + 64 < jm ? ringp + ((jo + 64 + L) & (kRing - 1)) : dummy + 64 + L) = (uint8_t)fv2[g];
                 }
                 farLeft &= farLeft ? farLeft - 1 : 0ull;
             }
@@ -1479,7 +1485,7 @@ __global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ frame
                                                uint32_t blockMax, uint8_t* __restrict__ out, uint64_t outCap,
                                                int32_t* __restrict__ dsize) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
-    __shared__ __attribute__((aligned(16))) uint8_t win[kInWin];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kInWin + 128];   /* + dummy write area */
     const uint32_t b = blockIdx.x;
     const BlockRec r = recs[b];
     const uint64_t slot = (uint64_t)b * blockMax;
@@ -1514,7 +1520,7 @@ __global__ void __launch_bounds__(64) k_decode_stats(const uint8_t* __restrict__
                                                      uint8_t* __restrict__ out, uint64_t outCap,
                                                      int32_t* __restrict__ dsize, uint64_t* __restrict__ stats) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
-    __shared__ __attribute__((aligned(16))) uint8_t win[kInWin];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kInWin + 128];   /* + dummy write area */
     const uint32_t b = blockIdx.x;
     const BlockRec r = recs[b];
     const uint64_t slot = (uint64_t)b * blockMax;

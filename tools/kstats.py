@@ -42,6 +42,9 @@ wall = time.time() - t
 d = list(dst16)
 print(f"DECODE: wall {wall*1e3:.1f} ms (incl. walk+alloc), total cycles/block {d[5]/nb:.3e}, batches {d[4]}, "
       f"sequences {d[6]} (batch {d[8]}, serial {d[9]}), far {d[7]} ({d[7]/max(d[6],1)*100:.1f}%)")
-dn = ["batch parse", "serial lit copy", "dep/serial match", "group+far copy"]
+dn = ["between batches", "group copy", "ordered matches", "longlit+far write"]
 for i in range(4):
     print(f"  {dn[i]:16s} {d[i]/d[5]*100:5.1f}%  {d[i]/max(d[6],1):8.1f} cyc/seq")
+bn = {10: "refill", 11: "deltas", 12: "hop", 13: "fields+scan+check", 14: "flush", 15: "far issue"}
+for i in range(10, 16):
+    print(f"  {bn[i]:16s} {d[i]/d[5]*100:5.1f}%  {d[i]/max(d[4],1):8.1f} cyc/batch")
