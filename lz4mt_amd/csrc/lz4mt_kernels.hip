@@ -1132,16 +1132,18 @@ struct Dec {
             }
         }
         STAMP_ADD(11, ts);
-        // 2. hop (bottom-tested: one backward branch per sequence)
+        // 2. hop (bottom-tested, one exit test).  A zero delta ends the chain;
+        // starts past the 64th match no lane and are dropped by the clamp.
         uint32_t startRel = 0, cnt = 0, cur = 0;
         do {
             const uint32_t ln = cur >> 3;
             const uint32_t wa0 = rdlane(pk0, (int)ln), wa1 = rdlane(pk1, (int)ln);
             const uint32_t d = (((cur & 4) ? wa1 : wa0) >> ((cur & 3) << 3)) & 255u;
-            if (d == 0) break;
-            startRel = (L == cnt) ? cur : startRel;
-            cur += d;
-        } while (++cnt < 64 && cur < 512);
+            startRel = (L == cnt) ? cur : startRel;   // a zero-delta position is not counted
+            cnt += d ? 1u : 0u;
+            cur = d ? cur + d : 512u;
+        } while (cur < 512);
+        cnt = min(cnt, 64u);
         STAMP_ADD(12, ts);
         if (cnt == 0) return 0;
         if (ST) acc[4] += 1;
@@ -1216,7 +1218,7 @@ struct Dec {
         // 5b. literal runs of every sequence + grouped matches, 8 per group
         const uint32_t tot = longLit ? 0u : lit + ((in && !far && !ord) ? mlen : 0u);
         const uint32_t pA = lit | (tot << 8) | ((uint32_t)(lp - (int32_t)wlo) << 16);     // lw < 2048
-        const uint32_t pB = (uint32_t)(oj - op) | (((uint32_t)src & (kRing - 1)) << 16);   // ojrel < 4096
+        const uint32_t pB = (uint32_t)(oj - op) | ((((uint32_t)src - lit) & (kRing - 1)) << 16);   // ojrel < 4096
         l_u8* const winp = win;
         l_u8* const ringp = ring;
         l_u8* const dummy = win + kInWin;   // 128 scratch bytes: target of masked-off lane writes
@@ -1231,7 +1233,7 @@ struct Dec {
                 const uint32_t A = rdlane(pA, (int)j), Bv = rdlane(pB, (int)j);
                 const uint32_t jl = A & 255u, jt = (j0 + g < nb) ? (A >> 8) & 255u : 0u, jlw = A >> 16;
                 const uint32_t jo = (uint32_t)op + (Bv & 0xFFFFu), js = Bv >> 16;
-                l_u8* ra = L < jl ? winp + jlw + L : ringp + ((js + L - jl) & (kRing - 1));
+                l_u8* ra = L < jl ? winp + jlw + L : ringp + ((js + L) & (kRing - 1));
                 v[g] = *ra;
                 wp[g] = L < jt ? ringp + ((jo + L) & (kRing - 1)) : dummy + L;
             }
@@ -1245,7 +1247,7 @@ struct Dec {
                     const uint32_t jl = A & 255u, jt = (j0 + g < nb) ? (A >> 8) & 255u : 0u, jlw = A >> 16;
                     const uint32_t jo = (uint32_t)op + (Bv & 0xFFFFu), js = Bv >> 16;
                     const uint32_t x = L + 64;
-                    l_u8* ra = x < jl ? winp + jlw + x : ringp + ((js + x - jl) & (kRing - 1));
+                    l_u8* ra = x < jl ? winp + jlw + x : ringp + ((js + x) & (kRing - 1));
                     v[g] = *ra;
                     wp[g] = x < jt ? ringp + ((jo + x) & (kRing - 1)) : dummy + 64 + L;
                 }
