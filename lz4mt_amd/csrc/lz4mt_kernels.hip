@@ -596,23 +596,29 @@ struct SeqEmit {
     uint32_t op, total, a1, a2, litExt, lit, token, litRem, mlRem, off, anchor;
     bool direct;
 };
-__device__ __forceinline__ void store_seq(const SeqEmit& e, uint32_t lb, uint32_t lbo, g_cu8* __restrict__ s,
-                                          g_u8* __restrict__ d) {
+__device__ __forceinline__ uint32_t seq_byte(const SeqEmit& e, uint32_t x, uint32_t lv) {
+    uint32_t v = x + 1 < e.total ? 255u : e.mlRem;
+    v = x == e.a2 + 1 ? e.off >> 8 : v;
+    v = x == e.a2 ? e.off & 255u : v;
+    v = x < e.a2 ? lv : v;
+    v = x < e.a1 ? (x < e.litExt ? 255u : e.litRem) : v;
+    return x == 0 ? e.token : v;
+}
+// common case (no catch-up, <= 64 bytes): lane L already holds its literal
+// byte; no loads, so nothing here waits on the round trip in flight
+__device__ __forceinline__ void store_seq_direct(const SeqEmit& e, uint32_t lbo, g_u8* __restrict__ d) {
+    const uint32_t L = laneid();
+    const uint32_t v = seq_byte(e, L, lbo);
+    if (L < e.total) d[e.op + L] = (uint8_t)v;
+}
+__device__ __forceinline__ void store_seq(const SeqEmit& e, uint32_t lb, g_cu8* __restrict__ s, g_u8* __restrict__ d) {
     const uint32_t L = laneid();
     for (uint32_t base = 0; base < e.total; base += 64) {
         const uint32_t x = base + L;
         const uint32_t j = x - e.a1;   // literal index (wraps when x < a1)
-        uint32_t lv = lbo;
-        if (!e.direct) {
-            lv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((j & 63) * 4), (int)lb);
-            if (j >= 64 && j < e.lit) lv = s[e.anchor + j];
-        }
-        uint32_t v = x + 1 < e.total ? 255u : e.mlRem;
-        v = x == e.a2 + 1 ? e.off >> 8 : v;
-        v = x == e.a2 ? e.off & 255u : v;
-        v = x < e.a2 ? lv : v;
-        v = x < e.a1 ? (x < e.litExt ? 255u : e.litRem) : v;
-        v = x == 0 ? e.token : v;
+        uint32_t lv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((j & 63) * 4), (int)lb);
+        if (j >= 64 && j < e.lit) lv = s[e.anchor + j];
+        const uint32_t v = seq_byte(e, x, lv);
         if (x < e.total) d[e.op + x] = (uint8_t)v;
     }
 }
@@ -728,7 +734,8 @@ __device__ int32_t encode_block_t(g_cu8* __restrict__ s, uint32_t n, g_u8* __res
             lbo = s[lj < last1 ? lj : last1];
             beq = bOn && bi == bc;
             if (havePe) {   // previous sequence's stores overlap this round trip
-                store_seq(pe, peLb, peLbo, s, d);
+                if (pe.direct) store_seq_direct(pe, peLbo, d);
+                else store_seq(pe, peLb, s, d);
                 havePe = false;
             }
             STAMP_ADD(3, ts);
@@ -741,7 +748,8 @@ __device__ int32_t encode_block_t(g_cu8* __restrict__ s, uint32_t n, g_u8* __res
             break;
         }
         if (havePe) {
-            store_seq(pe, peLb, peLbo, s, d);
+            if (pe.direct) store_seq_direct(pe, peLbo, d);
+            else store_seq(pe, peLb, s, d);
             havePe = false;
         }
         STAMP_ADD(5, ts);
@@ -831,6 +839,7 @@ __device__ int32_t encode_block_t(g_cu8* __restrict__ s, uint32_t n, g_u8* __res
             pe.direct = back == 0 && pe.total <= 64;   // lbo already holds each lane's literal
             peLb = lb;
             peLbo = lbo;
+            asm volatile("" : "+v"(peLb), "+v"(peLbo));   // settle them here, not under the next round trip
             havePe = true;
             op += pe.total;
         }
@@ -840,7 +849,10 @@ __device__ int32_t encode_block_t(g_cu8* __restrict__ s, uint32_t n, g_u8* __res
         if (ipe >= mflimitP1) break;
         hasIns = 1; hasTest = 1; insPos = ipe - 2; testPos = ipe; sPos = ipe + 1; k0 = 0;
     }
-    if (havePe) store_seq(pe, peLb, peLbo, s, d);
+    if (havePe) {
+        if (pe.direct) store_seq_direct(pe, peLbo, d);
+        else store_seq(pe, peLb, s, d);
+    }
     // ---- last literals
     {
         const uint32_t run = n - anchor;
