@@ -300,30 +300,61 @@ struct DeviceBuffers {
         if (st) hipStreamDestroy(st);
     }
     bool init(uint64_t in, uint64_t out, uint64_t ws) {
-        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
-        inCap = in; outCap = out; wsCap = ws;
-        return hipHostMalloc(reinterpret_cast<void**>(&hIn), in + 64, 0) == hipSuccess &&
-               hipHostMalloc(reinterpret_cast<void**>(&hOut), out + 64, 0) == hipSuccess &&
-               hipMalloc(reinterpret_cast<void**>(&dIn), in + 64) == hipSuccess &&
-               hipMalloc(reinterpret_cast<void**>(&dOut), out + 64) == hipSuccess &&
-               (ws == 0 || hipMalloc(reinterpret_cast<void**>(&dWs), ws + 64) == hipSuccess);
+        if (!st && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
+        return ensure(in, out, ws);
+    }
+    // grows the buffers (contents are not kept)
+    bool ensure(uint64_t in, uint64_t out, uint64_t ws) {
+        if (in > inCap) {
+            if (hIn) hipHostFree(hIn);
+            if (dIn) hipFree(dIn);
+            hIn = nullptr; dIn = nullptr; inCap = 0;
+            if (hipHostMalloc(reinterpret_cast<void**>(&hIn), in + 64, 0) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void**>(&dIn), in + 64) != hipSuccess)
+                return false;
+            inCap = in;
+        }
+        if (out > outCap) {
+            if (hOut) hipHostFree(hOut);
+            if (dOut) hipFree(dOut);
+            hOut = nullptr; dOut = nullptr; outCap = 0;
+            if (hipHostMalloc(reinterpret_cast<void**>(&hOut), out + 64, 0) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void**>(&dOut), out + 64) != hipSuccess)
+                return false;
+            outCap = out;
+        }
+        if (ws > wsCap) {
+            if (dWs) hipFree(dWs);
+            dWs = nullptr; wsCap = 0;
+            if (hipMalloc(reinterpret_cast<void**>(&dWs), ws + 64) != hipSuccess) return false;
+            wsCap = ws;
+        }
+        return true;
     }
 };
 
-constexpr uint64_t kBatchBytes = 256ull << 20;
+// A batch must hold enough blocks to fill the chip (one wavefront per block,
+// 256 CUs x 8): up to 2048 blocks, at least 256 MiB and at most 8 GiB of
+// input.  Batches start at 64 blocks and double while they come back full,
+// so short streams never pin the full size.
+uint64_t batch_blocks_max(uint32_t bm) {
+    const uint64_t want = 2048ull * bm;
+    const uint64_t bytes = std::min<uint64_t>(std::max<uint64_t>(want, 256ull << 20), 8ull << 30);
+    return std::max<uint64_t>(1, bytes / bm);
+}
 
 void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
     if (s.level() >= 3) { s.quit(LZ4MT_RESULT_BAD_ARG); return; }   // no GPU LZ4-HC
     if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return; }
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
-    const uint64_t K = std::max<uint64_t>(1, kBatchBytes / bm);
-    const uint64_t inCap = K * bm;
-    const uint64_t bodyCap = inCap + K * 8 + 64;
+    const uint64_t Kmax = batch_blocks_max(bm);
+    uint64_t K = std::min<uint64_t>(64, Kmax);
     DeviceBuffers B;
-    if (!B.init(inCap, bodyCap, compress_ws_bytes(inCap, bm))) { s.quit(LZ4MT_RESULT_ERROR); return; }
     bool eof = false;
     while (!eof && !s.error()) {
+        const uint64_t inCap = K * bm;
+        if (!B.init(inCap, inCap + K * 8 + 64, compress_ws_bytes(inCap, bm))) { s.quit(LZ4MT_RESULT_ERROR); return; }
         uint64_t total = 0;
         for (uint64_t j = 0; j < K; ++j) {   // one read() per block, as the reference does
             const int n = s.read(B.hIn + total, (int)bm);
@@ -353,6 +384,7 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
             if (!s.write(B.hOut + o, chunk)) return;
             o += (uint64_t)chunk;
         }
+        if (total == K * bm) K = std::min(2 * K, Kmax);   // full batch: more input likely
     }
 }
 
@@ -411,24 +443,26 @@ bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
     if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return false; }
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
-    const uint64_t K = std::max<uint64_t>(1, kBatchBytes / bm);
+    const uint64_t Kmax = batch_blocks_max(bm);
+    uint64_t K = std::min<uint64_t>(64, Kmax);
     DeviceBuffers B;
-    if (!B.init(K * bm, K * bm, 0)) { s.quit(LZ4MT_RESULT_ERROR); return false; }
     BlockRec* dRecs = nullptr;
     int32_t *dDs = nullptr, *dSt = nullptr;
     uint32_t* dDig = nullptr;
-    if (hipMalloc(reinterpret_cast<void**>(&dRecs), K * sizeof(BlockRec)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&dDs), K * 4) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&dSt), K * 4) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&dDig), K * 4) != hipSuccess) {
+    if (hipMalloc(reinterpret_cast<void**>(&dRecs), Kmax * sizeof(BlockRec)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&dDs), Kmax * 4) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&dSt), Kmax * 4) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&dDig), Kmax * 4) != hipSuccess) {
         s.quit(LZ4MT_RESULT_ERROR);
+        hipFree(dRecs); hipFree(dDs); hipFree(dSt); hipFree(dDig);
         return false;
     }
-    std::vector<BlockRec> recs(K);
-    std::vector<int32_t> ds(K), stv(K);
+    std::vector<BlockRec> recs(Kmax);
+    std::vector<int32_t> ds(Kmax), stv(Kmax);
     bool eos = false;
     Lz4MtResult pending = LZ4MT_RESULT_OK;   // a read error found while filling the batch
     while (!eos && pending == LZ4MT_RESULT_OK && !s.error() && !s.readEof()) {
+        if (!B.init(K * bm, K * bm, 0)) { s.quit(LZ4MT_RESULT_ERROR); break; }
         uint64_t used = 0, nb = 0;
         while (nb < K) {
             uint32_t bits = 0;
@@ -479,6 +513,7 @@ bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
             if (stop) break;
         }
         if (pending != LZ4MT_RESULT_OK) { s.quit(pending); break; }
+        if (nb == K) K = std::min(2 * K, Kmax);   // full batch: more input likely
     }
     hipFree(dRecs); hipFree(dDs); hipFree(dSt); hipFree(dDig);
     return eos;
