@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--block-id", type=int, default=7, help="4..7 = 64 KiB..4 MiB")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-mib", type=int, default=256, help="CPU baseline sample (MiB)")
+    p.add_argument("--decompress-only", action="store_true",
+                   help="configs[2]: time only the decompression of a pre-compressed stream (use --gib 32)")
     return p.parse_args()
 
 
@@ -80,7 +82,7 @@ def pmc_traffic(kernel, n, bm):
     summary (profiles/*_pmc.json, written by tools/prof.sh + tools/pmcsum.py on
     the same 8 GiB / 4 MiB-block workload); None when absent or not comparable."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))   # round tags sort by name
     if not files or n != 8 << 30 or bm != 4 << 20:
         return None, None
     try:
@@ -148,6 +150,9 @@ def main():
         if r != 0 or osz.value != n:
             raise L.Lz4MtError(r, f"decompress ({osz.value} of {n} bytes)")
 
+    if a.decompress_only:   # compress once, untimed
+        compress()
+        torch.cuda.synchronize()
     L.lib.lz4mtHipSetTiming(1)
     tc = td = 0.0
     enc_ms, dec_ms, frame_len = [], [], 0
@@ -157,11 +162,14 @@ def main():
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        compress()
+        tm = None
+        if not a.decompress_only:
+            compress()
         frame_len = int(fsz[0].item())          # synchronises the stream
-        tm = timings()
-        if world > 1:
-            gather_to_root(frame_len)
+        if not a.decompress_only:
+            tm = timings()
+            if world > 1:
+                gather_to_root(frame_len)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         decompress(frame_len)
@@ -188,9 +196,9 @@ def main():
         ok = bad == 0.0
     K = a.steps
     total = n * world * K
-    comp_gibps = total / GiB / tc
+    comp_gibps = total / GiB / tc if tc > 0 else None
     decomp_gibps = total / GiB / td
-    value = total / GiB / (tc + td)
+    value = decomp_gibps if a.decompress_only else total / GiB / (tc + td)
 
     enc_avg = sum(enc_ms) / len(enc_ms) if enc_ms else None
     dec_avg = sum(dec_ms) / len(dec_ms) if dec_ms else None
@@ -212,6 +220,10 @@ def main():
         dec_roof = {"kernel": "k_decode", "kernel_ms": round(dec_avg, 3), "achieved": round(ach, 2),
                     "frac": round(ach / HBM_PEAK_GBPS, 5), "traffic": dtraffic}
 
+    if a.decompress_only and dec_roof:   # the decode kernel is the dominant one here
+        roof = {"bound": "hbm", "achieved": dec_roof["achieved"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": dec_roof["frac"], "traffic": dec_roof["traffic"], "kernel": "k_decode",
+                "kernel_ms": dec_roof["kernel_ms"], "algorithmic_bytes": n + body}
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
@@ -221,11 +233,15 @@ def main():
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": K, "warmup": a.warmup,
             "ms_per_step": round((tc + td) / K * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic (SURVEY.md App. F generator, seed 42)",
-            "config": {"workload": f"configs[1]: {a.gib:g} GiB/GPU synthetic, {bm >> 10} KiB independent blocks, "
-                                   "-Sx -BX frame, compress+decompress+XXH32, device-resident",
+            "config": {"workload": (f"configs[2]: {a.gib:g} GiB/GPU pre-compressed synthetic stream, "
+                                    f"{bm >> 10} KiB blocks, decompress+XXH32 verify only, device-resident")
+                                   if a.decompress_only else
+                                   (f"configs[1]: {a.gib:g} GiB/GPU synthetic, {bm >> 10} KiB independent blocks, "
+                                    "-Sx -BX frame, compress+decompress+XXH32, device-resident"),
                        "bytes_per_gpu": n, "block_bytes": bm, "parallelism": f"block-sharded x{world}"
                                                                                 + (", RCCL gather" if world > 1 else "")},
-            "compress_GiBps": round(comp_gibps, 3), "decompress_GiBps": round(decomp_gibps, 3),
+            "compress_GiBps": round(comp_gibps, 3) if comp_gibps else None,
+            "decompress_GiBps": round(decomp_gibps, 3),
             "ratio": round(n / frame_len, 4), "frame_bytes": frame_len,
             "stitched_frame_bytes": stitched["len"] if world > 1 else frame_len, "roundtrip_ok": ok,
             "roofline": roof, "decode_roofline": dec_roof, "cpu_baseline": cpu,
