@@ -196,7 +196,7 @@ def main():
         ok = bad == 0.0
     K = a.steps
     total = n * world * K
-    comp_gibps = total / GiB / tc if tc > 0 else None
+    comp_gibps = None if a.decompress_only else total / GiB / tc
     decomp_gibps = total / GiB / td
     value = decomp_gibps if a.decompress_only else total / GiB / (tc + td)
 

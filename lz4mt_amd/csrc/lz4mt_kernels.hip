@@ -684,20 +684,23 @@ __device__ int32_t encode_block_t(g_cu8* __restrict__ s, uint32_t n, g_u8* __res
         uint64_t pending = ballot(live && sv != marker);
         int pred = -1;
         uint64_t gmask = 1ull << L;
-        while (pending) {   // one iteration per group of equal hashes
-            const int leader = __ffsll((long long)pending) - 1;
-            const uint32_t key = rdlane(h, leader);
-            const uint64_t m = ballot(live && h == key);
-            const bool inG = (m >> L) & 1;
-            const uint64_t below = m & ((1ull << L) - 1ull);
-            const int pr = below ? 63 - __clzll((long long)below) : -1;
-            pred = inG ? pr : pred;
-            gmask = inG ? m : gmask;
-            pending &= ~m;
+        uint32_t pw = 0, pp = 0;
+        if (pending) {   // in-window duplicate hashes (most windows have none)
+            while (pending) {   // one iteration per group of equal hashes
+                const int leader = __ffsll((long long)pending) - 1;
+                const uint32_t key = rdlane(h, leader);
+                const uint64_t m = ballot(live && h == key);
+                const bool inG = (m >> L) & 1;
+                const uint64_t below = m & ((1ull << L) - 1ull);
+                const int pr = below ? 63 - __clzll((long long)below) : -1;
+                pred = inG ? pr : pred;
+                gmask = inG ? m : gmask;
+                pending &= ~m;
+            }
+            const int pi = (pred < 0 ? 0 : pred) * 4;
+            pw = (uint32_t)__builtin_amdgcn_ds_bpermute(pi, (int)w0);   // predecessor's bytes
+            pp = (uint32_t)__builtin_amdgcn_ds_bpermute(pi, (int)p);    // and position
         }
-        const int pi = (pred < 0 ? 0 : pred) * 4;
-        const uint32_t pw = (uint32_t)__builtin_amdgcn_ds_bpermute(pi, (int)w0);   // predecessor's bytes
-        const uint32_t pp = (uint32_t)__builtin_amdgcn_ds_bpermute(pi, (int)p);    // and position
         const uint32_t cand = pred >= 0 ? pp : (told & kPosMask);
         STAMP_ADD(1, ts);
         const bool cok = live && !isIns && !term && (cand + kDistMax >= p);
@@ -1119,7 +1122,9 @@ struct Dec {
     //      and matches longer than one group slot (128 B)
     // ---------------------------------------------------------------------
     __device__ __forceinline__ int decode_batch(int64_t& ip64, int64_t& op64, int64_t iend64, int64_t oend64) {
-        if (ip64 + 1280 > iend64 || op64 + 8192 > oend64) return 0;
+        // every sequence is validated against 1.9.3's fast-loop conditions
+        // below; this guard only keeps the batch machinery inside the block
+        if (ip64 + 17 > iend64 || op64 + 64 > oend64) return 0;
         STAMP_ADD(0, ts);
         if (ip64 < wlo || ip64 + 1024 > wlo + kInWin) refill(ip64);
         STAMP_ADD(10, ts);
