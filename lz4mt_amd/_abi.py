@@ -12,7 +12,7 @@ c_int, c_uint32, c_uint64, c_size_t, c_void_p, c_char_p, c_float = (
     ctypes.c_float)
 
 LIB_NAME = "liblz4mt_amd.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+LIB_PATH = os.environ.get("LZ4MT_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 # Lz4MtMode (src/lz4mt.h:61-66) + the DEVICE extension bit
 MODE_PARALLEL = 0

@@ -839,7 +839,9 @@ __device__ int32_t encode_block_t(g_cu8* __restrict__ s, uint32_t n, g_u8* __res
             pe.total = pe.a2 + 2 + mlExt;
             pe.op = op;
             pe.anchor = anchor;
-            pe.direct = back == 0 && pe.total <= 64;   // lbo already holds each lane's literal
+            // lbo (loaded for lit0) is still each output lane's literal after a
+            // catch-up unless the literal-length extension changed size
+            pe.direct = pe.total <= 64 && litExt == ext_len(lit0);
             peLb = lb;
             peLbo = lbo;
             asm volatile("" : "+v"(peLb), "+v"(peLbo));   // settle them here, not under the next round trip
