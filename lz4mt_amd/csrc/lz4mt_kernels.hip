@@ -872,14 +872,340 @@ __device__ int32_t encode_block_t(g_cu8* __restrict__ s, uint32_t n, g_u8* __res
     return (int32_t)op;
 }
 
-// 20 KiB per wave (8 waves per CU): table + dedup scratch + 3 KiB shared by
-// the paths (encode_block: 2 KiB source ring + 1 KiB output ring;
-// encode_block_t: 2 KiB + 64 B mirrored source ring)
-#define ENCODE_LDS                                                               \
-    __shared__ __attribute__((aligned(16))) uint32_t T[4096];        /* 16 KiB */ \
-    __shared__ __attribute__((aligned(16))) uint32_t X[768];         /* 3 KiB */  \
-    __shared__ __attribute__((aligned(16))) uint8_t S[kDedup];       /* 1 KiB */
+// ---------------------------------------------------------------------------
+// Encoder v5: the frame path's encoder for 65547 <= n <= 4 MiB (same parse
+// and bytes as encode_block / encode_block_t, LZ4 1.9.3 SURVEY.md App. A),
+// laid out for the fewest instructions per window:
+//   * fixed lane roles: lane 0 INSERT, lane 1 TEST, lanes 2..63 SEARCH
+//     probes k0 .. k0+61 (step 1 for the first 64 probes: p = sPos + L - 2)
+//   * every LDS op is branch-free: lanes with nothing to do address their
+//     own dummy slot (T[4096 + L]) instead of toggling EXEC
+//   * the table is probed with the lane's FINAL entry as marker (position |
+//     tag); a readback that differs flags a same-bucket collision, and the
+//     exact predecessor resolution runs only when a collision reaches a lane
+//     at or before the first stop (about 1 window in 20)
+//   * ballots go straight to SGPRs (no v_cndmask + v_cmp per ballot)
+//   * the previous sequence's bytes are stored during this window's round
+//     trip, literal bytes taken from the LDS source ring
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t bal(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ uint32_t sff1(uint64_t m) { return m ? (uint32_t)__builtin_ctzll(m) : 64u; }
+constexpr uint32_t kDummy = 4096;   // T[4096 + L]: lane L's dummy slot (inside the 1 KiB scratch)
+
+// one encoded sequence whose bytes are stored during the next round trip
+struct PendSeq {
+    uint32_t op, total, a1, a2, token, litRem, mlRem, off, anchor;
+};
+// byte x of a sequence: token | literal-length ext | literals | offset | match-length ext
+// (flat selects: a nested ?: here is turned into an EXEC-mask branch)
+__device__ __forceinline__ uint32_t pend_byte(const PendSeq& e, uint32_t x, uint32_t litByte) {
+    const uint32_t vM = x + 1 < e.total ? 255u : e.mlRem;
+    const uint32_t vL = x + 1 < e.a1 ? 255u : e.litRem;
+    const uint32_t vO = x == e.a2 ? e.off & 255u : e.off >> 8;
+    uint32_t v = x < e.a2 + 2 ? vO : vM;
+    v = x < e.a2 ? litByte : v;
+    v = x < e.a1 ? vL : v;
+    asm volatile("" : "+v"(v));
+    return x == 0 ? e.token : v;
+}
+// The literal byte is made opaque right after its load, so the select chain
+// stays selects (no load sunk into a branch) and the store waits only on the
+// counter of its own load: LDS (ring, the common case) never waits on the
+// round-trip loads in flight.
+__device__ __forceinline__ void store_pend(const PendSeq& e, const SrcRing& V, g_cu8* __restrict__ s,
+                                           g_u8* __restrict__ d) {
+    const uint32_t L = laneid();
+    const uint32_t lit = e.a2 - e.a1;
+    if (e.anchor >= V.B && e.anchor + lit <= V.B + kSR) {
+        for (uint32_t base = 0; base < e.total; base += 64) {
+            const uint32_t x = min(base + L, e.total - 1);   // lanes past the end repeat the last byte
+            uint32_t lv = V.r[(e.anchor + x - e.a1) & (kSR - 1)];
+            asm volatile("" : "+v"(lv));
+            d[e.op + x] = (uint8_t)pend_byte(e, x, lv);
+        }
+    } else {   // literals no longer (or not yet) in the ring: global bytes
+        for (uint32_t base = 0; base < e.total; base += 64) {
+            const uint32_t x = min(base + L, e.total - 1);
+            uint32_t lv = s[(x >= e.a1 && x < e.a2) ? e.anchor + x - e.a1 : e.anchor];
+            asm volatile("" : "+v"(lv));
+            d[e.op + x] = (uint8_t)pend_byte(e, x, lv);
+        }
+    }
+}
+
+template <bool ST>
+__device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
+                                   l_u32* __restrict__ T, l_u8* __restrict__ R, uint64_t* acc) {
+    const uint32_t L = laneid();
+    uint64_t ts = STAMP_T();
+    const uint32_t bound = n + n / 255 + 16;
+    const bool limited = cap < bound;
+    {
+        const uint32_t t0 = cand_tag(gld4u(s)) << kPosBits;   // fresh entry = position 0 (a real candidate)
+        for (uint32_t i = L; i < 1024; i += 64) ((l_u4*)T)[i] = (v4u){t0, t0, t0, t0};
+    }
+    SrcRing V{s, n, R, 0, 0, 0};
+    V.init();
+    const uint32_t mflimitP1 = n - kMfLimit + 1;
+    const uint32_t matchlimit = n - kLastLiterals;
+    const uint32_t last4 = n - 4;
+    const uint32_t dumIdx = kDummy + L;
+    uint32_t anchor = 0, op = 0;
+    PendSeq pe{};
+    bool havePe = false;
+    // window: lane 0 INSERT insPos, lane 1 TEST testPos, lane L >= 2 SEARCH probe k0 + L - 2 at sPos + F(k)
+    bool insOn = true, testOn = false;
+    uint32_t insPos = 0, testPos = 0, sPos = 1, k0 = 0;
+    for (;;) {
+        if (ST) acc[10] += 1;
+        // ---- probe positions (uniform lo/hi bound the window's bytes)
+        uint32_t p, step, sLo, sHi;
+        if (k0 == 0) {
+            p = sPos + L - 2;
+            step = 1;
+            sLo = sPos;
+            sHi = sPos + 61;
+        } else {
+            const uint32_t kk = k0 + L - 2, km1 = kk - 1, q = km1 >> 6, r6 = km1 & 63u;
+            p = sPos + 1u + 32u * q * (q + 1u) + r6 * (q + 1u);
+            step = (63u + kk) >> 6;
+            sLo = sPos + probe_off(k0);
+            sHi = sPos + probe_off(k0 + 61);
+        }
+        p = L == 0 ? insPos : (L == 1 ? testPos : p);
+        const bool srch = L >= 2;
+        const bool live = srch ? p <= mflimitP1 : (L == 0 ? insOn : testOn);
+        const bool term = srch && live && p + step > mflimitP1;
+        const uint32_t lo = insOn ? insPos : (testOn ? testPos : sLo);
+        const uint32_t hi = (sHi < mflimitP1 ? sHi : mflimitP1) + 8;
+        uint64_t v8;
+        if (hi - lo <= 1024) {
+            V.cover(hi);
+            v8 = V.rd8(p);
+        } else {   // wide window (long searches): hash inputs straight from global
+            if (ST) acc[13] += 1;
+            v8 = gld8u(s + (p < n - 8 ? p : n - 8));
+            uint32_t a = (uint32_t)v8, b = (uint32_t)(v8 >> 32);
+            asm volatile("" : "+v"(a), "+v"(b));   // land it here, not at the join
+            v8 = ((uint64_t)b << 32) | a;
+        }
+        const uint32_t w0 = (uint32_t)v8;
+        const uint32_t h = lz4_hash<false>(w0, (uint32_t)(v8 >> 32));
+        const uint32_t mark = p | (cand_tag(w0) << kPosBits);   // the lane's final table entry
+        // ---- table probe: read, write the marker, read back (LDS ops of a wave run in order)
+        const uint32_t ti = live ? h : dumIdx;
+        const uint32_t told = T[ti];
+        T[ti] = mark;
+        WAVE_SYNC();
+        const uint32_t sv = T[ti];
+        const uint64_t pend = bal(sv != mark);   // same-bucket collision inside the window
+        uint32_t cand = told & kPosMask;
+        const bool cok = live && L != 0 && !term && cand + kDistMax >= p;
+        bool maybe = cok && (told >> kPosBits) == (mark >> kPosBits);
+        const uint64_t tmk = bal(term);
+        uint64_t sm = bal(maybe) | tmk;
+        uint64_t mm = sm & ~tmk;
+        STAMP_ADD(0, ts);
+        // ---- resolve the first stop.  Exact in-window predecessors are
+        // resolved (once) whenever a collision reaches the current stop
+        // candidate -- also after a tag alias moved the stop further out.
+        // The round trip: verify word + forward count words, catch-up bytes;
+        // the previous sequence's stores go out behind them.
+        uint32_t w;
+        bool dd = false;
+        uint64_t gmask = 0, aliased = 0;
+        uint32_t ip = 0, cd = 0, maxb = 0, cw = 0, iw = 0, bi = 0, bc = 0;
+        bool wTerm = false;
+        for (;;) {
+            w = sff1(sm);
+            if (!dd && (pend & mask_le(w < 63 ? w : 63))) {
+                if (ST) acc[12] += 1;
+                dd = true;
+                int pred = -1;
+                gmask = 1ull << L;
+                uint64_t todo = pend;
+                while (todo) {   // one iteration per group of equal hashes
+                    const uint32_t key = rdlane(h, (int)sff1(todo));
+                    const uint64_t m = bal(live && h == key);
+                    const bool inG = (m >> L) & 1;
+                    const uint64_t below = m & ((1ull << L) - 1ull);
+                    pred = inG ? (below ? 63 - __clzll((long long)below) : -1) : pred;
+                    gmask = inG ? m : gmask;
+                    todo &= ~m;
+                }
+                const int pi = (pred < 0 ? 0 : pred) * 4;
+                const uint32_t pw = (uint32_t)__builtin_amdgcn_ds_bpermute(pi, (int)w0);   // predecessor's bytes
+                const uint32_t pp = (uint32_t)__builtin_amdgcn_ds_bpermute(pi, (int)p);    // and position
+                const bool ok = live && L != 0 && !term && pred >= 0 && pp + kDistMax >= p && pw == w0;
+                maybe = maybe && pred < 0;
+                cand = pred >= 0 ? pp : cand;
+                mm = bal(maybe);
+                sm = (bal(ok) | mm | tmk) & ~aliased;
+                continue;
+            }
+            wTerm = w < 64 && ((tmk >> w) & 1);
+            if (w == 64 || wTerm) break;
+            ip = rdlane(p, (int)w);
+            cd = rdlane(cand, (int)w);
+            maxb = w == 1 ? 0u : min(ip - anchor, cd);
+            const uint32_t ci = cd + 4 * L, ii = ip + 4 * L;
+            cw = gld4u(s + (ci < last4 ? ci : last4));   // lane 0: verify word; lanes >= 1: count words
+            iw = gld4u(s + (ii < last4 ? ii : last4));
+            const bool bOn = L < maxb;
+            bi = s[bOn ? ip - L - 1 : 0u];
+            bc = s[bOn ? cd - L - 1 : 0u];
+            if (havePe) {
+                store_pend(pe, V, s, d);
+                havePe = false;
+            }
+            if (((mm >> w) & 1) && rdlane(cw, 0) != rdlane(w0, (int)w)) {   // tag alias: no match here
+                if (ST) acc[11] += 1;
+                // drain this try's loads here, so the loop head's load
+                // registers carry nothing pending into the common path
+                __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+                aliased |= 1ull << w;
+                sm &= ~(1ull << w);
+                continue;
+            }
+            break;
+        }
+        if (havePe) {
+            store_pend(pe, V, s, d);
+            havePe = false;
+        }
+        STAMP_ADD(1, ts);
+        // ---- table writes: lanes past the stop put the old entry back; on a
+        // collision the lanes up to the stop re-insert (last member of each group)
+        {
+            const int wlim = (w == 64) ? 63 : (wTerm ? (int)w - 1 : (int)w);
+            const bool le = (int)L <= wlim;
+            T[(live && !le) ? h : dumIdx] = told;
+            if (pend) {
+                const uint64_t upto = wlim < 0 ? 0ull : mask_le((uint32_t)wlim);
+                const bool lastM = !dd || !(gmask & ~mask_le(L) & upto);
+                T[(live && le && lastM) ? h : dumIdx] = mark;
+            }
+            WAVE_SYNC();
+        }
+        STAMP_ADD(2, ts);
+        if (w == 64) {   // no stop: the search goes on
+            k0 += 62;
+            insOn = false;
+            testOn = false;
+            continue;
+        }
+        if (wTerm) break;
+        // ---- catch-up (backwards) and LZ4_count (forwards from ip + 4)
+        // (bi/bc are consumed on every path, so no load of this window is
+        // left pending into the next window's round trip)
+        uint32_t back = 0;
+        asm volatile("" ::"v"(bi), "v"(bc));
+        uint64_t fm = ~bal(L < maxb && bi == bc);
+        if (maxb) {
+            for (;;) {
+                if (fm) {
+                    back += (uint32_t)__builtin_ctzll(fm);
+                    break;
+                }
+                back += 64;
+                if (back >= maxb) {
+                    back = maxb;
+                    break;
+                }
+                const uint32_t kb = back + L + 1;
+                const bool on = kb <= maxb;
+                fm = ~bal(on && s[on ? ip - kb : 0u] == s[on ? cd - kb : 0u]);
+            }
+        }
+        const uint32_t lim = matchlimit - (ip + kMinMatch);
+        uint32_t mc;
+        {
+            const uint32_t rel = 4 * L - 4;
+            const uint32_t x = cw ^ iw;
+            uint32_t e = min(x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u, lim - rel);
+            e = (L != 0 && rel < lim) ? e : 0u;
+            const uint64_t nf = bal(L != 0 && e < 4);
+            if (nf) {
+                const uint32_t f = (uint32_t)__builtin_ctzll(nf);
+                mc = 4 * (f - 1) + rdlane(e, (int)f);
+            } else {
+                mc = 252;
+                for (;;) {   // long match: 256 bytes per round
+                    const uint32_t r2 = mc + 4 * L;
+                    const uint32_t a2 = ip + kMinMatch + r2, c2 = cd + kMinMatch + r2;
+                    const uint32_t x2 = gld4u(s + (a2 < last4 ? a2 : last4)) ^ gld4u(s + (c2 < last4 ? c2 : last4));
+                    uint32_t e2 = min(x2 ? ((uint32_t)__builtin_ctz(x2) >> 3) : 4u, lim - r2);
+                    e2 = r2 < lim ? e2 : 0u;
+                    const uint64_t nf2 = bal(e2 < 4);
+                    if (nf2) {
+                        const uint32_t f = (uint32_t)__builtin_ctzll(nf2);
+                        mc += 4 * f + rdlane(e2, (int)f);
+                        break;
+                    }
+                    mc += 256;
+                }
+            }
+        }
+        STAMP_ADD(3, ts);
+        // ---- sequence layout (stored during the next round trip)
+        {
+            const uint32_t lit = ip - anchor - back, mcf = mc + back;
+            const uint32_t litExt = ext_len(lit), mlExt = ext_len(mcf);
+            if (limited) {
+                if (w != 1 && op + 1 + lit + 8 + lit / 255 > cap) return 0;
+                if (op + 1 + litExt + lit + 2 + 6 + (mcf + 240) / 255 > cap) return 0;
+            }
+            pe.op = op;
+            pe.token = ((lit < 15 ? lit : 15) << 4) | (mcf < 15 ? mcf : 15);
+            pe.litRem = lit >= 15 ? (lit - 15) % 255 : 0u;
+            pe.mlRem = mcf >= 15 ? (mcf - 15) % 255 : 0u;
+            pe.off = ip - cd;
+            pe.anchor = anchor;
+            pe.a1 = 1 + litExt;
+            pe.a2 = pe.a1 + lit;
+            pe.total = pe.a2 + 2 + mlExt;
+            havePe = true;
+            op += pe.total;
+        }
+        STAMP_ADD(4, ts);
+        const uint32_t ipe = ip + kMinMatch + mc;
+        anchor = ipe;
+        if (ipe >= mflimitP1) break;
+        insOn = true;
+        testOn = true;
+        insPos = ipe - 2;
+        testPos = ipe;
+        sPos = ipe + 1;
+        k0 = 0;
+    }
+    if (havePe) store_pend(pe, V, s, d);
+    // ---- last literals
+    {
+        const uint32_t run = n - anchor;
+        if (limited && op + run + 1 + (run + 240) / 255 > cap) return 0;
+        const uint32_t ext = ext_len(run), rem = run >= 15 ? (run - 15) % 255 : 0u;
+        if (L == 0) d[op] = (uint8_t)((run < 15 ? run : 15) << 4);
+        for (uint32_t x = L; x < ext; x += 64) d[op + 1 + x] = (uint8_t)(x + 1 < ext ? 255u : rem);
+        op += 1 + ext;
+        for (uint32_t x = L; x < run; x += 64) d[op + x] = s[anchor + x];
+        op += run;
+    }
+    return (int32_t)op;
+}
+
+// 20 KiB per wave (8 waves per CU), one array so lanes can address dummy
+// slots branch-free:
+//   [0, 16 KiB)          hash table (4096 x u32, or 8192 x u16)
+//   [16 KiB, 17 KiB)     dedup scratch (encode_block) / dummy slots (v5)
+//   [17 KiB, 20 KiB)     encode_block: 2 KiB source ring + 1 KiB output ring;
+//                        encode_block_t / v5: 2 KiB + 64 B mirrored source ring
+#define ENCODE_LDS                                                     \
+    __shared__ __attribute__((aligned(16))) uint32_t ELDS[5120];       \
+    uint32_t* const T = ELDS;                                          \
+    uint8_t* const S = (uint8_t*)(ELDS + 4096);                        \
+    uint32_t* const X = ELDS + 4352;
 static_assert(kSR + kSRMirror <= 3072, "ring exceeds the shared scratch");
+static_assert(kDedup == 1024, "scratch layout");
 
 __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, uint64_t srcSize, uint32_t blockSize,
                                                uint8_t* __restrict__ slots, uint64_t slotStride,
@@ -898,7 +1224,11 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
     if (n < (uint32_t)kLimit64K)
         r = encode_block<true, false, false>(s, n, d, cap, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
     else if (n <= (1u << kPosBits))
+#ifdef LZ4MT_ENC_T
         r = encode_block_t<false>(s, n, d, cap, Tl, Sl, Xl, nullptr);
+#else
+        r = encode_block_v5<false>(s, n, d, cap, Tl, Xl, nullptr);
+#endif
     else
         r = encode_block<false, false, false>(s, n, d, cap, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
     if (laneid() == 0) csize[b] = r;
@@ -921,7 +1251,11 @@ __global__ void __launch_bounds__(64) k_encode_stats(const uint8_t* __restrict__
     if (n < (uint32_t)kLimit64K)
         r = encode_block<true, false, true>(s, n, d, n, (l_u32*)T, (l_u8*)S, (l_u32*)Xl, Xl + kRingE, acc);
     else if (n <= (1u << kPosBits))
+#ifdef LZ4MT_ENC_T
         r = encode_block_t<true>(s, n, d, n, (l_u32*)T, (l_u8*)S, Xl, acc);
+#else
+        r = encode_block_v5<true>(s, n, d, n, (l_u32*)T, Xl, acc);
+#endif
     else
         r = encode_block<false, false, true>(s, n, d, n, (l_u32*)T, (l_u8*)S, (l_u32*)Xl, Xl + kRingE, acc);
     if (laneid() == 0) {
