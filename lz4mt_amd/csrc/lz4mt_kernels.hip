@@ -893,12 +893,25 @@ __device__ __forceinline__ uint32_t sff1(uint64_t m) { return m ? (uint32_t)__bu
 constexpr uint32_t kDummy = 4096;   // T[4096 + L]: lane L's dummy slot (inside the 1 KiB scratch)
 
 // one encoded sequence whose bytes are stored during the next round trip
+// (few loop-carried fields; the layout is derived at store time)
 struct PendSeq {
-    uint32_t op, total, a1, a2, token, litRem, mlRem, off, anchor;
+    uint32_t op, lit, mcf, off, anchor;
+};
+struct SeqLayout {
+    uint32_t total, a1, a2, token, litRem, mlRem, off;
+    __device__ __forceinline__ explicit SeqLayout(const PendSeq& e) {
+        a1 = 1 + ext_len(e.lit);
+        a2 = a1 + e.lit;
+        total = a2 + 2 + ext_len(e.mcf);
+        token = ((e.lit < 15 ? e.lit : 15) << 4) | (e.mcf < 15 ? e.mcf : 15);
+        litRem = e.lit >= 15 ? (e.lit - 15) % 255 : 0u;
+        mlRem = e.mcf >= 15 ? (e.mcf - 15) % 255 : 0u;
+        off = e.off;
+    }
 };
 // byte x of a sequence: token | literal-length ext | literals | offset | match-length ext
 // (flat selects: a nested ?: here is turned into an EXEC-mask branch)
-__device__ __forceinline__ uint32_t pend_byte(const PendSeq& e, uint32_t x, uint32_t litByte) {
+__device__ __forceinline__ uint32_t pend_byte(const SeqLayout& e, uint32_t x, uint32_t litByte) {
     const uint32_t vM = x + 1 < e.total ? 255u : e.mlRem;
     const uint32_t vL = x + 1 < e.a1 ? 255u : e.litRem;
     const uint32_t vO = x == e.a2 ? e.off & 255u : e.off >> 8;
@@ -912,23 +925,23 @@ __device__ __forceinline__ uint32_t pend_byte(const PendSeq& e, uint32_t x, uint
 // stays selects (no load sunk into a branch) and the store waits only on the
 // counter of its own load: LDS (ring, the common case) never waits on the
 // round-trip loads in flight.
-__device__ __forceinline__ void store_pend(const PendSeq& e, const SrcRing& V, g_cu8* __restrict__ s,
+__device__ __forceinline__ void store_pend(const PendSeq& p, const SrcRing& V, g_cu8* __restrict__ s,
                                            g_u8* __restrict__ d) {
     const uint32_t L = laneid();
-    const uint32_t lit = e.a2 - e.a1;
-    if (e.anchor >= V.B && e.anchor + lit <= V.B + kSR) {
+    const SeqLayout e(p);
+    if (p.anchor >= V.B && p.anchor + p.lit <= V.B + kSR) {
         for (uint32_t base = 0; base < e.total; base += 64) {
             const uint32_t x = min(base + L, e.total - 1);   // lanes past the end repeat the last byte
-            uint32_t lv = V.r[(e.anchor + x - e.a1) & (kSR - 1)];
+            uint32_t lv = V.r[(p.anchor + x - e.a1) & (kSR - 1)];
             asm volatile("" : "+v"(lv));
-            d[e.op + x] = (uint8_t)pend_byte(e, x, lv);
+            d[p.op + x] = (uint8_t)pend_byte(e, x, lv);
         }
     } else {   // literals no longer (or not yet) in the ring: global bytes
         for (uint32_t base = 0; base < e.total; base += 64) {
             const uint32_t x = min(base + L, e.total - 1);
-            uint32_t lv = s[(x >= e.a1 && x < e.a2) ? e.anchor + x - e.a1 : e.anchor];
+            uint32_t lv = s[(x >= e.a1 && x < e.a2) ? p.anchor + x - e.a1 : p.anchor];
             asm volatile("" : "+v"(lv));
-            d[e.op + x] = (uint8_t)pend_byte(e, x, lv);
+            d[p.op + x] = (uint8_t)pend_byte(e, x, lv);
         }
     }
 }
@@ -954,9 +967,19 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     PendSeq pe{};
     bool havePe = false;
     // window: lane 0 INSERT insPos, lane 1 TEST testPos, lane L >= 2 SEARCH probe k0 + L - 2 at sPos + F(k)
-    bool insOn = true, testOn = false;
-    uint32_t insPos = 0, testPos = 0, sPos = 1, k0 = 0;
-    for (;;) {
+    // window state: sPos, k0 and the mode (0 continuation: search only;
+    // 1 after a match at sPos - 1: INSERT sPos - 3, TEST sPos - 1; 2 first
+    // window: INSERT 0)
+    uint32_t sPos = 1, k0 = 0, mode = 2;
+    // ONE exit and no continue: the structurizer then needs no flow
+    // variables and the loop-carried state stays in place across windows
+    bool done = false, fail = false;
+    while (!done) {
+      // windows without a stop (continuations) loop here, inside: the
+      // match-path state (anchor, op, pe) is not touched by them
+      uint32_t w, ip, cd, maxb, cw, iw, bi, bc;
+      bool wTerm;
+      do {
         if (ST) acc[10] += 1;
         // ---- probe positions (uniform lo/hi bound the window's bytes)
         uint32_t p, step, sLo, sHi;
@@ -972,11 +995,13 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             sLo = sPos + probe_off(k0);
             sHi = sPos + probe_off(k0 + 61);
         }
+        const bool insOn = mode != 0, testOn = mode == 1;
+        const uint32_t insPos = mode == 2 ? 0u : sPos - 3, testPos = sPos - 1;
         p = L == 0 ? insPos : (L == 1 ? testPos : p);
         const bool srch = L >= 2;
         const bool live = srch ? p <= mflimitP1 : (L == 0 ? insOn : testOn);
         const bool term = srch && live && p + step > mflimitP1;
-        const uint32_t lo = insOn ? insPos : (testOn ? testPos : sLo);
+        const uint32_t lo = insOn ? insPos : sLo;
         const uint32_t hi = (sHi < mflimitP1 ? sHi : mflimitP1) + 8;
         uint64_t v8;
         if (hi - lo <= 1024) {
@@ -1003,20 +1028,21 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         const bool cok = live && L != 0 && !term && cand + kDistMax >= p;
         bool maybe = cok && (told >> kPosBits) == (mark >> kPosBits);
         const uint64_t tmk = bal(term);
-        uint64_t sm = bal(maybe) | tmk;
-        uint64_t mm = sm & ~tmk;
+        uint64_t mm = bal(maybe);
+        uint64_t sm = mm | tmk;
         STAMP_ADD(0, ts);
         // ---- resolve the first stop.  Exact in-window predecessors are
         // resolved (once) whenever a collision reaches the current stop
         // candidate -- also after a tag alias moved the stop further out.
         // The round trip: verify word + forward count words, catch-up bytes;
         // the previous sequence's stores go out behind them.
-        uint32_t w;
+        w = 64;
         bool dd = false;
         uint64_t gmask = 0, aliased = 0;
-        uint32_t ip = 0, cd = 0, maxb = 0, cw = 0, iw = 0, bi = 0, bc = 0;
-        bool wTerm = false;
-        for (;;) {
+        ip = 0; cd = 0; maxb = 0; cw = 0; iw = 0; bi = 0; bc = 0;
+        wTerm = false;
+        bool again = true;
+        while (again) {
             w = sff1(sm);
             if (!dd && (pend & mask_le(w < 63 ? w : 63))) {
                 if (ST) acc[12] += 1;
@@ -1041,33 +1067,34 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                 cand = pred >= 0 ? pp : cand;
                 mm = bal(maybe);
                 sm = (bal(ok) | mm | tmk) & ~aliased;
-                continue;
+            } else {
+                wTerm = w < 64 && ((tmk >> w) & 1);
+                again = false;
+                if (w < 64 && !wTerm) {
+                    ip = rdlane(p, (int)w);
+                    cd = rdlane(cand, (int)w);
+                    maxb = w == 1 ? 0u : min(ip - anchor, cd);
+                    const uint32_t ci = cd + 4 * L, ii = ip + 4 * L;
+                    cw = gld4u(s + (ci < last4 ? ci : last4));   // lane 0: verify word; lanes >= 1: count words
+                    iw = gld4u(s + (ii < last4 ? ii : last4));
+                    const bool bOn = L < maxb;
+                    bi = s[bOn ? ip - L - 1 : 0u];
+                    bc = s[bOn ? cd - L - 1 : 0u];
+                    if (havePe) {
+                        store_pend(pe, V, s, d);
+                        havePe = false;
+                    }
+                    if (((mm >> w) & 1) && rdlane(cw, 0) != rdlane(w0, (int)w)) {   // tag alias: no match here
+                        if (ST) acc[11] += 1;
+                        // drain this try's loads here, so the loop head's load
+                        // registers carry nothing pending into the common path
+                        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+                        aliased |= 1ull << w;
+                        sm &= ~(1ull << w);
+                        again = true;
+                    }
+                }
             }
-            wTerm = w < 64 && ((tmk >> w) & 1);
-            if (w == 64 || wTerm) break;
-            ip = rdlane(p, (int)w);
-            cd = rdlane(cand, (int)w);
-            maxb = w == 1 ? 0u : min(ip - anchor, cd);
-            const uint32_t ci = cd + 4 * L, ii = ip + 4 * L;
-            cw = gld4u(s + (ci < last4 ? ci : last4));   // lane 0: verify word; lanes >= 1: count words
-            iw = gld4u(s + (ii < last4 ? ii : last4));
-            const bool bOn = L < maxb;
-            bi = s[bOn ? ip - L - 1 : 0u];
-            bc = s[bOn ? cd - L - 1 : 0u];
-            if (havePe) {
-                store_pend(pe, V, s, d);
-                havePe = false;
-            }
-            if (((mm >> w) & 1) && rdlane(cw, 0) != rdlane(w0, (int)w)) {   // tag alias: no match here
-                if (ST) acc[11] += 1;
-                // drain this try's loads here, so the loop head's load
-                // registers carry nothing pending into the common path
-                __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-                aliased |= 1ull << w;
-                sm &= ~(1ull << w);
-                continue;
-            }
-            break;
         }
         if (havePe) {
             store_pend(pe, V, s, d);
@@ -1090,94 +1117,77 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         STAMP_ADD(2, ts);
         if (w == 64) {   // no stop: the search goes on
             k0 += 62;
-            insOn = false;
-            testOn = false;
-            continue;
+            mode = 0;
         }
-        if (wTerm) break;
-        // ---- catch-up (backwards) and LZ4_count (forwards from ip + 4)
-        // (bi/bc are consumed on every path, so no load of this window is
-        // left pending into the next window's round trip)
-        uint32_t back = 0;
-        asm volatile("" ::"v"(bi), "v"(bc));
-        uint64_t fm = ~bal(L < maxb && bi == bc);
-        if (maxb) {
-            for (;;) {
-                if (fm) {
-                    back += (uint32_t)__builtin_ctzll(fm);
-                    break;
-                }
+      } while (w == 64);
+        if (wTerm) {
+            done = true;
+        } else {
+            // ---- catch-up (backwards) and LZ4_count (forwards from ip + 4).
+            // bi/bc are consumed on every path, so no load of this window is
+            // left pending into the next window's round trip.
+            asm volatile("" ::"v"(bi), "v"(bc));
+            uint64_t fm = ~bal(L < maxb && bi == bc);
+            uint32_t back = 0;
+            while (fm == 0 && back + 64 < maxb) {   // catch-up longer than 64 bytes
                 back += 64;
-                if (back >= maxb) {
-                    back = maxb;
-                    break;
-                }
                 const uint32_t kb = back + L + 1;
                 const bool on = kb <= maxb;
                 fm = ~bal(on && s[on ? ip - kb : 0u] == s[on ? cd - kb : 0u]);
             }
-        }
-        const uint32_t lim = matchlimit - (ip + kMinMatch);
-        uint32_t mc;
-        {
-            const uint32_t rel = 4 * L - 4;
-            const uint32_t x = cw ^ iw;
-            uint32_t e = min(x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u, lim - rel);
-            e = (L != 0 && rel < lim) ? e : 0u;
-            const uint64_t nf = bal(L != 0 && e < 4);
-            if (nf) {
-                const uint32_t f = (uint32_t)__builtin_ctzll(nf);
-                mc = 4 * (f - 1) + rdlane(e, (int)f);
-            } else {
-                mc = 252;
-                for (;;) {   // long match: 256 bytes per round
-                    const uint32_t r2 = mc + 4 * L;
-                    const uint32_t a2 = ip + kMinMatch + r2, c2 = cd + kMinMatch + r2;
-                    const uint32_t x2 = gld4u(s + (a2 < last4 ? a2 : last4)) ^ gld4u(s + (c2 < last4 ? c2 : last4));
-                    uint32_t e2 = min(x2 ? ((uint32_t)__builtin_ctz(x2) >> 3) : 4u, lim - r2);
-                    e2 = r2 < lim ? e2 : 0u;
-                    const uint64_t nf2 = bal(e2 < 4);
-                    if (nf2) {
-                        const uint32_t f = (uint32_t)__builtin_ctzll(nf2);
-                        mc += 4 * f + rdlane(e2, (int)f);
-                        break;
+            back = fm ? back + (uint32_t)__builtin_ctzll(fm) : maxb;
+            const uint32_t lim = matchlimit - (ip + kMinMatch);
+            uint32_t mc;
+            {
+                const uint32_t rel = 4 * L - 4;
+                const uint32_t x = cw ^ iw;
+                uint32_t e = min(x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u, lim - rel);
+                e = (L != 0 && rel < lim) ? e : 0u;
+                const uint64_t nf = bal(L != 0 && e < 4);
+                if (nf) {
+                    const uint32_t f = (uint32_t)__builtin_ctzll(nf);
+                    mc = 4 * (f - 1) + rdlane(e, (int)f);
+                } else {
+                    mc = 252;
+                    uint64_t nf2 = 0;
+                    while (!nf2) {   // long match: 256 bytes per round
+                        const uint32_t r2 = mc + 4 * L;
+                        const uint32_t a2 = ip + kMinMatch + r2, c2 = cd + kMinMatch + r2;
+                        const uint32_t x2 =
+                            gld4u(s + (a2 < last4 ? a2 : last4)) ^ gld4u(s + (c2 < last4 ? c2 : last4));
+                        uint32_t e2 = min(x2 ? ((uint32_t)__builtin_ctz(x2) >> 3) : 4u, lim - r2);
+                        e2 = r2 < lim ? e2 : 0u;
+                        nf2 = bal(e2 < 4);
+                        mc += nf2 ? 4 * (uint32_t)__builtin_ctzll(nf2) + rdlane(e2, (int)__builtin_ctzll(nf2))
+                                  : 256u;
                     }
-                    mc += 256;
                 }
             }
-        }
-        STAMP_ADD(3, ts);
-        // ---- sequence layout (stored during the next round trip)
-        {
+            STAMP_ADD(3, ts);
+            // ---- sequence layout (stored during the next round trip)
             const uint32_t lit = ip - anchor - back, mcf = mc + back;
             const uint32_t litExt = ext_len(lit), mlExt = ext_len(mcf);
             if (limited) {
-                if (w != 1 && op + 1 + lit + 8 + lit / 255 > cap) return 0;
-                if (op + 1 + litExt + lit + 2 + 6 + (mcf + 240) / 255 > cap) return 0;
+                fail = (w != 1 && op + 1 + lit + 8 + lit / 255 > cap) ||
+                       (op + 1 + litExt + lit + 2 + 6 + (mcf + 240) / 255 > cap);
             }
             pe.op = op;
-            pe.token = ((lit < 15 ? lit : 15) << 4) | (mcf < 15 ? mcf : 15);
-            pe.litRem = lit >= 15 ? (lit - 15) % 255 : 0u;
-            pe.mlRem = mcf >= 15 ? (mcf - 15) % 255 : 0u;
+            pe.lit = lit;
+            pe.mcf = mcf;
             pe.off = ip - cd;
             pe.anchor = anchor;
-            pe.a1 = 1 + litExt;
-            pe.a2 = pe.a1 + lit;
-            pe.total = pe.a2 + 2 + mlExt;
-            havePe = true;
-            op += pe.total;
+            havePe = !fail;
+            op += 1 + litExt + lit + 2 + mlExt;
+            const uint32_t ipe = ip + kMinMatch + mc;
+            anchor = ipe;
+            done = fail || ipe >= mflimitP1;
+            mode = 1;
+            sPos = ipe + 1;
+            k0 = 0;
+            STAMP_ADD(4, ts);
         }
-        STAMP_ADD(4, ts);
-        const uint32_t ipe = ip + kMinMatch + mc;
-        anchor = ipe;
-        if (ipe >= mflimitP1) break;
-        insOn = true;
-        testOn = true;
-        insPos = ipe - 2;
-        testPos = ipe;
-        sPos = ipe + 1;
-        k0 = 0;
     }
+    if (fail) return 0;
     if (havePe) store_pend(pe, V, s, d);
     // ---- last literals
     {

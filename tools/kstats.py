@@ -24,12 +24,13 @@ assert L.lib.lz4mtHipDebugEncodeStats(ctypes.c_void_p(src.data_ptr()), n, bm, st
 wall = time.time() - t
 e = list(st16)
 nb = n // bm
-names = ["hash", "table+dedup", "cand check", "round issue", "lit staging", "round wait", "table writes",
-         "count", "emit", "loop-ovh"]
+# encode_block_v5 phases (4 MiB .. 65547 B blocks)
+names = ["probe", "stop+round trip", "table writes", "back+count", "layout", "-", "-", "-", "-", "-"]
 tot = sum(e[:10])
+names[5] = "(loop top)"
 win = max(e[10], 1)
 print(f"ENCODE {gib} GiB B{bid}: wall {wall*1e3:.1f} ms, blocks {nb}, windows {e[10]}, cycles/block {tot/nb:.3e}, "
-      f"tag aliases {e[11]}, tag-candidate winners {e[12]}")
+      f"tag aliases {e[11]}, predecessor resolutions {e[12]}, wide windows {e[13]}")
 for i in range(10):
     print(f"  {names[i]:14s} {e[i]/tot*100:5.1f}%  {e[i]/win:8.1f} cyc/window")
 sd = L.make_sd(bid, False, True)
