@@ -1308,6 +1308,12 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 constexpr int32_t kRing = 16384;   // LDS history ring (bytes)
 constexpr int32_t kInWin = 2048;   // LDS input window (bytes)
 constexpr int32_t kFlush = 1024;   // ring -> HBM flush granule (64 lanes x 16 B)
+// next-sequence table of a batch: u16 per candidate token position (512),
+// plus PAST (element 512) and DEAD (element 513); values are BYTE offsets
+// into the table, so a hop is one dependent ds_read_u16
+constexpr int32_t kNxOff = kInWin + 128;      // inside the win[] allocation
+constexpr uint32_t kNxPast = 1024, kNxDead = 1026;
+constexpr int32_t kWinAlloc = kInWin + 128 + 1040;
 
 template <bool ST>
 struct Dec {
@@ -1495,18 +1501,44 @@ struct Dec {
             }
         }
         STAMP_ADD(11, ts);
-        // 2. hop (bottom-tested, one exit test).  A zero delta ends the chain;
-        // starts past the 64th match no lane and are dropped by the clamp.
-        uint32_t startRel = 0, cnt = 0, cur = 0;
-        do {
-            const uint32_t ln = cur >> 3;
-            const uint32_t wa0 = rdlane(pk0, (int)ln), wa1 = rdlane(pk1, (int)ln);
-            const uint32_t d = (((cur & 4) ? wa1 : wa0) >> ((cur & 3) << 3)) & 255u;
-            startRel = (L == cnt) ? cur : startRel;   // a zero-delta position is not counted
-            cnt += d ? 1u : 0u;
-            cur = d ? cur + d : 512u;
-        } while (cur < 512);
-        cnt = min(cnt, 64u);
+        // 2. hop.  next(i) = i + delta(i) goes into an LDS table (8 entries
+        // per lane, one ds_write_b128); the chain from position 0 is then
+        // one dependent ds_read_u16 per sequence, with every lane running it
+        // redundantly (uniform broadcast reads) and lane m recording x_m and
+        // x_(m+1).  A zero delta (complex token) leads to DEAD, a start past
+        // the 512 candidates to PAST (whose sequence still counts).
+        uint32_t startRel, cnt;
+        {
+            l_u8* const nxb = win + kNxOff;
+            uint32_t nv[4];
+#pragma unroll
+            for (int e2 = 0; e2 < 4; ++e2) {
+                uint32_t pr = 0;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int e = 2 * e2 + h;
+                    const uint32_t d = ((e < 4 ? pk0 : pk1) >> (8 * (e & 3))) & 255u;
+                    const uint32_t pos = 8 * L + (uint32_t)e;
+                    const uint32_t nx = d == 0 ? kNxDead : (pos + d < 512 ? 2 * (pos + d) : kNxPast);
+                    pr |= nx << (16 * h);
+                }
+                nv[e2] = pr;
+            }
+            *(l_u4*)(nxb + 16 * L) = (v4u){nv[0], nv[1], nv[2], nv[3]};
+            WAVE_SYNC();
+            uint32_t x = 0, startA = 0, nextA = kNxDead;
+            for (uint32_t m0 = 0; m0 < 64; m0 += 8) {
+#pragma unroll
+                for (uint32_t e = 0; e < 8; ++e) {
+                    x = *(l_u16*)(nxb + x);
+                    nextA = L == m0 + e ? x : nextA;
+                    startA = L == m0 + e + 1 ? x : startA;
+                }
+                if ((uint32_t)__builtin_amdgcn_readfirstlane((int)x) == kNxDead) break;
+            }
+            cnt = (uint32_t)__popcll(bal(nextA != kNxDead));
+            startRel = startA >> 1;
+        }
         STAMP_ADD(12, ts);
         if (cnt == 0) return 0;
         if (ST) acc[4] += 1;
@@ -1712,6 +1744,7 @@ __device__ int32_t decode_block(Dec<ST>& D, int64_t cap) {
 
     if (cap == 0) return (D.len == 1 && D.in8(0) == 0) ? 0 : -1;
     if (D.len == 0) return -1;
+    *(l_u32*)(D.win + kNxOff + kNxPast) = kNxDead | (kNxDead << 16);   // next(PAST) = next(DEAD) = DEAD
 
 #define PHYS_CHECK(end_) \
     if ((end_) > D.physcap) return kDecodeOutputTooSmall;
@@ -1850,7 +1883,7 @@ __global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ frame
                                                uint32_t blockMax, uint8_t* __restrict__ out, uint64_t outCap,
                                                int32_t* __restrict__ dsize) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
-    __shared__ __attribute__((aligned(16))) uint8_t win[kInWin + 128];   /* + dummy write area */
+    __shared__ __attribute__((aligned(16))) uint8_t win[kWinAlloc];   /* + dummy write area + hop table */
     const uint32_t b = blockIdx.x;
     const BlockRec r = recs[b];
     const uint64_t slot = (uint64_t)b * blockMax;
@@ -1885,7 +1918,7 @@ __global__ void __launch_bounds__(64) k_decode_stats(const uint8_t* __restrict__
                                                      uint8_t* __restrict__ out, uint64_t outCap,
                                                      int32_t* __restrict__ dsize, uint64_t* __restrict__ stats) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
-    __shared__ __attribute__((aligned(16))) uint8_t win[kInWin + 128];   /* + dummy write area */
+    __shared__ __attribute__((aligned(16))) uint8_t win[kWinAlloc];   /* + dummy write area + hop table */
     const uint32_t b = blockIdx.x;
     const BlockRec r = recs[b];
     const uint64_t slot = (uint64_t)b * blockMax;
