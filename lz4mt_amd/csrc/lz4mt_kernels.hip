@@ -237,7 +237,9 @@ struct OutView {
     }
 };
 
-__device__ __forceinline__ uint32_t ext_len(uint32_t v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
+// bytes of a 4-bit length field's extension: (v - 15) / 255 + 1 for v >= 15,
+// else 0 -- one formula for both: (v + 240) / 255
+__device__ __forceinline__ uint32_t ext_len(uint32_t v) { return (v + 240) / 255; }
 
 // Stages literal bytes src[from + i] for i in [i0, i1) at out position
 // base + i, 4 per lane, flushing complete chunks below `safe + i` between
@@ -904,8 +906,8 @@ struct SeqLayout {
         a2 = a1 + e.lit;
         total = a2 + 2 + ext_len(e.mcf);
         token = ((e.lit < 15 ? e.lit : 15) << 4) | (e.mcf < 15 ? e.mcf : 15);
-        litRem = e.lit >= 15 ? (e.lit - 15) % 255 : 0u;
-        mlRem = e.mcf >= 15 ? (e.mcf - 15) % 255 : 0u;
+        litRem = e.lit + 240 - 255 * (a1 - 1);   // (lit - 15) % 255 when an extension exists
+        mlRem = e.mcf + 240 - 255 * ext_len(e.mcf);
         off = e.off;
     }
 };
@@ -1037,8 +1039,22 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         // The round trip: verify word + forward count words, catch-up bytes;
         // the previous sequence's stores go out behind them.
         w = 64;
-        bool dd = false;
+        bool dd = false, twDone = false, twRedo = false;
         uint64_t gmask = 0, aliased = 0;
+        // table writes for stop w: lanes past the stop put the old entry
+        // back; on a collision (or when redone after a tag alias moved the
+        // stop) the lanes up to the stop re-insert (last member of each group)
+        auto table_writes = [&](uint32_t ws, bool wsTerm) {
+            const int wlim = (ws == 64) ? 63 : (wsTerm ? (int)ws - 1 : (int)ws);
+            const bool le = (int)L <= wlim;
+            T[(live && !le) ? h : dumIdx] = told;
+            if (pend || twRedo) {
+                const uint64_t upto = wlim < 0 ? 0ull : mask_le((uint32_t)wlim);
+                const bool lastM = !dd || !(gmask & ~mask_le(L) & upto);
+                T[(live && le && lastM) ? h : dumIdx] = mark;
+            }
+            WAVE_SYNC();
+        };
         ip = 0; cd = 0; maxb = 0; cw = 0; iw = 0; bi = 0; bc = 0;
         wTerm = false;
         bool again = true;
@@ -1084,6 +1100,8 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                         store_pend(pe, V, s, d);
                         havePe = false;
                     }
+                    table_writes(w, false);   // in the round trip's shadow; redone if w moves
+                    twDone = true;
                     if (((mm >> w) & 1) && rdlane(cw, 0) != rdlane(w0, (int)w)) {   // tag alias: no match here
                         if (ST) acc[11] += 1;
                         // drain this try's loads here, so the loop head's load
@@ -1092,6 +1110,8 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                         aliased |= 1ull << w;
                         sm &= ~(1ull << w);
                         again = true;
+                        twDone = false;
+                        twRedo = true;
                     }
                 }
             }
@@ -1100,20 +1120,8 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             store_pend(pe, V, s, d);
             havePe = false;
         }
+        if (!twDone) table_writes(w, wTerm);
         STAMP_ADD(1, ts);
-        // ---- table writes: lanes past the stop put the old entry back; on a
-        // collision the lanes up to the stop re-insert (last member of each group)
-        {
-            const int wlim = (w == 64) ? 63 : (wTerm ? (int)w - 1 : (int)w);
-            const bool le = (int)L <= wlim;
-            T[(live && !le) ? h : dumIdx] = told;
-            if (pend) {
-                const uint64_t upto = wlim < 0 ? 0ull : mask_le((uint32_t)wlim);
-                const bool lastM = !dd || !(gmask & ~mask_le(L) & upto);
-                T[(live && le && lastM) ? h : dumIdx] = mark;
-            }
-            WAVE_SYNC();
-        }
         STAMP_ADD(2, ts);
         if (w == 64) {   // no stop: the search goes on
             k0 += 62;
@@ -1167,7 +1175,9 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             // ---- sequence layout (stored during the next round trip)
             const uint32_t lit = ip - anchor - back, mcf = mc + back;
             const uint32_t litExt = ext_len(lit), mlExt = ext_len(mcf);
-            if (limited) {
+            // 1.9.3's limitedOutput margins; both hold whenever
+            // op + 2 (lit + mcf) + 16 <= cap, so the exact test runs rarely
+            if (limited && op + 2 * (lit + mcf) + 16 > cap) {
                 fail = (w != 1 && op + 1 + lit + 8 + lit / 255 > cap) ||
                        (op + 1 + litExt + lit + 2 + 6 + (mcf + 240) / 255 > cap);
             }

@@ -85,7 +85,8 @@ def encode(s, cap, last_lane_wins=True):
         aliased = set()
         while True:
             w = next((L for L in range(64) if sm[L]), 64)
-            if not dd and any(pend[L] for L in range(min(w, 63) + 1)):
+            collide = any(pend[L] for L in range(min(w, 63) + 1))
+            if not dd and collide:
                 dd = True
                 pred = [-1] * 64
                 for L in range(64):
