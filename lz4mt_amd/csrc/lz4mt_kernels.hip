@@ -968,11 +968,12 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     uint32_t anchor = 0, op = 0;
     PendSeq pe{};
     bool havePe = false;
-    // window: lane 0 INSERT insPos, lane 1 TEST testPos, lane L >= 2 SEARCH probe k0 + L - 2 at sPos + F(k)
-    // window state: sPos, k0 and the mode (0 continuation: search only;
-    // 1 after a match at sPos - 1: INSERT sPos - 3, TEST sPos - 1; 2 first
-    // window: INSERT 0)
-    uint32_t sPos = 1, k0 = 0, mode = 2;
+    // window: lane 0 INSERT insPos, lane 1 TEST testPos, lane L >= 2 SEARCH
+    // probe k0 + L - 2 (at sBase + F(k) - F(k0), sBase = first search position)
+    // window state: sBase, k0 (+ s0, j1 derived from it) and the mode
+    // (0 continuation: search only; 1 after a match ending at sBase - 1:
+    // INSERT sBase - 3, TEST sBase - 1; 2 first window: INSERT 0)
+    uint32_t sBase = 1, k0 = 0, s0 = 1, j1 = 65, mode = 2;
     // ONE exit and no continue: the structurizer then needs no flow
     // variables and the loop-carried state stays in place across windows
     bool done = false, fail = false;
@@ -983,27 +984,21 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
       bool wTerm;
       do {
         if (ST) acc[10] += 1;
-        // ---- probe positions (uniform lo/hi bound the window's bytes)
-        uint32_t p, step, sLo, sHi;
-        if (k0 == 0) {
-            p = sPos + L - 2;
-            step = 1;
-            sLo = sPos;
-            sHi = sPos + 61;
-        } else {
-            const uint32_t kk = k0 + L - 2, km1 = kk - 1, q = km1 >> 6, r6 = km1 & 63u;
-            p = sPos + 1u + 32u * q * (q + 1u) + r6 * (q + 1u);
-            step = (63u + kk) >> 6;
-            sLo = sPos + probe_off(k0);
-            sHi = sPos + probe_off(k0 + 61);
-        }
+        // ---- probe positions.  SEARCH lane L probes k = k0 + j (j = L - 2) at
+        // sBase + j*s0 + max(0, j - j1): the step s0 = step(k0) rises by one at
+        // most once inside a window (at j = j1; never in the k0 = 0 window)
+        const uint32_t j = L - 2;
+        const int32_t jx = (int32_t)j - (int32_t)j1;
+        uint32_t p = sBase + j * s0 + (uint32_t)max(jx, 0);
+        const uint32_t step = s0 + (jx >= 0 ? 1u : 0u);
+        const uint32_t sHi = sBase + 61 * s0 + (61 > j1 ? 61 - j1 : 0u);
         const bool insOn = mode != 0, testOn = mode == 1;
-        const uint32_t insPos = mode == 2 ? 0u : sPos - 3, testPos = sPos - 1;
+        const uint32_t insPos = mode == 2 ? 0u : sBase - 3, testPos = sBase - 1;
         p = L == 0 ? insPos : (L == 1 ? testPos : p);
         const bool srch = L >= 2;
         const bool live = srch ? p <= mflimitP1 : (L == 0 ? insOn : testOn);
         const bool term = srch && live && p + step > mflimitP1;
-        const uint32_t lo = insOn ? insPos : sLo;
+        const uint32_t lo = insOn ? insPos : sBase;
         const uint32_t hi = (sHi < mflimitP1 ? sHi : mflimitP1) + 8;
         uint64_t v8;
         if (hi - lo <= 1024) {
@@ -1124,7 +1119,10 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         STAMP_ADD(1, ts);
         STAMP_ADD(2, ts);
         if (w == 64) {   // no stop: the search goes on
+            sBase += 62 * s0 + (62 > j1 ? 62 - j1 : 0u);
             k0 += 62;
+            s0 = (63 + k0) >> 6;   // k0 >= 62: no max(1, .) needed
+            j1 = (k0 < 65 ? 65u : ((k0 - 1) & ~63u) + 65) - k0;
             mode = 0;
         }
       } while (w == 64);
@@ -1192,8 +1190,10 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             anchor = ipe;
             done = fail || ipe >= mflimitP1;
             mode = 1;
-            sPos = ipe + 1;
+            sBase = ipe + 1;
             k0 = 0;
+            s0 = 1;
+            j1 = 65;
             STAMP_ADD(4, ts);
         }
     }
