@@ -3,6 +3,7 @@ timing of experiment builds: LZ4MT_AMD_LIB=<variant .so> python tools/ktime.py""
 import ctypes
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
@@ -14,15 +15,23 @@ src = L.gen_synthetic(n)
 sd = L.make_sd(7, False, True)
 L.lib.lz4mtHipSetTiming(1)
 ms = (ctypes.c_float * 4)()
-enc, dec = 1e9, 1e9
+enc, dec, wc, wd, xc, xd = 1e9, 1e9, 1e9, 1e9, 1e9, 1e9
 for _ in range(3):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     fr = L.compress_frame(src, sd)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
     L.lib.lz4mtHipGetTimings(ms)
-    enc = min(enc, ms[0])
+    enc, xc = min(enc, ms[0]), min(xc, ms[1])
     out, r = L.decompress_frame(fr)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    wc, wd = min(wc, t1 - t0), min(wd, t2 - t1)
     L.lib.lz4mtHipGetTimings(ms)
-    dec = min(dec, ms[1])
+    dec, xd = min(dec, ms[1]), min(xd, ms[2])
     assert r == 0
     del fr, out
 assert torch.equal(L.decompress_frame(L.compress_frame(src, sd))[0], src)
-print(f"{os.path.basename(os.environ.get('LZ4MT_AMD_LIB', 'product'))}: encode {enc:.2f} ms  decode {dec:.2f} ms")
+print(f"{os.path.basename(os.environ.get('LZ4MT_AMD_LIB', 'product'))}: encode {enc:.2f} ms  decode {dec:.2f} ms  "
+      f"| block xxh32 {xc:.2f} / {xd:.2f} ms (+verify) | compress call {wc * 1e3:.2f} ms  decompress call {wd * 1e3:.2f} ms")
