@@ -1628,36 +1628,78 @@ struct Dec {
         l_u8* const ringp = ring;
         l_u8* const dummy = win + kInWin;   // 128 scratch bytes: target of masked-off lane writes
         const uint64_t bigM = ballot(tot > 64);
-        for (uint32_t j0 = 0; j0 < nb; j0 += 8) {
-            uint32_t v[8];
-            l_u8* wp[8];
-            const bool big = ((bigM >> j0) & 0xFFull) != 0;
+        // Fast path: each sequence's copy parameters are precomputed by its
+        // lane as LDS byte addresses (literal source, match source, target)
+        // and broadcast to the wave with one ds_read_b128 (the hop table is
+        // dead by now) -- no v_readlane / SALU unpacking per sequence.  It
+        // needs every copied range to stay clear of the ring's end (true for
+        // ~15 batches in 16); otherwise the masked per-sequence path below.
+        const uint32_t jt0 = in ? tot : 0u;
+        const uint32_t r2i = ((uint32_t)src - lit) & (kRing - 1), wi = (uint32_t)oj & (kRing - 1);
+        const bool wrapJ = jt0 && (wi + jt0 > (uint32_t)kRing || r2i + jt0 > (uint32_t)kRing);
+        if (!ballot(wrapJ)) {
+            const uint32_t ringA = (uint32_t)(uintptr_t)ringp, winA = (uint32_t)(uintptr_t)winp;
+            l_u4* const prm = (l_u4*)(win + kNxOff);
+            prm[L] = (v4u){winA + (uint32_t)(lp - (int32_t)wlo), ringA + r2i, ringA + wi, (lit & 255u) | (jt0 << 8)};
+            WAVE_SYNC();
+            const uint32_t dumA = (uint32_t)(uintptr_t)dummy;
+            for (uint32_t j0 = 0; j0 < nb; j0 += 8) {
+                uint32_t v[8], wa[8];
+                const bool big = ((bigM >> j0) & 0xFFull) != 0;
 #pragma unroll
-            for (int g = 0; g < 8; ++g) {
-                const uint32_t j = min(j0 + g, 63u);
-                const uint32_t A = rdlane(pA, (int)j), Bv = rdlane(pB, (int)j);
-                const uint32_t jl = A & 255u, jt = (j0 + g < nb) ? (A >> 8) & 255u : 0u, jlw = A >> 16;
-                const uint32_t jo = (uint32_t)op + (Bv & 0xFFFFu), js = Bv >> 16;
-                l_u8* ra = L < jl ? winp + jlw + L : ringp + ((js + L) & (kRing - 1));
-                v[g] = *ra;
-                wp[g] = L < jt ? ringp + ((jo + L) & (kRing - 1)) : dummy + L;
+                for (int g = 0; g < 8; ++g) {
+                    const v4u q = prm[j0 + g];
+                    const uint32_t jl = q.w & 255u, jt = q.w >> 8;
+                    v[g] = *(l_u8*)(uintptr_t)((L < jl ? q.x : q.y) + L);
+                    wa[g] = (L < jt ? q.z : dumA) + L;
+                }
+#pragma unroll
+                for (int g = 0; g < 8; ++g) *(l_u8*)(uintptr_t)wa[g] = (uint8_t)v[g];
+                if (big) {   // second 64-byte half of sequences longer than 64 bytes
+#pragma unroll
+                    for (int g = 0; g < 8; ++g) {
+                        const v4u q = prm[j0 + g];
+                        const uint32_t jl = q.w & 255u, jt = q.w >> 8, x = L + 64;
+                        v[g] = *(l_u8*)(uintptr_t)((x < jl ? q.x : q.y) + x);
+                        wa[g] = x < jt ? q.z + x : dumA + 64 + L;
+                    }
+#pragma unroll
+                    for (int g = 0; g < 8; ++g) *(l_u8*)(uintptr_t)wa[g] = (uint8_t)v[g];
+                }
             }
-#pragma unroll
-            for (int g = 0; g < 8; ++g) *wp[g] = (uint8_t)v[g];
-            if (big) {   // second 64-byte half of sequences longer than 64 bytes
-#pragma unroll
+        } else {
+            const uint64_t bigM = ballot(tot > 64);
+            for (uint32_t j0 = 0; j0 < nb; j0 += 8) {
+                uint32_t v[8];
+                l_u8* wp[8];
+                const bool big = ((bigM >> j0) & 0xFFull) != 0;
+    #pragma unroll
                 for (int g = 0; g < 8; ++g) {
                     const uint32_t j = min(j0 + g, 63u);
                     const uint32_t A = rdlane(pA, (int)j), Bv = rdlane(pB, (int)j);
                     const uint32_t jl = A & 255u, jt = (j0 + g < nb) ? (A >> 8) & 255u : 0u, jlw = A >> 16;
                     const uint32_t jo = (uint32_t)op + (Bv & 0xFFFFu), js = Bv >> 16;
-                    const uint32_t x = L + 64;
-                    l_u8* ra = x < jl ? winp + jlw + x : ringp + ((js + x) & (kRing - 1));
+                    l_u8* ra = L < jl ? winp + jlw + L : ringp + ((js + L) & (kRing - 1));
                     v[g] = *ra;
-                    wp[g] = x < jt ? ringp + ((jo + x) & (kRing - 1)) : dummy + 64 + L;
+                    wp[g] = L < jt ? ringp + ((jo + L) & (kRing - 1)) : dummy + L;
                 }
-#pragma unroll
+    #pragma unroll
                 for (int g = 0; g < 8; ++g) *wp[g] = (uint8_t)v[g];
+                if (big) {   // second 64-byte half of sequences longer than 64 bytes
+    #pragma unroll
+                    for (int g = 0; g < 8; ++g) {
+                        const uint32_t j = min(j0 + g, 63u);
+                        const uint32_t A = rdlane(pA, (int)j), Bv = rdlane(pB, (int)j);
+                        const uint32_t jl = A & 255u, jt = (j0 + g < nb) ? (A >> 8) & 255u : 0u, jlw = A >> 16;
+                        const uint32_t jo = (uint32_t)op + (Bv & 0xFFFFu), js = Bv >> 16;
+                        const uint32_t x = L + 64;
+                        l_u8* ra = x < jl ? winp + jlw + x : ringp + ((js + x) & (kRing - 1));
+                        v[g] = *ra;
+                        wp[g] = x < jt ? ringp + ((jo + x) & (kRing - 1)) : dummy + 64 + L;
+                    }
+    #pragma unroll
+                    for (int g = 0; g < 8; ++g) *wp[g] = (uint8_t)v[g];
+                }
             }
         }
         STAMP_ADD(1, ts);
