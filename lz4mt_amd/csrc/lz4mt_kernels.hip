@@ -1323,7 +1323,8 @@ constexpr int32_t kFlush = 1024;   // ring -> HBM flush granule (64 lanes x 16 B
 // into the table, so a hop is one dependent ds_read_u16
 constexpr int32_t kNxOff = kInWin + 128;      // inside the win[] allocation
 constexpr uint32_t kNxPast = 1024, kNxDead = 1026;
-constexpr int32_t kWinAlloc = kInWin + 128 + 1040;
+constexpr int32_t kFpOff = kInWin + 128 + 1040;   // far-match table of a batch (8 x 16 B)
+constexpr int32_t kWinAlloc = kFpOff + 128;
 
 template <bool ST>
 struct Dec {
@@ -1598,25 +1599,29 @@ struct Dec {
         const bool longLit = in && lit > 64;
         const bool ord = in && !far && (longLit || src + (int32_t)mlen > op || lit + mlen > 128);
         const uint64_t farM = ballot(far), ordM = ballot(ord);
-        // 5a. far loads (up to 8 sequences, lane per byte), in flight during 5b
+        // 5a. far loads (up to 8 sequences, lane per byte), in flight during 5b.
+        // The far lanes publish (source, ring target, length) in rank order to
+        // a small LDS table that the wave reads back by broadcast.
         uint32_t fv[8], fv2[8];
-        uint64_t farLeft = farM;
+        const uint32_t fr = __builtin_amdgcn_mbcnt_hi((uint32_t)(farM >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)farM, 0u));
+        const uint32_t nf8 = min((uint32_t)__popcll(farM), 8u);
+        l_u4* const fprm = (l_u4*)(win + kFpOff);
         if (farM) {
             if (completed < (int64_t)ringLo) {   // their bytes were stored to dst: make sure the stores landed
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 completed = flushed;
             }
             if (ST) acc[7] += __popcll(farM);
+            if (far && fr < 8) fprm[fr] = (v4u){(uint32_t)src, (uint32_t)om & (kRing - 1), mlen, 0u};
+            WAVE_SYNC();
 #pragma unroll
             for (int g = 0; g < 8; ++g) {
                 fv[g] = 0; fv2[g] = 0;
-                if (farLeft) {
-                    const int j = __ffsll((long long)farLeft) - 1;
-                    const uint32_t js = (uint32_t)rdlane((uint32_t)src, j), jm = rdlane(mlen, j);
-                    fv[g] = L < jm ? (uint32_t)dst[js + L] : 0u;
-                    if (jm > 64) fv2[g] = L + 64 < jm ? (uint32_t)dst[js + 64 + L] : 0u;
+                if ((uint32_t)g < nf8) {
+                    const v4u q = fprm[g];   // bytes past the match repeat its last one (never written)
+                    fv[g] = dst[q.x + min(L, q.z - 1)];
+                    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)q.z) > 64) fv2[g] = dst[q.x + min(L + 64, q.z - 1)];
                 }
-                farLeft &= farLeft ? farLeft - 1 : 0ull;
             }
         }
         STAMP_ADD(15, ts);
@@ -1717,17 +1722,16 @@ struct Dec {
         }
         // 5c. far bytes into the ring at the match outputs
         if (farM) {
-            farLeft = farM;
 #pragma unroll
             for (int g = 0; g < 8; ++g) {
-                if (farLeft) {
-                    const int j = __ffsll((long long)farLeft) - 1;
-                    const uint32_t jo = (uint32_t)rdlane((uint32_t)om, j), jm = rdlane(mlen, j);
-                    *(L < jm ? ringp + ((jo + L) & (kRing - 1)) : dummy + L) = (uint8_t)fv[g];
-                    if (jm > 64) *(L + 64 < jm ? ringp + ((jo + 64 + L) & (kRing - 1)) : dummy + 64 + L) = (uint8_t)fv2[g];
+                if ((uint32_t)g < nf8) {
+                    const v4u q = fprm[g];
+                    *(L < q.z ? ringp + ((q.y + L) & (kRing - 1)) : dummy + L) = (uint8_t)fv[g];
+                    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)q.z) > 64)
+                        *(L + 64 < q.z ? ringp + ((q.y + 64 + L) & (kRing - 1)) : dummy + 64 + L) = (uint8_t)fv2[g];
                 }
-                farLeft &= farLeft ? farLeft - 1 : 0ull;
             }
+            uint64_t farLeft = ballot(far && fr >= 8);
             while (farLeft) {   // more than 8 far matches: one at a time
                 const int j = __ffsll((long long)farLeft) - 1;
                 const uint32_t js = (uint32_t)rdlane((uint32_t)src, j), jm = rdlane(mlen, j);
@@ -1743,21 +1747,27 @@ struct Dec {
         }
         WAVE_SYNC();
         STAMP_ADD(3, ts);
-        // 5d. ordered matches (k mod off when the source overlaps the match)
-        uint64_t ordLeft = ordM;
-        while (ordLeft) {
-            const int j = __ffsll((long long)ordLeft) - 1;
-            ordLeft &= ordLeft - 1;
-            const uint32_t jm = rdlane(mlen, j), joff = rdlane(off, j);
-            const uint32_t jom = (uint32_t)rdlane((uint32_t)om, j);
-            const uint32_t magic = joff < 64 ? (65536u + joff - 1) / joff : 0u;
-            for (uint32_t base = 0; base < jm; base += 64) {
-                const uint32_t k = base + L;
-                if (k < jm) {
+        // 5d. ordered matches (k mod off when the source overlaps the match),
+        // in sequence order; the ordered lanes publish their parameters by
+        // rank into the (now free) copy table, read back by broadcast
+        const uint32_t nOrd = (uint32_t)__popcll(ordM);
+        if (nOrd) {
+            l_u4* const oprm = (l_u4*)(win + kNxOff);
+            const uint32_t orank = __builtin_amdgcn_mbcnt_hi((uint32_t)(ordM >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ordM, 0u));
+            const uint32_t magicL = (off > 0 && off < 64) ? (65536u + off - 1) / off : 0u;
+            if (ord) oprm[orank] = (v4u){(uint32_t)om & (kRing - 1), off, mlen, magicL};
+            WAVE_SYNC();
+            for (uint32_t g = 0; g < nOrd; ++g) {
+                const v4u q = oprm[g];
+                const uint32_t jom = q.x, joff = q.y, jm = q.z, magic = q.w;
+                const uint32_t jmS = (uint32_t)__builtin_amdgcn_readfirstlane((int)jm);
+                for (uint32_t base = 0; base < jmS; base += 64) {
+                    const uint32_t k = base + L;
                     const uint32_t kk = (joff >= 64 || k < joff) ? k : k - ((k * magic) >> 16) * joff;
-                    ring[(jom + k) & (kRing - 1)] = ring[(jom - joff + kk) & (kRing - 1)];
+                    const uint8_t v = ring[(jom - joff + kk) & (kRing - 1)];
+                    *(k < jm ? ringp + ((jom + k) & (kRing - 1)) : dummy + L) = v;
+                    WAVE_SYNC();
                 }
-                WAVE_SYNC();
             }
         }
         STAMP_ADD(2, ts);
