@@ -284,30 +284,46 @@ void compress_host(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
 }
 
 // ---------------------------------------------------------------------------
-// compress: DEVICE batch engine
+// DEVICE engine: batch slots.  Each slot owns pinned host staging, device
+// buffers and its own stream; several slots are in flight at once, so the
+// host's read() of batch i+1, the H2D/kernels/D2H of batches i-k..i and the
+// in-order write() of batch i-k-1 overlap, and the GPU sees several batches'
+// blocks at once (one wavefront per block needs many blocks to fill the
+// chip).  Slots are cached per thread across calls (pinning is expensive),
+// sized by the largest batch seen; they are reused in FIFO order, which is
+// the block order the writes must keep.
 // ---------------------------------------------------------------------------
-struct DeviceBuffers {
+constexpr int kSlots = 6;
+
+struct Slot {
     hipStream_t st = nullptr;
     uint8_t *hIn = nullptr, *hOut = nullptr, *dIn = nullptr, *dOut = nullptr, *dWs = nullptr;
     uint64_t inCap = 0, outCap = 0, wsCap = 0;
-    ~DeviceBuffers() {
+    // per-batch metadata, pinned so it can travel asynchronously
+    uint64_t* hMeta = nullptr;                // [0] = compressed body size
+    BlockRec* hRecs = nullptr;                // decompress: block records
+    int32_t *hDs = nullptr, *hSt = nullptr;   // decompress: decoded sizes, verify status
+    BlockRec* dRecs = nullptr;
+    int32_t *dDs = nullptr, *dSt = nullptr;
+    uint32_t* dDig = nullptr;
+    uint64_t metaCap = 0;                     // blocks the metadata arrays hold
+    // the batch in flight
+    bool busy = false;
+    uint64_t total = 0, nb = 0;
+
+    void release() {
         if (st) hipStreamSynchronize(st);
-        if (hIn) hipHostFree(hIn);
-        if (hOut) hipHostFree(hOut);
-        if (dIn) hipFree(dIn);
-        if (dOut) hipFree(dOut);
-        if (dWs) hipFree(dWs);
+        hipHostFree(hIn); hipHostFree(hOut); hipHostFree(hMeta); hipHostFree(hRecs); hipHostFree(hDs);
+        hipHostFree(hSt);
+        hipFree(dIn); hipFree(dOut); hipFree(dWs); hipFree(dRecs); hipFree(dDs); hipFree(dSt); hipFree(dDig);
         if (st) hipStreamDestroy(st);
+        *this = Slot();
     }
-    bool init(uint64_t in, uint64_t out, uint64_t ws) {
+    // grows the buffers (contents are not kept); 0 sizes leave a buffer alone
+    bool ensure(uint64_t in, uint64_t out, uint64_t ws, uint64_t blocks) {
         if (!st && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
-        return ensure(in, out, ws);
-    }
-    // grows the buffers (contents are not kept)
-    bool ensure(uint64_t in, uint64_t out, uint64_t ws) {
         if (in > inCap) {
-            if (hIn) hipHostFree(hIn);
-            if (dIn) hipFree(dIn);
+            hipHostFree(hIn); hipFree(dIn);
             hIn = nullptr; dIn = nullptr; inCap = 0;
             if (hipHostMalloc(reinterpret_cast<void**>(&hIn), in + 64, 0) != hipSuccess ||
                 hipMalloc(reinterpret_cast<void**>(&dIn), in + 64) != hipSuccess)
@@ -315,8 +331,7 @@ struct DeviceBuffers {
             inCap = in;
         }
         if (out > outCap) {
-            if (hOut) hipHostFree(hOut);
-            if (dOut) hipFree(dOut);
+            hipHostFree(hOut); hipFree(dOut);
             hOut = nullptr; dOut = nullptr; outCap = 0;
             if (hipHostMalloc(reinterpret_cast<void**>(&hOut), out + 64, 0) != hipSuccess ||
                 hipMalloc(reinterpret_cast<void**>(&dOut), out + 64) != hipSuccess)
@@ -324,68 +339,169 @@ struct DeviceBuffers {
             outCap = out;
         }
         if (ws > wsCap) {
-            if (dWs) hipFree(dWs);
+            hipFree(dWs);
             dWs = nullptr; wsCap = 0;
             if (hipMalloc(reinterpret_cast<void**>(&dWs), ws + 64) != hipSuccess) return false;
             wsCap = ws;
+        }
+        if (blocks > metaCap || !hMeta) {
+            hipHostFree(hMeta); hipHostFree(hRecs); hipHostFree(hDs); hipHostFree(hSt);
+            hipFree(dRecs); hipFree(dDs); hipFree(dSt); hipFree(dDig);
+            hMeta = nullptr; hRecs = nullptr; hDs = nullptr; hSt = nullptr;
+            dRecs = nullptr; dDs = nullptr; dSt = nullptr; dDig = nullptr; metaCap = 0;
+            const uint64_t k = std::max<uint64_t>(blocks, 1);
+            if (hipHostMalloc(reinterpret_cast<void**>(&hMeta), 64, 0) != hipSuccess ||
+                hipHostMalloc(reinterpret_cast<void**>(&hRecs), k * sizeof(BlockRec), 0) != hipSuccess ||
+                hipHostMalloc(reinterpret_cast<void**>(&hDs), k * 4, 0) != hipSuccess ||
+                hipHostMalloc(reinterpret_cast<void**>(&hSt), k * 4, 0) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void**>(&dRecs), k * sizeof(BlockRec)) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void**>(&dDs), k * 4) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void**>(&dSt), k * 4) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void**>(&dDig), k * 4) != hipSuccess)
+                return false;
+            metaCap = k;
         }
         return true;
     }
 };
 
-// A batch must hold enough blocks to fill the chip (one wavefront per block,
-// 256 CUs x 8): up to 2048 blocks, at least 256 MiB and at most 8 GiB of
-// input.  Batches start at 64 blocks and double while they come back full,
-// so short streams never pin the full size.
-uint64_t batch_blocks_max(uint32_t bm) {
-    const uint64_t want = 2048ull * bm;
-    const uint64_t bytes = std::min<uint64_t>(std::max<uint64_t>(want, 256ull << 20), 8ull << 30);
-    return std::max<uint64_t>(1, bytes / bm);
+struct SlotCache {
+    Slot slot[kSlots];
+    ~SlotCache() {
+        for (Slot& s : slot) s.release();
+    }
+    // a call that ends early (error) may leave batches in flight: drain them
+    void quiesce() {
+        for (Slot& s : slot) {
+            if (s.st) hipStreamSynchronize(s.st);
+            s.busy = false;
+        }
+    }
+};
+thread_local SlotCache g_slots;
+
+// The slot pipeline: the calling thread fills and launches batches (all
+// read() calls stay on it, as the reference requires); one writer thread
+// completes them in FIFO order (D2H, in-order write(); the reference also
+// writes from a worker thread).  fill(S) returns false when there is no
+// more input (S not launched) and sets *stop to end after a launched batch;
+// finish(S) returns false to stop the frame (later batches are drained
+// without writes).
+template <class Fill, class Finish>
+void run_slot_pipeline(Session& s, Fill fill, Finish finish) {
+    SlotCache& C = g_slots;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<int> q;
+    bool done = false, failed = false;
+    std::thread writer([&] {
+        for (;;) {
+            int i;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return !q.empty() || done; });
+                if (q.empty()) return;
+                i = q.front();
+                q.pop_front();
+            }
+            Slot& S = C.slot[i];
+            bool okS;
+            {
+                bool f;
+                { std::lock_guard<std::mutex> g(mu); f = failed; }
+                if (f) { hipStreamSynchronize(S.st); okS = false; }
+                else okS = finish(S);
+            }
+            {
+                std::lock_guard<std::mutex> g(mu);
+                if (!okS) failed = true;
+                S.busy = false;
+            }
+            cv.notify_all();
+        }
+    });
+    int head = 0;
+    for (;;) {
+        Slot& S = C.slot[head];
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return !S.busy || failed; });
+            if (failed) break;
+        }
+        if (s.error()) break;
+        bool stop = false;
+        if (!fill(S, &stop)) break;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            S.busy = true;
+            q.push_back(head);
+        }
+        cv.notify_all();
+        head = (head + 1) % kSlots;
+        if (stop) break;
+    }
+    {
+        std::lock_guard<std::mutex> g(mu);
+        done = true;
+    }
+    cv.notify_all();
+    writer.join();
+    C.quiesce();
 }
+
+// Blocks per batch: ~512 MiB of input (at least one block); kSlots batches
+// in flight keep up to 3 GiB of blocks on the GPU at once.
+uint64_t batch_blocks(uint32_t bm) { return std::max<uint64_t>(1, (512ull << 20) / bm); }
 
 void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
     if (s.level() >= 3) { s.quit(LZ4MT_RESULT_BAD_ARG); return; }   // no GPU LZ4-HC
     if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return; }
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
-    const uint64_t Kmax = batch_blocks_max(bm);
-    uint64_t K = std::min<uint64_t>(64, Kmax);
-    DeviceBuffers B;
-    bool eof = false;
-    while (!eof && !s.error()) {
-        const uint64_t inCap = K * bm;
-        if (!B.init(inCap, inCap + K * 8 + 64, compress_ws_bytes(inCap, bm))) { s.quit(LZ4MT_RESULT_ERROR); return; }
+    const uint64_t K = batch_blocks(bm), inCap = K * bm;
+    auto fill = [&](Slot& S, bool* stop) -> bool {
+        if (!S.ensure(inCap, inCap + K * 8 + 64, compress_ws_bytes(inCap, bm), 0)) {
+            s.quit(LZ4MT_RESULT_ERROR);
+            return false;
+        }
         uint64_t total = 0;
         for (uint64_t j = 0; j < K; ++j) {   // one read() per block, as the reference does
-            const int n = s.read(B.hIn + total, (int)bm);
-            if (n <= 0) { eof = true; break; }
+            const int n = s.read(S.hIn + total, (int)bm);
+            if (n <= 0) { *stop = true; break; }
             total += (uint64_t)n;
-            if ((uint32_t)n < bm) break;     // short block ends the batch (block boundaries kept)
+            if ((uint32_t)n < bm) { *stop = true; break; }   // a short block is the last one
         }
-        if (total == 0) break;
+        if (total == 0) return false;
         uint64_t* dRecOff = nullptr;
-        if (hipMemcpyAsync(B.dIn, B.hIn, total, hipMemcpyHostToDevice, B.st) != hipSuccess ||
-            device_compress_body(B.dIn, total, bm, bck, B.dWs, B.dOut, 0, B.st, &dRecOff) != LZ4MT_RESULT_OK) {
-            s.quit(LZ4MT_RESULT_ERROR);
-            return;
-        }
         const uint64_t nb = (total + bm - 1) / bm;
-        uint64_t bodySize = 0;
-        hipMemcpyAsync(&bodySize, dRecOff + nb, 8, hipMemcpyDeviceToHost, B.st);
-        if (sck) xs.update(B.hIn, total);   // serial content checksum overlaps the kernels
-        if (hipStreamSynchronize(B.st) != hipSuccess) { s.quit(LZ4MT_RESULT_ERROR); return; }
-        if (hipMemcpyAsync(B.hOut, B.dOut, bodySize, hipMemcpyDeviceToHost, B.st) != hipSuccess ||
-            hipStreamSynchronize(B.st) != hipSuccess) {
+        if (hipMemcpyAsync(S.dIn, S.hIn, total, hipMemcpyHostToDevice, S.st) != hipSuccess ||
+            device_compress_body(S.dIn, total, bm, bck, S.dWs, S.dOut, 0, S.st, &dRecOff) != LZ4MT_RESULT_OK ||
+            hipMemcpyAsync(S.hMeta, dRecOff + nb, 8, hipMemcpyDeviceToHost, S.st) != hipSuccess) {
             s.quit(LZ4MT_RESULT_ERROR);
-            return;
+            return false;
+        }
+        S.total = total;
+        S.nb = nb;
+        if (sck) xs.update(S.hIn, total);   // serial content checksum overlaps the kernels
+        return true;
+    };
+    // the body size, D2H of the body, in-order write
+    auto finish = [&](Slot& S) -> bool {
+        if (hipStreamSynchronize(S.st) != hipSuccess) { s.quit(LZ4MT_RESULT_ERROR); return false; }
+        const uint64_t bodySize = S.hMeta[0];
+        if (hipMemcpyAsync(S.hOut, S.dOut, bodySize, hipMemcpyDeviceToHost, S.st) != hipSuccess ||
+            hipStreamSynchronize(S.st) != hipSuccess) {
+            s.quit(LZ4MT_RESULT_ERROR);
+            return false;
         }
         for (uint64_t o = 0; o < bodySize;) {   // write() takes int sizes
             const int chunk = (int)std::min<uint64_t>(bodySize - o, 1u << 30);
-            if (!s.write(B.hOut + o, chunk)) return;
+            if (!s.write(S.hOut + o, chunk)) return false;
             o += (uint64_t)chunk;
         }
-        if (total == K * bm) K = std::min(2 * K, Kmax);   // full batch: more input likely
-    }
+        return true;
+    };
+    run_slot_pipeline(s, fill, finish);
 }
 
 // ---------------------------------------------------------------------------
@@ -437,32 +553,18 @@ bool decompress_host(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
 }
 
 // ---------------------------------------------------------------------------
-// decompress: DEVICE batch engine
+// decompress: DEVICE batch engine (the same slot pipeline as compress)
 // ---------------------------------------------------------------------------
 bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
     if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return false; }
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
-    const uint64_t Kmax = batch_blocks_max(bm);
-    uint64_t K = std::min<uint64_t>(64, Kmax);
-    DeviceBuffers B;
-    BlockRec* dRecs = nullptr;
-    int32_t *dDs = nullptr, *dSt = nullptr;
-    uint32_t* dDig = nullptr;
-    if (hipMalloc(reinterpret_cast<void**>(&dRecs), Kmax * sizeof(BlockRec)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&dDs), Kmax * 4) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&dSt), Kmax * 4) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&dDig), Kmax * 4) != hipSuccess) {
-        s.quit(LZ4MT_RESULT_ERROR);
-        hipFree(dRecs); hipFree(dDs); hipFree(dSt); hipFree(dDig);
-        return false;
-    }
-    std::vector<BlockRec> recs(Kmax);
-    std::vector<int32_t> ds(Kmax), stv(Kmax);
+    const uint64_t K = batch_blocks(bm);
     bool eos = false;
-    Lz4MtResult pending = LZ4MT_RESULT_OK;   // a read error found while filling the batch
-    while (!eos && pending == LZ4MT_RESULT_OK && !s.error() && !s.readEof()) {
-        if (!B.init(K * bm, K * bm, 0)) { s.quit(LZ4MT_RESULT_ERROR); break; }
+    Lz4MtResult pending = LZ4MT_RESULT_OK;   // a read error found while filling a batch
+    auto fill = [&](Slot& S, bool* stop) -> bool {
+        if (eos || pending != LZ4MT_RESULT_OK || s.readEof()) return false;
+        if (!S.ensure(K * bm + 16 * K, K * bm, 0, K)) { s.quit(LZ4MT_RESULT_ERROR); return false; }
         uint64_t used = 0, nb = 0;
         while (nb < K) {
             uint32_t bits = 0;
@@ -471,51 +573,52 @@ bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
             if (bits == 0) { eos = true; break; }
             const uint32_t n = bits & ~kRawBit;
             if (n > bm) { pending = LZ4MT_RESULT_INVALID_BLOCK_SIZE; break; }
-            if (s.read(B.hIn + used, (int)n) != (int)n) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_DATA; break; }
+            if (s.read(S.hIn + used, (int)n) != (int)n) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_DATA; break; }
             uint32_t ck = 0;
             if (bck && !s.readU32(&ck)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_CHECKSUM; break; }
-            recs[nb++] = BlockRec{used, bits, ck};
+            S.hRecs[nb++] = BlockRec{used, bits, ck};
             used = (used + n + 15) & ~15ull;
         }
-        if (nb) {
-            if (hipMemcpyAsync(B.dIn, B.hIn, used, hipMemcpyHostToDevice, B.st) != hipSuccess ||
-                hipMemcpyAsync(dRecs, recs.data(), nb * sizeof(BlockRec), hipMemcpyHostToDevice, B.st) != hipSuccess ||
-                launch_decode(B.dIn, dRecs, (uint32_t)nb, bm, B.dOut, nb * bm, dDs, B.st) != hipSuccess ||
-                (bck && launch_xxh32_frame_blocks(B.dIn, dRecs, (uint32_t)nb, dDig, B.st) != hipSuccess) ||
-                launch_block_verify(dRecs, (uint32_t)nb, dDig, dDs, bm, bck, dSt, B.st) != hipSuccess ||
-                hipMemcpyAsync(ds.data(), dDs, nb * 4, hipMemcpyDeviceToHost, B.st) != hipSuccess ||
-                hipMemcpyAsync(stv.data(), dSt, nb * 4, hipMemcpyDeviceToHost, B.st) != hipSuccess ||
-                hipMemcpyAsync(B.hOut, B.dOut, nb * bm, hipMemcpyDeviceToHost, B.st) != hipSuccess ||
-                hipStreamSynchronize(B.st) != hipSuccess) {
-                s.quit(LZ4MT_RESULT_ERROR);
-                break;
-            }
-            // write in block order; the first failing block stops the frame
-            bool stop = false;
-            for (uint64_t i = 0; i < nb && !stop; ++i) {
-                const bool raw = (recs[i].bits & kRawBit) != 0;
-                if (stv[i] == 18 || stv[i] == 1) {
-                    // reference precedence: decode failure before writing
-                    s.quit(stv[i] == 18 ? LZ4MT_RESULT_DECOMPRESS_FAIL : LZ4MT_RESULT_ERROR);
-                    stop = true;
-                    break;
-                }
-                const uint8_t* p = B.hOut + i * bm;
-                const int n = ds[i];
-                if (sck) xs.update(p, (size_t)n);
-                if (!s.write(p, n)) {
-                    s.quit(raw ? LZ4MT_RESULT_CANNOT_WRITE_DATA_BLOCK : LZ4MT_RESULT_CANNOT_WRITE_DECODED_BLOCK);
-                    stop = true;
-                    break;
-                }
-                if (stv[i] == 16) { s.quit(LZ4MT_RESULT_BLOCK_CHECKSUM_MISMATCH); stop = true; }
-            }
-            if (stop) break;
+        *stop = eos || pending != LZ4MT_RESULT_OK;
+        if (nb == 0) return false;
+        if (hipMemcpyAsync(S.dIn, S.hIn, used, hipMemcpyHostToDevice, S.st) != hipSuccess ||
+            hipMemcpyAsync(S.dRecs, S.hRecs, nb * sizeof(BlockRec), hipMemcpyHostToDevice, S.st) != hipSuccess ||
+            launch_decode(S.dIn, S.dRecs, (uint32_t)nb, bm, S.dOut, nb * bm, S.dDs, S.st) != hipSuccess ||
+            (bck && launch_xxh32_frame_blocks(S.dIn, S.dRecs, (uint32_t)nb, S.dDig, S.st) != hipSuccess) ||
+            launch_block_verify(S.dRecs, (uint32_t)nb, S.dDig, S.dDs, bm, bck, S.dSt, S.st) != hipSuccess ||
+            hipMemcpyAsync(S.hDs, S.dDs, nb * 4, hipMemcpyDeviceToHost, S.st) != hipSuccess ||
+            hipMemcpyAsync(S.hSt, S.dSt, nb * 4, hipMemcpyDeviceToHost, S.st) != hipSuccess ||
+            hipMemcpyAsync(S.hOut, S.dOut, nb * bm, hipMemcpyDeviceToHost, S.st) != hipSuccess) {
+            s.quit(LZ4MT_RESULT_ERROR);
+            return false;
         }
-        if (pending != LZ4MT_RESULT_OK) { s.quit(pending); break; }
-        if (nb == K) K = std::min(2 * K, Kmax);   // full batch: more input likely
-    }
-    hipFree(dRecs); hipFree(dDs); hipFree(dSt); hipFree(dDig);
+        S.nb = nb;
+        return true;
+    };
+    // statuses, then the blocks in order; the first failing block stops the
+    // frame (reference precedence: a decode failure before writing)
+    auto finish = [&](Slot& S) -> bool {
+        if (hipStreamSynchronize(S.st) != hipSuccess) { s.quit(LZ4MT_RESULT_ERROR); return false; }
+        for (uint64_t i = 0; i < S.nb; ++i) {
+            const bool raw = (S.hRecs[i].bits & kRawBit) != 0;
+            const int32_t st = S.hSt[i];
+            if (st == 18 || st == 1) {
+                s.quit(st == 18 ? LZ4MT_RESULT_DECOMPRESS_FAIL : LZ4MT_RESULT_ERROR);
+                return false;
+            }
+            const uint8_t* p = S.hOut + i * bm;
+            const int n = S.hDs[i];
+            if (sck) xs.update(p, (size_t)n);
+            if (!s.write(p, n)) {
+                s.quit(raw ? LZ4MT_RESULT_CANNOT_WRITE_DATA_BLOCK : LZ4MT_RESULT_CANNOT_WRITE_DECODED_BLOCK);
+                return false;
+            }
+            if (st == 16) { s.quit(LZ4MT_RESULT_BLOCK_CHECKSUM_MISMATCH); return false; }
+        }
+        return true;
+    };
+    run_slot_pipeline(s, fill, finish);
+    if (pending != LZ4MT_RESULT_OK) s.quit(pending);   // refines a read ERROR; a block's own failure wins
     return eos;
 }
 
