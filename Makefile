@@ -6,13 +6,22 @@ HIPFLAGS ?= --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 BUILD  := build
 CSRC   := lz4mt_amd/csrc
 LIB    := lz4mt_amd/liblz4mt_amd.so
-OBJS   := $(BUILD)/lz4mt_kernels.o $(BUILD)/lz4mt_engine.o $(BUILD)/lz4mt_frame.o $(BUILD)/lz4mt_io.o
+OBJS   := $(BUILD)/lz4mt_kernels_enc.o $(BUILD)/lz4mt_kernels_dec.o $(BUILD)/lz4mt_engine.o $(BUILD)/lz4mt_frame.o $(BUILD)/lz4mt_io.o
 HDRS   := $(CSRC)/lz4mt_device.h $(CSRC)/lz4mt_host.h include/lz4mt.h include/lz4mt_hip.h include/lz4mt_io.h
 
 all: $(LIB) oracle
 
 $(BUILD):
 	mkdir -p $(BUILD)
+
+# One source, two objects: the decoder's dependent-load chains schedule
+# better under max-ilp (decode kernel 31.8 -> 30.1 ms at 8 GiB); the
+# encoder keeps the default scheduler.
+$(BUILD)/lz4mt_kernels_enc.o: $(CSRC)/lz4mt_kernels.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DLZ4MT_PART=1 -c -o $@ $<
+
+$(BUILD)/lz4mt_kernels_dec.o: $(CSRC)/lz4mt_kernels.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DLZ4MT_PART=2 -mllvm --amdgpu-sched-strategy=max-ilp -c -o $@ $<
 
 $(BUILD)/%.o: $(CSRC)/%.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<

@@ -21,6 +21,13 @@
 // (16 KiB) and the decoder's history ring (16 KiB) sit in LDS.
 #include "lz4mt_device.h"
 
+// LZ4MT_PART splits this file into two objects so each half gets its own
+// scheduler flags (Makefile): 1 = everything but the decoder kernels,
+// 2 = the decoder kernels only, 0 (default) = all.
+#ifndef LZ4MT_PART
+#define LZ4MT_PART 0
+#endif
+
 namespace lz4mt {
 
 // ---------------------------------------------------------------------------
@@ -85,7 +92,7 @@ __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) 
         }                                         \
     } while (0)
 
-constexpr uint32_t kP1 = 2654435761u, kP2 = 2246822519u, kP3 = 3266489917u, kP4 = 668265263u, kP5 = 374761393u;
+[[maybe_unused]] constexpr uint32_t kP1 = 2654435761u, kP2 = 2246822519u, kP3 = 3266489917u, kP4 = 668265263u, kP5 = 374761393u;
 
 // ---------------------------------------------------------------------------
 // Encoder
@@ -1227,6 +1234,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
 static_assert(kSR + kSRMirror <= 3072, "ring exceeds the shared scratch");
 static_assert(kDedup == 1024, "scratch layout");
 
+#if LZ4MT_PART != 2
 __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, uint64_t srcSize, uint32_t blockSize,
                                                uint8_t* __restrict__ slots, uint64_t slotStride,
                                                uint32_t capOverride, int32_t* __restrict__ csize) {
@@ -1291,6 +1299,8 @@ hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSiz
                        capOverride, csize);
     return hipGetLastError();
 }
+#endif
+
 
 // ---------------------------------------------------------------------------
 // Wave-wide inclusive prefix sum and max (DPP row shifts + 3 cross-row adds)
@@ -1324,7 +1334,7 @@ constexpr int32_t kFlush = 1024;   // ring -> HBM flush granule (64 lanes x 16 B
 constexpr int32_t kNxOff = kInWin + 128;      // inside the win[] allocation
 constexpr uint32_t kNxPast = 1024, kNxDead = 1026;
 constexpr int32_t kFpOff = kInWin + 128 + 1040;   // far-match table of a batch (8 x 16 B)
-constexpr int32_t kWinAlloc = kFpOff + 128;
+[[maybe_unused]] constexpr int32_t kWinAlloc = kFpOff + 128;
 
 template <bool ST>
 struct Dec {
@@ -1941,6 +1951,7 @@ __device__ void copy_raw(g_cu8* src, g_u8* dst, int64_t n) {
     for (int64_t i = nd * 4 + L; i < n; i += 64) dst[i] = src[i];
 }
 
+#if LZ4MT_PART != 1
 __global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ frame, const BlockRec* __restrict__ recs,
                                                uint32_t blockMax, uint8_t* __restrict__ out, uint64_t outCap,
                                                int32_t* __restrict__ dsize) {
@@ -2014,21 +2025,30 @@ hipError_t launch_decode_stats(const uint8_t* frame, const BlockRec* recs, uint3
                        stats);
     return hipGetLastError();
 }
+#endif
 
+
+#if LZ4MT_PART != 2
 hipError_t launch_encode_stats(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                                uint8_t* slots, int32_t* csize, uint64_t* stats, hipStream_t st) {
     hipLaunchKernelGGL(k_encode_stats, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots,
                        (uint64_t)blockSize, csize, stats);
     return hipGetLastError();
 }
+#endif
 
+
+#if LZ4MT_PART != 1
 hipError_t launch_decode(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax, uint8_t* out,
                          uint64_t outCap, int32_t* dsize, hipStream_t st) {
     if (nBlocks == 0) return hipSuccess;
     hipLaunchKernelGGL(k_decode, dim3(nBlocks), dim3(64), 0, st, frame, recs, blockMax, out, outCap, dsize);
     return hipGetLastError();
 }
+#endif
 
+
+#if LZ4MT_PART != 2
 // ---------------------------------------------------------------------------
 // XXH32: 4 lanes per block (one per accumulator), 16 blocks per wavefront
 // ---------------------------------------------------------------------------
@@ -2370,5 +2390,7 @@ hipError_t launch_gen_synthetic(uint8_t* dst, uint64_t n, uint64_t seed, hipStre
     hipLaunchKernelGGL(k_gen_synthetic, dim3((uint32_t)segs), dim3(64), 0, st, dst, n, seed);
     return hipGetLastError();
 }
+
+#endif  // LZ4MT_PART != 2
 
 }  // namespace lz4mt
