@@ -32,6 +32,18 @@ struct WalkInfo {
     int32_t  result;     // Lz4MtResult code (0 = OK)
 };
 
+// Scratch of the parallel frame walk (launch_frame_walk_count/_path): the
+// frame is scanned in 64 KiB chunks for candidate record offsets.
+constexpr int kWalkChunkLog = 16;
+struct WalkScratch {
+    uint32_t* count;     // nChunks: candidates per chunk
+    uint64_t* base;      // nChunks + 1: exclusive scan of count, M at [nChunks]
+    uint64_t* pos;       // M: node -> frame offset (ascending)
+    uint32_t* Ja;        // M + 1: successor tables (node M = DEAD)
+    uint32_t* Jb;
+    uint32_t* P;         // maxBlocks + 1 (path)
+};
+
 // ---- kernel launchers (lz4mt_kernels.hip) ----
 hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                          uint8_t* slots, uint64_t slotStride, uint32_t capOverride, int32_t* csize,
@@ -57,6 +69,12 @@ hipError_t launch_frame_finalize(uint8_t* frame, const uint8_t* hdr, uint32_t hd
 hipError_t launch_frame_walk(const uint8_t* frame, uint64_t frameSize, uint64_t bodyPos, uint32_t blockMax,
                              int blockChecksum, uint32_t maxBlocks, BlockRec* recs, WalkInfo* info,
                              hipStream_t st);
+uint64_t frame_walk_par_chunks(uint64_t frameSize);
+hipError_t launch_frame_walk_count(const uint8_t* frame, uint64_t frameSize, uint64_t bodyPos, uint32_t blockMax,
+                                   int blockChecksum, const WalkScratch& ws, hipStream_t st);
+hipError_t launch_frame_walk_path(const uint8_t* frame, uint64_t frameSize, uint64_t bodyPos, uint32_t blockMax,
+                                  int blockChecksum, uint32_t maxBlocks, uint32_t M, const WalkScratch& ws,
+                                  BlockRec* recs, WalkInfo* info, hipStream_t st);
 hipError_t launch_block_verify(const BlockRec* recs, uint32_t nBlocks, const uint32_t* digest, const int32_t* dsize,
                                uint32_t blockMax, int blockChecksum, int32_t* status, hipStream_t st);
 hipError_t launch_encode_stats(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,

@@ -12,6 +12,8 @@
 //   lz4mtDecompress (src/lz4mt.cpp:593-734, 938-1011).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
 #include <algorithm>
 #include <mutex>
 #include <vector>
@@ -285,9 +287,39 @@ struct DecodeBuffers {
     uint32_t* ssum = nullptr;
     uint64_t cap = 0;
     ~DecodeBuffers() { release(); }
+    WalkScratch ws{};
+    uint64_t wsChunks = 0, wsCap = 0, wsNodes = 0;
     void release() {
         hipFree(recs); hipFree(digest); hipFree(dsize); hipFree(status); hipFree(info); hipFree(ssum);
         recs = nullptr; digest = nullptr; dsize = nullptr; status = nullptr; info = nullptr; ssum = nullptr; cap = 0;
+        release_walk();
+    }
+    void release_walk() {
+        hipFree(ws.count); hipFree(ws.base); hipFree(ws.P);
+        release_nodes();
+        ws = WalkScratch{};
+        wsChunks = 0; wsCap = 0;
+    }
+    void release_nodes() {
+        hipFree(ws.pos); hipFree(ws.Ja); hipFree(ws.Jb);
+        ws.pos = nullptr; ws.Ja = nullptr; ws.Jb = nullptr;
+        wsNodes = 0;
+    }
+    bool ensure_walk(uint64_t chunks, uint64_t nb) {
+        if (ws.P && chunks <= wsChunks && nb <= wsCap) return true;
+        release_walk();
+        wsChunks = chunks; wsCap = nb;
+        return hipMalloc(reinterpret_cast<void**>(&ws.count), chunks * 4) == hipSuccess &&
+               hipMalloc(reinterpret_cast<void**>(&ws.base), (chunks + 1) * 8) == hipSuccess &&
+               hipMalloc(reinterpret_cast<void**>(&ws.P), (nb + 1) * 4) == hipSuccess;
+    }
+    bool ensure_nodes(uint64_t m) {
+        if (ws.pos && m <= wsNodes) return true;
+        release_nodes();
+        wsNodes = std::max<uint64_t>(m, 1024);
+        return hipMalloc(reinterpret_cast<void**>(&ws.pos), wsNodes * 8) == hipSuccess &&
+               hipMalloc(reinterpret_cast<void**>(&ws.Ja), (wsNodes + 1) * 4) == hipSuccess &&
+               hipMalloc(reinterpret_cast<void**>(&ws.Jb), (wsNodes + 1) * 4) == hipSuccess;
     }
     bool ensure(uint64_t nb) {
         if (info && nb <= cap) return true;
@@ -306,11 +338,38 @@ struct DecodeBuffers {
 Lz4MtResult walk_frame(const uint8_t* frame, uint64_t frameSize, uint64_t bodyPos, uint32_t bm, int bck,
                        DecodeBuffers& B, WalkInfo& wi, hipStream_t st) {
     uint64_t guess = std::min<uint64_t>((frameSize - bodyPos) / 4 + 1, (frameSize - bodyPos) / 1024 + 4096);
+    // The serial walk pays one dependent load per block; the parallel one a
+    // pass over the body.  Parallel wins once blocks are small (<= 1 MiB)
+    // and many.
+    // LZ4MT_AMD_WALK=serial|parallel forces one (tests run both on small frames).
+    const char* fe = getenv("LZ4MT_AMD_WALK");
+    const int force = !fe ? 0 : (strcmp(fe, "serial") == 0 ? 1 : (strcmp(fe, "parallel") == 0 ? 2 : 0));
+    const bool autoPar = bm <= (1u << 20) && frameSize - bodyPos >= (64ull << 20);
+    const bool par = frameSize < (1ull << 40) && (force == 2 || (force == 0 && autoPar));
     for (int attempt = 0; attempt < 2; ++attempt) {
         if (!B.ensure(guess)) return LZ4MT_RESULT_ERROR;
-        HIPCHK(launch_frame_walk(frame, frameSize, bodyPos, bm, bck, (uint32_t)B.cap, B.recs, B.info, st));
-        HIPCHK(hipMemcpyAsync(&wi, B.info, sizeof(wi), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
+        wi.result = -1;
+        if (par) {
+            const uint64_t nc = frame_walk_par_chunks(frameSize);
+            if (!B.ensure_walk(nc, B.cap)) return LZ4MT_RESULT_ERROR;
+            HIPCHK(launch_frame_walk_count(frame, frameSize, bodyPos, bm, bck, B.ws, st));
+            uint64_t M = 0;
+            HIPCHK(hipMemcpyAsync(&M, B.ws.base + nc, 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            // more candidates than 1 per 8 bytes: not worth it (and node ids are u32)
+            if (M > 0 && M <= (frameSize - bodyPos) / 8 + 1024 && M < (1ull << 31)) {
+                if (!B.ensure_nodes(M)) return LZ4MT_RESULT_ERROR;
+                HIPCHK(launch_frame_walk_path(frame, frameSize, bodyPos, bm, bck, (uint32_t)B.cap, (uint32_t)M, B.ws,
+                                              B.recs, B.info, st));
+                HIPCHK(hipMemcpyAsync(&wi, B.info, sizeof(wi), hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+            }
+        }
+        if (wi.result == -1) {   // serial walk (also: malformed frames, for the exact error code)
+            HIPCHK(launch_frame_walk(frame, frameSize, bodyPos, bm, bck, (uint32_t)B.cap, B.recs, B.info, st));
+            HIPCHK(hipMemcpyAsync(&wi, B.info, sizeof(wi), hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+        }
         if (!(wi.result == 1 && wi.nBlocks == B.cap)) return LZ4MT_RESULT_OK;
         guess = (frameSize - bodyPos) / 4 + 1;
     }

@@ -8,6 +8,7 @@ properties (XXH32 of input == XXH32 of output, per-block checksums verified
 by the decoder, block sample vs the oracle).
 """
 import ctypes
+import os
 import random
 
 import pytest
@@ -253,3 +254,41 @@ def test_callback_api_on_gpu(golden_inputs, mode):
         assert frame == oracle.compress_frame(data, oracle.params(bid, sck, bck)), (mode, bid)
         r, out, _ = L.decompress(frame, len(data) + 64, mode=m)
         assert r == 0 and out == data, (mode, bid, L.result_to_string(r))
+
+
+# ---------------------------------------------------------------------------
+# the parallel frame walk (candidate offsets + pointer doubling) must give the
+# serial walk's records and error codes on every frame, well-formed or not
+# ---------------------------------------------------------------------------
+def _decode_both(b, cap):
+    res = []
+    for mode in ("serial", "parallel"):
+        os.environ["LZ4MT_AMD_WALK"] = mode
+        try:
+            out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+            o, r = L.decompress_frame(dev(b), out=out, check=False)
+            res.append((r, host(o) if r == 0 else None))
+        finally:
+            del os.environ["LZ4MT_AMD_WALK"]
+    return res
+
+
+@pytest.mark.parametrize("bid,sck,bck", [(4, True, True), (4, False, False), (5, False, True)])
+def test_frame_walk_parallel_matches_serial(golden_inputs, bid, sck, bck):
+    data = (golden_inputs["syn300k"] + golden_inputs["zeros300k"] + golden_inputs["random100k"]) * 3
+    f = host(L.compress_frame(dev(data), L.make_sd(bid, sck, bck)))
+    cap = len(data) + (1 << 20)
+    (rs, os_), (rp, op_) = _decode_both(f, cap)
+    assert rs == rp == 0 and os_ == op_ == data
+    rng = random.Random(bid * 7 + sck * 3 + bck)
+    bodies = [7 + rng.randrange(len(f) - 7) for _ in range(12)]
+    cases = [f[:k] for k in bodies]                                   # truncations
+    for k in bodies:                                                  # flipped bytes (size words, payload)
+        bad = bytearray(f); bad[k] ^= 1 << rng.randrange(8); cases.append(bytes(bad))
+    bad = bytearray(f); bad[7:11] = (0).to_bytes(4, "little"); cases.append(bytes(bad))          # early EOS
+    bad = bytearray(f); bad[7:11] = ((1 << 24) | 5).to_bytes(4, "little"); cases.append(bytes(bad))  # > blockMax
+    skip = (0x184D2A50).to_bytes(4, "little") + (3).to_bytes(4, "little") + b"abc"
+    cases += [f + skip + f, f + f[:-3], f + b"xy"]
+    for b in cases:
+        (rs, os_), (rp, op_) = _decode_both(b, 2 * cap)
+        assert rs == rp and os_ == op_, (len(b), rs, rp)
