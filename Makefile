@@ -2,7 +2,7 @@
 # No cmake: plain hipcc / gcc.  `python -c "import __graft_entry__ as g; g.build()"` runs this.
 HIPCC  ?= /opt/rocm/bin/hipcc
 ARCH   ?= gfx950
-HIPFLAGS ?= --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value
+HIPFLAGS ?= $(EXTRA) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value
 BUILD  := build
 CSRC   := lz4mt_amd/csrc
 LIB    := lz4mt_amd/liblz4mt_amd.so

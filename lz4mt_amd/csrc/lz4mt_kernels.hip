@@ -900,7 +900,41 @@ __device__ int32_t encode_block_t(g_cu8* __restrict__ s, uint32_t n, g_u8* __res
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t bal(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ uint32_t sff1(uint64_t m) { return m ? (uint32_t)__builtin_ctzll(m) : 64u; }
-constexpr uint32_t kDummy = 4096;   // T[4096 + L]: lane L's dummy slot (inside the 1 KiB scratch)
+// Table geometry per table type: lz4 1.9.3 uses byU32 (4096 entries,
+// hash5) from 65 547 bytes up and byU16 (8192 entries, hash4) below.  An
+// entry is position | tag << PB; the tag is 32 - PB more bits of the
+// sequence's own hash.  T[kTE + L] is lane L's dummy slot.
+// SPLIT (byU16 only): positions in a u16 array and 8-bit tags in a u8
+// array (26 KiB of LDS in all: 6 waves per CU instead of 4); the marker
+// readback compares positions only (distinct per live lane).
+template <bool U16, bool SPLIT = false> struct V5Geo {
+    static constexpr uint32_t kTE = U16 ? 8192u : 4096u;
+    static constexpr uint32_t PB = U16 ? 16u : kPosBits;
+    static constexpr uint32_t PM = (1u << PB) - 1u;
+    static constexpr uint32_t TB = SPLIT ? 8u : 32u - PB;   // tag bits
+    static __device__ __forceinline__ uint32_t tag(uint32_t w0) { return (w0 * 0x85EBCA77u) >> (32 - TB); }
+    l_u32* T;
+    __device__ __forceinline__ l_u16* T16() const { return (l_u16*)T; }
+    __device__ __forceinline__ l_u8* TG() const { return (l_u8*)T + 2 * (kTE + 64); }
+    __device__ __forceinline__ uint32_t ld(uint32_t i) const {
+        return SPLIT ? ((uint32_t)T16()[i] | ((uint32_t)TG()[i] << 16)) : T[i];
+    }
+    __device__ __forceinline__ void st(uint32_t i, uint32_t e) const {
+        if (SPLIT) { T16()[i] = (uint16_t)e; TG()[i] = (uint8_t)(e >> 16); } else T[i] = e;
+    }
+    __device__ __forceinline__ uint32_t rb(uint32_t i) const { return SPLIT ? (uint32_t)T16()[i] : T[i]; }
+    static constexpr uint32_t kRbMask = SPLIT ? 0xFFFFu : 0xFFFFFFFFu;
+    __device__ __forceinline__ void init(uint32_t e0) const {
+        const uint32_t L = laneid();
+        if (SPLIT) {
+            const uint32_t p2 = (e0 & 0xFFFFu) * 0x10001u, t4 = (e0 >> 16) * 0x01010101u;
+            for (uint32_t i = L; i < kTE / 8; i += 64) ((l_u4*)T16())[i] = (v4u){p2, p2, p2, p2};
+            for (uint32_t i = L; i < kTE / 16; i += 64) ((l_u4*)TG())[i] = (v4u){t4, t4, t4, t4};
+        } else {
+            for (uint32_t i = L; i < kTE / 4; i += 64) ((l_u4*)T)[i] = (v4u){e0, e0, e0, e0};
+        }
+    }
+};
 
 // one encoded sequence whose bytes are stored during the next round trip
 // (few loop-carried fields; the layout is derived at store time)
@@ -956,23 +990,30 @@ __device__ __forceinline__ void store_pend(const PendSeq& p, const SrcRing& V, g
     }
 }
 
-template <bool ST>
+template <bool ST, bool U16, bool SPLIT = false>
 __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
                                    l_u32* __restrict__ T, l_u8* __restrict__ R, uint64_t* acc) {
+    using G = V5Geo<U16, SPLIT>;
+    const G tab{T};
     const uint32_t L = laneid();
     uint64_t ts = STAMP_T();
     const uint32_t bound = n + n / 255 + 16;
     const bool limited = cap < bound;
+    if (n < (uint32_t)kMinLength) {   // too short to search: one literal run (1.9.3 _last_literals)
+        if (limited && n + 1 + (n + 240) / 255 > cap) return 0;
+        if (L == 0) d[0] = (uint8_t)(n << 4);
+        for (uint32_t x = L; x < n; x += 64) d[1 + x] = s[x];
+        return (int32_t)(n + 1);
+    }
     {
-        const uint32_t t0 = cand_tag(gld4u(s)) << kPosBits;   // fresh entry = position 0 (a real candidate)
-        for (uint32_t i = L; i < 1024; i += 64) ((l_u4*)T)[i] = (v4u){t0, t0, t0, t0};
+        tab.init(G::tag(gld4u(s)) << G::PB);   // fresh entry = position 0 (a real candidate)
     }
     SrcRing V{s, n, R, 0, 0, 0};
     V.init();
     const uint32_t mflimitP1 = n - kMfLimit + 1;
     const uint32_t matchlimit = n - kLastLiterals;
     const uint32_t last4 = n - 4;
-    const uint32_t dumIdx = kDummy + L;
+    const uint32_t dumIdx = G::kTE + L;
     uint32_t anchor = 0, op = 0;
     PendSeq pe{};
     bool havePe = false;
@@ -1020,18 +1061,18 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             v8 = ((uint64_t)b << 32) | a;
         }
         const uint32_t w0 = (uint32_t)v8;
-        const uint32_t h = lz4_hash<false>(w0, (uint32_t)(v8 >> 32));
-        const uint32_t mark = p | (cand_tag(w0) << kPosBits);   // the lane's final table entry
+        const uint32_t h = lz4_hash<U16>(w0, (uint32_t)(v8 >> 32));
+        const uint32_t mark = p | (G::tag(w0) << G::PB);   // the lane's final table entry
         // ---- table probe: read, write the marker, read back (LDS ops of a wave run in order)
         const uint32_t ti = live ? h : dumIdx;
-        const uint32_t told = T[ti];
-        T[ti] = mark;
+        const uint32_t told = tab.ld(ti);
+        tab.st(ti, mark);
         WAVE_SYNC();
-        const uint32_t sv = T[ti];
-        const uint64_t pend = bal(sv != mark);   // same-bucket collision inside the window
-        uint32_t cand = told & kPosMask;
+        const uint32_t sv = tab.rb(ti);
+        const uint64_t pend = bal(sv != (mark & G::kRbMask));   // same-bucket collision inside the window
+        uint32_t cand = told & G::PM;
         const bool cok = live && L != 0 && !term && cand + kDistMax >= p;
-        bool maybe = cok && (told >> kPosBits) == (mark >> kPosBits);
+        bool maybe = cok && (told >> G::PB) == (mark >> G::PB);
         const uint64_t tmk = bal(term);
         uint64_t mm = bal(maybe);
         uint64_t sm = mm | tmk;
@@ -1050,11 +1091,11 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         auto table_writes = [&](uint32_t ws, bool wsTerm) {
             const int wlim = (ws == 64) ? 63 : (wsTerm ? (int)ws - 1 : (int)ws);
             const bool le = (int)L <= wlim;
-            T[(live && !le) ? h : dumIdx] = told;
+            tab.st((live && !le) ? h : dumIdx, told);
             if (pend || twRedo) {
                 const uint64_t upto = wlim < 0 ? 0ull : mask_le((uint32_t)wlim);
                 const bool lastM = !dd || !(gmask & ~mask_le(L) & upto);
-                T[(live && le && lastM) ? h : dumIdx] = mark;
+                tab.st((live && le && lastM) ? h : dumIdx, mark);
             }
             WAVE_SYNC();
         };
@@ -1256,7 +1297,7 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
 #ifdef LZ4MT_ENC_T
         r = encode_block_t<false>(s, n, d, cap, Tl, Sl, Xl, nullptr);
 #else
-        r = encode_block_v5<false>(s, n, d, cap, Tl, Xl, nullptr);
+        r = encode_block_v5<false, false>(s, n, d, cap, Tl, Xl, nullptr);
 #endif
     else
         r = encode_block<false, false, false>(s, n, d, cap, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
@@ -1283,7 +1324,7 @@ __global__ void __launch_bounds__(64) k_encode_stats(const uint8_t* __restrict__
 #ifdef LZ4MT_ENC_T
         r = encode_block_t<true>(s, n, d, n, (l_u32*)T, (l_u8*)S, Xl, acc);
 #else
-        r = encode_block_v5<true>(s, n, d, n, (l_u32*)T, Xl, acc);
+        r = encode_block_v5<true, false>(s, n, d, n, (l_u32*)T, Xl, acc);
 #endif
     else
         r = encode_block<false, false, true>(s, n, d, n, (l_u32*)T, (l_u8*)S, (l_u32*)Xl, Xl + kRingE, acc);
@@ -1293,11 +1334,38 @@ __global__ void __launch_bounds__(64) k_encode_stats(const uint8_t* __restrict__
     }
 }
 
+// Frames of blocks below 65 547 bytes (-B4: 64 KiB): every block uses the
+// byU16 table, so the kernel carries the 8192-entry table (34.3 KiB of LDS,
+// 4 waves per CU) instead of k_encode's 20 KiB.
+#ifndef LZ4MT_E16_SPLIT
+#define LZ4MT_E16_SPLIT 1
+#endif
+constexpr bool kE16Split = LZ4MT_E16_SPLIT;
+constexpr uint32_t kE16TabWords = kE16Split ? (8192 + 64) * 3 / 4 : 8192 + 64;
+constexpr uint32_t kE16Words = kE16TabWords + (kSR + kSRMirror) / 4;
+__global__ void __launch_bounds__(64) k_encode16(const uint8_t* __restrict__ src, uint64_t srcSize,
+                                                 uint32_t blockSize, uint8_t* __restrict__ slots,
+                                                 uint64_t slotStride, uint32_t capOverride,
+                                                 int32_t* __restrict__ csize) {
+    __shared__ uint32_t E16[kE16Words];
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
+    const uint32_t cap = (capOverride == 0xFFFFFFFFu) ? n : capOverride;   // lz4mt: cap = n
+    const int32_t r = encode_block_v5<false, true, kE16Split>(gptr(src) + off, n, gptr(slots) + (uint64_t)b * slotStride,
+                                                              cap, (l_u32*)E16, (l_u8*)(E16 + kE16TabWords), nullptr);
+    if (laneid() == 0) csize[b] = r;
+}
+
 hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks, uint8_t* slots,
                          uint64_t slotStride, uint32_t capOverride, int32_t* csize, hipStream_t st) {
     if (nBlocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_encode, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, slotStride,
-                       capOverride, csize);
+    if (blockSize < (uint32_t)kLimit64K)
+        hipLaunchKernelGGL(k_encode16, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, slotStride,
+                           capOverride, csize);
+    else
+        hipLaunchKernelGGL(k_encode, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, slotStride,
+                           capOverride, csize);
     return hipGetLastError();
 }
 #endif

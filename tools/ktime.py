@@ -1,4 +1,4 @@
-"""Encode and decode kernel times (8 GiB, 4 MiB blocks; best of 3) for A/B
+"""Encode and decode kernel times (8 GiB, 4 MiB blocks or BID=4..6; best of 3) for A/B
 timing of experiment builds: LZ4MT_AMD_LIB=<variant .so> python tools/ktime.py"""
 import ctypes
 import os
@@ -12,7 +12,7 @@ import lz4mt_amd as L  # noqa: E402
 
 n = 8 << 30
 src = L.gen_synthetic(n)
-sd = L.make_sd(7, False, True)
+sd = L.make_sd(int(os.environ.get("BID", "7")), False, True)
 L.lib.lz4mtHipSetTiming(1)
 ms = (ctypes.c_float * 4)()
 enc, dec, wc, wd, xc, xd = 1e9, 1e9, 1e9, 1e9, 1e9, 1e9
