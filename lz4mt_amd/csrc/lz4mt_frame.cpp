@@ -24,6 +24,8 @@
 // no counterpart; lz4mtResultToString names every code.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
@@ -293,12 +295,40 @@ void compress_host(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
 // sized by the largest batch seen; they are reused in FIFO order, which is
 // the block order the writes must keep.
 // ---------------------------------------------------------------------------
-constexpr int kSlots = 6;
+constexpr int kSlots = 8;   // slots allocated (at most); slot_count() are used
+// LZ4MT_AMD_SLOTS / LZ4MT_AMD_BATCH_MIB override the defaults (tuning runs)
+int env_int(const char* name, int dflt, int lo, int hi) {
+    const char* e = getenv(name);
+    const int v = e ? atoi(e) : dflt;
+    return v < lo ? lo : (v > hi ? hi : v);
+}
+// Pipeline shape per direction.  An encode batch of any size takes about one
+// block latency (~150-190 ms for 4 MiB blocks), so compress
+// needs GiBs in flight to approach the kernel rate: 4 slots of up to 2 GiB.
+// Decode latency is ~6x shorter: 8 slots of up to 1 GiB.  Batches start at
+// 256 MiB and double per fill, so small inputs stage little.
+struct PipeShape {
+    int slots;
+    uint64_t maxBatch;   // bytes of uncompressed data per batch
+};
+PipeShape pipe_shape(bool compress) {
+    const int dS = compress ? 4 : 8, dM = compress ? 2048 : 1024;
+    return PipeShape{env_int("LZ4MT_AMD_SLOTS", dS, 1, kSlots),
+                     (uint64_t)env_int("LZ4MT_AMD_BATCH_MIB", dM, 1, 16384) << 20};
+}
+// blocks of batch number `i` (0, 1, ...): 256 MiB << i, capped, >= 1 block
+uint64_t batch_blocks(const PipeShape& P, uint32_t bm, uint64_t i) {
+    const uint64_t want = std::min<uint64_t>(P.maxBatch, (256ull << 20) << std::min<uint64_t>(i, 8));
+    return std::max<uint64_t>(1, want / bm);
+}
 
 struct Slot {
     hipStream_t st = nullptr;
+    // one pinned host buffer per slot: hOut aliases hIn (a batch's H2D is
+    // stream-ordered before its D2H, and the host is done with its input
+    // before the D2H is issued)
     uint8_t *hIn = nullptr, *hOut = nullptr, *dIn = nullptr, *dOut = nullptr, *dWs = nullptr;
-    uint64_t inCap = 0, outCap = 0, wsCap = 0;
+    uint64_t hCap = 0, inCap = 0, outCap = 0, wsCap = 0;
     // per-batch metadata, pinned so it can travel asynchronously
     uint64_t* hMeta = nullptr;                // [0] = compressed body size
     BlockRec* hRecs = nullptr;                // decompress: block records
@@ -313,7 +343,7 @@ struct Slot {
 
     void release() {
         if (st) hipStreamSynchronize(st);
-        hipHostFree(hIn); hipHostFree(hOut); hipHostFree(hMeta); hipHostFree(hRecs); hipHostFree(hDs);
+        hipHostFree(hIn); hipHostFree(hMeta); hipHostFree(hRecs); hipHostFree(hDs);
         hipHostFree(hSt);
         hipFree(dIn); hipFree(dOut); hipFree(dWs); hipFree(dRecs); hipFree(dDs); hipFree(dSt); hipFree(dDig);
         if (st) hipStreamDestroy(st);
@@ -322,20 +352,24 @@ struct Slot {
     // grows the buffers (contents are not kept); 0 sizes leave a buffer alone
     bool ensure(uint64_t in, uint64_t out, uint64_t ws, uint64_t blocks) {
         if (!st && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
+        const uint64_t h = std::max(in, out);
+        if (h > hCap) {
+            hipHostFree(hIn);
+            hIn = hOut = nullptr; hCap = 0;
+            if (hipHostMalloc(reinterpret_cast<void**>(&hIn), h + 64, 0) != hipSuccess) return false;
+            hOut = hIn;
+            hCap = h;
+        }
         if (in > inCap) {
-            hipHostFree(hIn); hipFree(dIn);
-            hIn = nullptr; dIn = nullptr; inCap = 0;
-            if (hipHostMalloc(reinterpret_cast<void**>(&hIn), in + 64, 0) != hipSuccess ||
-                hipMalloc(reinterpret_cast<void**>(&dIn), in + 64) != hipSuccess)
-                return false;
+            hipFree(dIn);
+            dIn = nullptr; inCap = 0;
+            if (hipMalloc(reinterpret_cast<void**>(&dIn), in + 64) != hipSuccess) return false;
             inCap = in;
         }
         if (out > outCap) {
-            hipHostFree(hOut); hipFree(dOut);
-            hOut = nullptr; dOut = nullptr; outCap = 0;
-            if (hipHostMalloc(reinterpret_cast<void**>(&hOut), out + 64, 0) != hipSuccess ||
-                hipMalloc(reinterpret_cast<void**>(&dOut), out + 64) != hipSuccess)
-                return false;
+            hipFree(dOut);
+            dOut = nullptr; outCap = 0;
+            if (hipMalloc(reinterpret_cast<void**>(&dOut), out + 64) != hipSuccess) return false;
             outCap = out;
         }
         if (ws > wsCap) {
@@ -388,7 +422,7 @@ thread_local SlotCache g_slots;
 // finish(S) returns false to stop the frame (later batches are drained
 // without writes).
 template <class Fill, class Finish>
-void run_slot_pipeline(Session& s, Fill fill, Finish finish) {
+void run_slot_pipeline(Session& s, int nSlots, Fill fill, Finish finish) {
     SlotCache& C = g_slots;
     std::mutex mu;
     std::condition_variable cv;
@@ -437,7 +471,7 @@ void run_slot_pipeline(Session& s, Fill fill, Finish finish) {
             q.push_back(head);
         }
         cv.notify_all();
-        head = (head + 1) % kSlots;
+        head = (head + 1) % nSlots;
         if (stop) break;
     }
     {
@@ -451,15 +485,17 @@ void run_slot_pipeline(Session& s, Fill fill, Finish finish) {
 
 // Blocks per batch: ~512 MiB of input (at least one block); kSlots batches
 // in flight keep up to 3 GiB of blocks on the GPU at once.
-uint64_t batch_blocks(uint32_t bm) { return std::max<uint64_t>(1, (512ull << 20) / bm); }
+
 
 void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
     if (s.level() >= 3) { s.quit(LZ4MT_RESULT_BAD_ARG); return; }   // no GPU LZ4-HC
     if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return; }
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
-    const uint64_t K = batch_blocks(bm), inCap = K * bm;
+    const PipeShape P = pipe_shape(true);
+    uint64_t batch = 0;
     auto fill = [&](Slot& S, bool* stop) -> bool {
+        const uint64_t K = batch_blocks(P, bm, batch++), inCap = K * bm;
         if (!S.ensure(inCap, inCap + K * 8 + 64, compress_ws_bytes(inCap, bm), 0)) {
             s.quit(LZ4MT_RESULT_ERROR);
             return false;
@@ -501,7 +537,7 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
         }
         return true;
     };
-    run_slot_pipeline(s, fill, finish);
+    run_slot_pipeline(s, P.slots, fill, finish);
 }
 
 // ---------------------------------------------------------------------------
@@ -559,11 +595,13 @@ bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
     if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return false; }
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
-    const uint64_t K = batch_blocks(bm);
+    const PipeShape P = pipe_shape(false);
+    uint64_t batch = 0;
     bool eos = false;
     Lz4MtResult pending = LZ4MT_RESULT_OK;   // a read error found while filling a batch
     auto fill = [&](Slot& S, bool* stop) -> bool {
         if (eos || pending != LZ4MT_RESULT_OK || s.readEof()) return false;
+        const uint64_t K = batch_blocks(P, bm, batch++);
         if (!S.ensure(K * bm + 16 * K, K * bm, 0, K)) { s.quit(LZ4MT_RESULT_ERROR); return false; }
         uint64_t used = 0, nb = 0;
         while (nb < K) {
@@ -617,7 +655,7 @@ bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
         }
         return true;
     };
-    run_slot_pipeline(s, fill, finish);
+    run_slot_pipeline(s, P.slots, fill, finish);
     if (pending != LZ4MT_RESULT_OK) s.quit(pending);   // refines a read ERROR; a block's own failure wins
     return eos;
 }

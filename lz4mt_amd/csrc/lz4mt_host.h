@@ -45,7 +45,16 @@ public:
             stripe(buf_);
             fill_ = 0;
         }
-        while (len >= 16) { stripe(p); p += 16; len -= 16; }
+        // bulk: the four lanes in locals (stores to v_ through `this` would
+        // alias the byte pointer and pin them to memory every stripe)
+        uint32_t a = v_[0], b = v_[1], c = v_[2], d = v_[3];
+        for (; len >= 16; p += 16, len -= 16) {
+            a = rotl(a + get32(p) * P2, 13) * P1;
+            b = rotl(b + get32(p + 4) * P2, 13) * P1;
+            c = rotl(c + get32(p + 8) * P2, 13) * P1;
+            d = rotl(d + get32(p + 12) * P2, 13) * P1;
+        }
+        v_[0] = a; v_[1] = b; v_[2] = c; v_[3] = d;
         memcpy(buf_, p, len);
         fill_ = (uint32_t)len;
     }

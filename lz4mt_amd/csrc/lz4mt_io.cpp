@@ -1,13 +1,151 @@
 // lz4mt_io.cpp — FILE* and memory callbacks for Lz4MtContext.
 // FILE* side mirrors reference src/lz4mt_io_cstdio.cpp:75-175 (fread/fwrite/
 // fseek/feof; "stdin"/"stdout" names; null sink = writeCtx == ctx).
+//
+// Large transfers (>= 2 MiB: the DEVICE engine reads and writes whole
+// blocks) are split over a small copy pool, so one calling thread is not
+// held to one core's memcpy/page-cache rate (~6.5 GB/s into pinned memory).
+// The callbacks keep the reference's contract: they are still called from
+// one thread at a time per stream and return only when the bytes are there.
+#include <fcntl.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
 
 #include "../../include/lz4mt_io.h"
 
 namespace {
+constexpr size_t kParMin = 2u << 20;     // smaller transfers stay on the caller
+constexpr size_t kPiece = 1u << 20;      // at least 1 MiB per piece
+
+// Persistent helper threads; run(n, f) calls f(0..n-1) on the helpers and
+// the caller and returns when all are done.  Safe for concurrent callers
+// (the DEVICE engine reads on the calling thread while its writer writes).
+class CopyPool {
+    struct Job {
+        std::function<void(int)> fn;
+        int n = 0;
+        std::atomic<int> next{0};
+        std::atomic<int> done{0};
+        std::mutex m;
+        std::condition_variable cv;
+        void work() {
+            for (int i; (i = next.fetch_add(1)) < n;) {
+                fn(i);
+                if (done.fetch_add(1) + 1 == n) {
+                    std::lock_guard<std::mutex> g(m);
+                    cv.notify_all();
+                }
+            }
+        }
+    };
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::deque<std::shared_ptr<Job>> q_;
+    std::vector<std::thread> th_;
+    bool stop_ = false;
+
+    CopyPool() {
+        const unsigned hw = std::thread::hardware_concurrency();
+        const unsigned nt = std::min(7u, hw > 1 ? hw - 1 : 0u);
+        for (unsigned i = 0; i < nt; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~CopyPool() {
+        { std::lock_guard<std::mutex> g(m_); stop_ = true; }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void loop() {
+        for (;;) {
+            std::shared_ptr<Job> j;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return stop_ || !q_.empty(); });
+                if (stop_) return;
+                j = std::move(q_.front());
+                q_.pop_front();
+            }
+            j->work();
+        }
+    }
+
+public:
+    static CopyPool& get() { static CopyPool p; return p; }
+    int width() const { return (int)th_.size() + 1; }
+    void run(int n, std::function<void(int)> fn) {
+        if (n <= 1 || th_.empty()) {
+            for (int i = 0; i < n; ++i) fn(i);
+            return;
+        }
+        auto j = std::make_shared<Job>();
+        j->fn = std::move(fn);
+        j->n = n;
+        {
+            std::lock_guard<std::mutex> g(m_);
+            for (int k = 1; k < std::min(n, width()); ++k) q_.push_back(j);
+        }
+        cv_.notify_all();
+        j->work();
+        std::unique_lock<std::mutex> g(j->m);
+        j->cv.wait(g, [&] { return j->done.load() == j->n; });
+    }
+};
+
+int pieces(size_t n) { return (int)std::min<size_t>((size_t)CopyPool::get().width(), n / kPiece); }
+
+void par_copy(void* dst, const void* src, size_t n) {
+    if (n < kParMin) { memcpy(dst, src, n); return; }
+    const int k = pieces(n);
+    const size_t per = (n / (size_t)k + 4095) & ~(size_t)4095;
+    CopyPool::get().run(k, [=](int i) {
+        const size_t o = (size_t)i * per;
+        if (o < n) memcpy(static_cast<char*>(dst) + o, static_cast<const char*>(src) + o, std::min(per, n - o));
+    });
+}
+
+// pread/pwrite of [off, off + n) split over the pool; returns bytes moved
+// from the start (stops at the first short piece, like one big call)
+size_t par_pio(int fd, void* buf, size_t n, off_t off, bool wr) {
+    const int k = pieces(n);
+    const size_t per = (n / (size_t)k + 4095) & ~(size_t)4095;
+    std::vector<size_t> got((size_t)k, 0);
+    CopyPool::get().run(k, [&](int i) {
+        const size_t o = (size_t)i * per;
+        if (o >= n) return;
+        const size_t len = std::min(per, n - o);
+        size_t d = 0;
+        while (d < len) {
+            char* p = static_cast<char*>(buf) + o + d;
+            const ssize_t r = wr ? pwrite(fd, p, len - d, off + (off_t)(o + d)) : pread(fd, p, len - d, off + (off_t)(o + d));
+            if (r <= 0) break;
+            d += (size_t)r;
+        }
+        got[(size_t)i] = d;
+    });
+    size_t total = 0;
+    for (int i = 0; i < k; ++i) {
+        total += got[(size_t)i];
+        if (got[(size_t)i] < std::min(per, n - std::min(n, (size_t)i * per))) break;
+    }
+    return total;
+}
+
+bool regular(FILE* fp) {
+    struct stat st;
+    return fstat(fileno(fp), &st) == 0 && S_ISREG(st.st_mode);
+}
+
 FILE* in_fp(const Lz4MtContext* c) { return static_cast<FILE*>(c->readCtx); }
 FILE* out_fp(const Lz4MtContext* c) { return static_cast<FILE*>(c->writeCtx); }
 bool is_null_sink(const Lz4MtContext* c) { return c->writeCtx == static_cast<const void*>(c); }
@@ -45,7 +183,20 @@ extern "C" void lz4mtIoCloseOstream(Lz4MtContext* ctx) {
 
 extern "C" int lz4mtIoRead(Lz4MtContext* ctx, void* dst, int dstSize) {
     FILE* fp = in_fp(ctx);
-    return fp ? (int)fread(dst, 1, (size_t)dstSize, fp) : 0;
+    if (!fp) return 0;
+    if (dstSize >= (int)kParMin && regular(fp)) {   // parallel pread at the stream position
+        const off_t off = ftello(fp);
+        if (off >= 0) {
+            const size_t got = par_pio(fileno(fp), dst, (size_t)dstSize, off, false);
+            fseeko(fp, off + (off_t)got, SEEK_SET);
+            if (got < (size_t)dstSize) {   // short: leave the stream at EOF like fread
+                const int c = fgetc(fp);
+                if (c != EOF) ungetc(c, fp);
+            }
+            return (int)got;
+        }
+    }
+    return (int)fread(dst, 1, (size_t)dstSize, fp);
 }
 
 extern "C" int lz4mtIoReadSkippable(const Lz4MtContext* ctx, uint32_t, size_t size) {
@@ -66,7 +217,16 @@ extern "C" int lz4mtIoReadEof(const Lz4MtContext* ctx) {
 extern "C" int lz4mtIoWrite(const Lz4MtContext* ctx, const void* src, int srcSize) {
     if (is_null_sink(ctx)) return srcSize;
     FILE* fp = out_fp(ctx);
-    return fp ? (int)fwrite(src, 1, (size_t)srcSize, fp) : 0;
+    if (!fp) return 0;
+    if (srcSize >= (int)kParMin && regular(fp) && fflush(fp) == 0) {   // parallel pwrite at the position
+        const off_t off = ftello(fp);
+        if (off >= 0) {
+            const size_t put = par_pio(fileno(fp), const_cast<void*>(src), (size_t)srcSize, off, true);
+            fseeko(fp, off + (off_t)put, SEEK_SET);
+            return (int)put;
+        }
+    }
+    return (int)fwrite(src, 1, (size_t)srcSize, fp);
 }
 
 extern "C" uint64_t lz4mtIoGetFilesize(const char* filename) {
@@ -93,7 +253,7 @@ int mem_read(Lz4MtContext* ctx, void* dst, int n) {
     const uint64_t rem = io->inSize - io->inPos;
     const uint64_t got = (uint64_t)n < rem ? (uint64_t)n : rem;
     if ((uint64_t)n > rem) io->eof = 1;
-    memcpy(dst, io->in + io->inPos, got);
+    par_copy(dst, io->in + io->inPos, got);
     io->inPos += got;
     return (int)got;
 }
@@ -118,7 +278,7 @@ int mem_write(const Lz4MtContext* ctx, const void* src, int n) {
     if (n < 0) return 0;
     if (io->out) {
         if (io->outPos + (uint64_t)n > io->outCap) return 0;
-        memcpy(io->out + io->outPos, src, (size_t)n);
+        par_copy(io->out + io->outPos, src, (size_t)n);
     }
     io->outPos += (uint64_t)n;
     return n;

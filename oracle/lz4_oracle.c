@@ -75,9 +75,14 @@ void orc_xxh32_update(orc_xxh32_state* s, const void* in, size_t len) {
         for (int i = 0; i < 4; i++) s->v[i] = xround(s->v[i], rd32(s->mem + 4 * i));
         p += fill; len -= fill; s->memSize = 0;
     }
-    while (len >= 16) {
-        for (int i = 0; i < 4; i++) s->v[i] = xround(s->v[i], rd32(p + 4 * i));
-        p += 16; len -= 16;
+    {   /* lanes in locals: s->v stores would alias the byte pointer */
+        uint32_t v1 = s->v[0], v2 = s->v[1], v3 = s->v[2], v4 = s->v[3];
+        while (len >= 16) {
+            v1 = xround(v1, rd32(p)); v2 = xround(v2, rd32(p + 4));
+            v3 = xround(v3, rd32(p + 8)); v4 = xround(v4, rd32(p + 12));
+            p += 16; len -= 16;
+        }
+        s->v[0] = v1; s->v[1] = v2; s->v[2] = v3; s->v[3] = v4;
     }
     memcpy(s->mem, p, len); s->memSize = (uint32_t)len;
 }

@@ -185,3 +185,45 @@ def test_cstdio_adapters(tmp_path, golden_inputs, cpu_codec):
     L.lib.lz4mtIoCloseOstream(ctypes.byref(ctx))
     assert dst.read_bytes() == read_golden("frames/text20k.B7Sx.lz4")
     assert L.lib.lz4mtIoGetFilesize(str(dst).encode()) == dst.stat().st_size
+
+
+def test_large_transfers_through_io_bindings(tmp_path):
+    """Reads/writes >= 2 MiB go through the copy pool (parallel memcpy /
+    pread / pwrite); bytes, positions and fread/feof semantics must not change."""
+    import random
+    rnd = random.Random(7)
+    data = bytes(rnd.getrandbits(8) for _ in range(1 << 16)) * 150 + b"tail!"   # 9.4 MiB
+    src, dst = tmp_path / "in.bin", tmp_path / "out.bin"
+    src.write_bytes(data)
+    ctx = L.init_context()
+    L.lib.lz4mtIoBindCstdio(ctypes.byref(ctx))
+    assert L.lib.lz4mtIoOpenIstream(ctypes.byref(ctx), str(src).encode())
+    assert L.lib.lz4mtIoOpenOstream(ctypes.byref(ctx), str(dst).encode(), 0)
+    got = []
+    for size in (5, 3 << 20, 4096, 4 << 20, 4 << 20):   # small, large, small, large, short-at-EOF
+        buf = ctypes.create_string_buffer(size)
+        n = L.lib.lz4mtIoRead(ctypes.byref(ctx), buf, size)
+        got.append(buf.raw[:n])
+        assert L.lib.lz4mtIoWrite(ctypes.byref(ctx), buf, n) == n
+    assert b"".join(got) == data
+    assert L.lib.lz4mtIoReadEof(ctypes.byref(ctx)) != 0
+    buf = ctypes.create_string_buffer(8)
+    assert L.lib.lz4mtIoRead(ctypes.byref(ctx), buf, 8) == 0
+    L.lib.lz4mtIoCloseIstream(ctypes.byref(ctx))
+    L.lib.lz4mtIoCloseOstream(ctypes.byref(ctx))
+    assert dst.read_bytes() == data
+
+    # memory binding: the same sequence of reads and writes
+    inb = ctypes.create_string_buffer(data, len(data))
+    outb = ctypes.create_string_buffer(len(data) + 16)
+    io = _abi.Lz4MtMemIo(ctypes.cast(inb, ctypes.c_void_p).value, len(data), 0, 0,
+                         ctypes.cast(outb, ctypes.c_void_p).value, len(data) + 16, 0)
+    ctx = L.init_context()
+    L.lib.lz4mtMemBind(ctypes.byref(ctx), ctypes.byref(io))
+    rd, wr = _abi.READ_FN(ctx.read), _abi.WRITE_FN(ctx.write)
+    for size in (5, 3 << 20, 4096, 4 << 20, 4 << 20):
+        buf = ctypes.create_string_buffer(size)
+        n = rd(ctypes.byref(ctx), ctypes.cast(buf, ctypes.c_void_p), size)
+        assert wr(ctypes.byref(ctx), ctypes.cast(buf, ctypes.c_void_p), n) == n
+    assert io.eof == 1 and io.inPos == len(data) and io.outPos == len(data)
+    assert outb.raw[:len(data)] == data
