@@ -334,6 +334,22 @@ struct DecodeBuffers {
     }
 };
 
+// Per-thread cache of the decode scratch (records, digests, walk scratch):
+// no hipMalloc / hipFree per call -- hipFree waits for the whole device,
+// which would also wait for unrelated work such as an RCCL transfer running
+// beside the decode.  Re-made when the thread's current device changes.
+DecodeBuffers& decode_cache() {
+    thread_local DecodeBuffers B;
+    thread_local int dev = -1;
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) d = -1;
+    if (d != dev) {
+        B.release();
+        dev = d;
+    }
+    return B;
+}
+
 // Walks one frame body; retries with a larger block table if needed.
 Lz4MtResult walk_frame(const uint8_t* frame, uint64_t frameSize, uint64_t bodyPos, uint32_t bm, int bck,
                        DecodeBuffers& B, WalkInfo& wi, hipStream_t st) {
@@ -424,7 +440,7 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
     uint64_t pos = 0, opos = 0;
     bool seen = false;
     Lz4MtResult result = LZ4MT_RESULT_OK;
-    DecodeBuffers B;
+    DecodeBuffers& B = decode_cache();
     uint8_t* tmp = nullptr;   // staging when a frame's output is unaligned or needs compaction
     uint64_t tmpCap = 0;
     if (outSize) *outSize = 0;

@@ -79,7 +79,7 @@ def frame_records(frame, frame_len=None):
     return hdr, rec
 
 
-def gather_frame(frame, frame_len, dst=0, group=None):
+def gather_frame(frame, frame_len, dst=0, group=None, async_op=False):
     """Gathers every rank's shard frame into ONE frame on ``dst``.
 
     ``frame`` is this rank's uint8 tensor (device tensor under RCCL, CPU under
@@ -92,6 +92,11 @@ def gather_frame(frame, frame_len, dst=0, group=None):
     grouped point-to-point sends of each rank's record run straight into its
     final place in the root's frame (no padding, no staging copy).  This is
     the path's only collective; it is bound by the root's inbound xGMI links.
+
+    With ``async_op`` the point-to-point transfers are only enqueued: the
+    call returns ``(frame_or_None, works)`` and the caller waits on
+    ``works`` (e.g. after launching the local decompress, which only reads
+    ``frame``); the stitched frame is complete once they are done.
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -104,21 +109,31 @@ def gather_frame(frame, frame_len, dst=0, group=None):
     peer = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
     if rank == dst:
         out = torch.empty(hdr + sum(lens) + 4, dtype=torch.uint8, device=dev)
-        out[:hdr] = frame[:hdr]
-        ops, pos = [], hdr
+        ops, pos, mine = [], hdr, None
         for r, n in enumerate(lens):
             if r == rank:
-                out[pos:pos + n] = frame[hdr:hdr + n]
+                mine = (pos, n)
             elif n:
                 ops.append(dist.P2POp(dist.irecv, out[pos:pos + n], peer(r), group))
             pos += n
+        # receives first (their kernels then get the GPU before anything
+        # launched after this call), then the local pieces, which touch
+        # other bytes of `out`
+        works = dist.batch_isend_irecv(ops) if ops else []
+        out[:hdr] = frame[:hdr]
+        if mine and mine[1]:
+            out[mine[0]:mine[0] + mine[1]] = frame[hdr:hdr + mine[1]]
         out[pos:pos + 4] = 0
-        for w in (dist.batch_isend_irecv(ops) if ops else []):
+        if async_op:
+            return out, works
+        for w in works:
             w.wait()
         return out
-    if rec:
-        for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, frame[hdr:hdr + rec], peer(dst), group)]):
-            w.wait()
+    works = dist.batch_isend_irecv([dist.P2POp(dist.isend, frame[hdr:hdr + rec], peer(dst), group)]) if rec else []
+    if async_op:
+        return None, works
+    for w in works:
+        w.wait()
     return None
 
 

@@ -21,7 +21,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, block_id, bck, q):
+def _worker(rank, world, port, n, block_id, bck, q, async_op=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -31,18 +31,24 @@ def _worker(rank, world, port, n, block_id, bck, q):
         p = oracle.params(block_id, stream_checksum=False, block_checksum=bck)
         local = oracle.compress_frame(data[off:off + ln], p)
         t = torch.frombuffer(bytearray(local + b"\xAA" * 13), dtype=torch.uint8)   # slack past the frame end
-        full = D.gather_frame(t, len(local))
+        if async_op:   # enqueue, do other work reading the frame, then wait (bench.py at N > 1)
+            full, works = D.gather_frame(t, len(local), async_op=True)
+            assert oracle.decompress_frame(bytes(t.numpy().tobytes())[:len(local)], ln + bm)[1] == data[off:off + ln]
+            for w in works:
+                w.wait()
+        else:
+            full = D.gather_frame(t, len(local))
         if rank == 0:
             q.put(bytes(full.numpy().tobytes()))
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, n, block_id, bck):
+def _run(world, n, block_id, bck, async_op=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, block_id, bck, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, block_id, bck, q, async_op)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)
@@ -52,9 +58,11 @@ def _run(world, n, block_id, bck):
     return got
 
 
-@pytest.mark.parametrize("n,block_id,bck", [(17 * 65536 + 12345, 4, True), (3 * 262144, 5, False)])
-def test_gather_stitches_whole_stream_frame(n, block_id, bck):
-    got = _run(2, n, block_id, bck)
+@pytest.mark.parametrize("n,block_id,bck,async_op", [(17 * 65536 + 12345, 4, True, False),
+                                                     (3 * 262144, 5, False, False),
+                                                     (17 * 65536 + 12345, 4, True, True)])
+def test_gather_stitches_whole_stream_frame(n, block_id, bck, async_op):
+    got = _run(2, n, block_id, bck, async_op)
     want = oracle.compress_frame(oracle.gen_synthetic(n, 42), oracle.params(block_id, False, bck))
     assert got == want
 
