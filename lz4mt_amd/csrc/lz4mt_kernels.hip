@@ -600,291 +600,9 @@ struct SrcRing {
     __device__ __forceinline__ uint64_t rd8(uint32_t pos) const { return *(l_u64u*)(r + (pos & (kSR - 1))); }
 };
 
-// One encoded sequence waiting to be stored (issued while the next window's
-// round trip is in flight).
-struct SeqEmit {
-    uint32_t op, total, a1, a2, litExt, lit, token, litRem, mlRem, off, anchor;
-    bool direct;
-};
-__device__ __forceinline__ uint32_t seq_byte(const SeqEmit& e, uint32_t x, uint32_t lv) {
-    uint32_t v = x + 1 < e.total ? 255u : e.mlRem;
-    v = x == e.a2 + 1 ? e.off >> 8 : v;
-    v = x == e.a2 ? e.off & 255u : v;
-    v = x < e.a2 ? lv : v;
-    v = x < e.a1 ? (x < e.litExt ? 255u : e.litRem) : v;
-    return x == 0 ? e.token : v;
-}
-// common case (no catch-up, <= 64 bytes): lane L already holds its literal
-// byte; no loads, so nothing here waits on the round trip in flight
-__device__ __forceinline__ void store_seq_direct(const SeqEmit& e, uint32_t lbo, g_u8* __restrict__ d) {
-    const uint32_t L = laneid();
-    const uint32_t v = seq_byte(e, L, lbo);
-    if (L < e.total) d[e.op + L] = (uint8_t)v;
-}
-__device__ __forceinline__ void store_seq(const SeqEmit& e, uint32_t lb, g_cu8* __restrict__ s, g_u8* __restrict__ d) {
-    const uint32_t L = laneid();
-    for (uint32_t base = 0; base < e.total; base += 64) {
-        const uint32_t x = base + L;
-        const uint32_t j = x - e.a1;   // literal index (wraps when x < a1)
-        uint32_t lv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((j & 63) * 4), (int)lb);
-        if (j >= 64 && j < e.lit) lv = s[e.anchor + j];
-        const uint32_t v = seq_byte(e, x, lv);
-        if (x < e.total) d[e.op + x] = (uint8_t)v;
-    }
-}
-
-template <bool ST>
-__device__ int32_t encode_block_t(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
-                                  l_u32* __restrict__ T, l_u8* __restrict__ S, l_u8* __restrict__ R, uint64_t* acc) {
-    const uint32_t L = laneid();
-    uint64_t ts = STAMP_T();
-    const uint32_t bound = n + n / 255 + 16;
-    const bool limited = cap < bound;
-    {
-        const uint32_t t0 = cand_tag(gld4u(s)) << kPosBits;   // fresh entry = position 0 (a real candidate)
-        for (uint32_t i = L; i < 1024; i += 64) ((l_u4*)T)[i] = (v4u){t0, t0, t0, t0};
-    }
-    SrcRing V{s, n, R, 0, 0, 0};
-    V.init();
-    const uint32_t mflimitP1 = n - kMfLimit + 1;
-    const uint32_t matchlimit = n - kLastLiterals;
-    const uint32_t last4 = n - 4, last1 = n - 1;   // clamps: every load stays inside the block
-    uint32_t anchor = 0, op = 0;
-    SeqEmit pe{};
-    bool havePe = false;
-    uint32_t peLb = 0, peLbo = 0;
-    // window: [INSERT][TEST] SEARCH...; probe k0+j of the search sits at sPos + F(k0+j)
-    uint32_t hasIns = 1, hasTest = 0, insPos = 0, testPos = 0, sPos = 1, k0 = 0;
-    for (;;) {
-        if (ST) acc[10] += 1;
-        STAMP_ADD(9, ts);
-        // ---- lane positions, branch-free
-        const uint32_t ns = hasIns + hasTest;
-        const int kk = (int)(k0 + L) - (int)ns;          // search index (< 0: INSERT / TEST lanes)
-        const uint32_t km1 = (uint32_t)(kk - 1), q = km1 >> 6, r6 = km1 & 63u;
-        const uint32_t offk = kk <= 0 ? 0u : 1u + 32u * q * (q + 1u) + r6 * (q + 1u);
-        const uint32_t step = kk <= 0 ? 1u : ((uint32_t)(63 + kk) >> 6);
-        const bool isIns = L < hasIns;
-        const bool isSearch = L >= ns;
-        const uint32_t p = isIns ? insPos : (isSearch ? sPos + offk : testPos);
-        const bool live = !isSearch || p <= mflimitP1;
-        const bool term = isSearch && live && (p + step > mflimitP1);
-        // ---- hash inputs: bytes [p, p+8)
-        const uint32_t lo = rdlane(p, 0), plast = rdlane(p, 63);
-        const uint32_t hi = (plast < mflimitP1 ? plast : mflimitP1) + 8;
-        uint64_t v8;
-        if (hi - lo <= 1024) {
-            V.cover(hi);
-            v8 = V.rd8(p);
-        } else {
-            v8 = gld8u(s + (p < n - 8 ? p : n - 8));
-        }
-        const uint32_t w0 = (uint32_t)v8;
-        const uint32_t h = live ? lz4_hash<false>(w0, (uint32_t)(v8 >> 32)) : 0u;
-        const uint32_t mytag = cand_tag(w0);
-        STAMP_ADD(0, ts);
-        // ---- table + exact in-window duplicate hashes: every live lane
-        // writes a lane marker into its bucket and reads it back (LDS ops of
-        // one wave execute in order); buckets are repaired below
-        const uint32_t told = T[h];
-        const uint32_t marker = 0xFFC00000u | L;
-        if (live) T[h] = marker;
-        WAVE_SYNC();
-        const uint32_t sv = T[h];
-        uint64_t pending = ballot(live && sv != marker);
-        int pred = -1;
-        uint64_t gmask = 1ull << L;
-        uint32_t pw = 0, pp = 0;
-        if (pending) {   // in-window duplicate hashes (most windows have none)
-            while (pending) {   // one iteration per group of equal hashes
-                const int leader = __ffsll((long long)pending) - 1;
-                const uint32_t key = rdlane(h, leader);
-                const uint64_t m = ballot(live && h == key);
-                const bool inG = (m >> L) & 1;
-                const uint64_t below = m & ((1ull << L) - 1ull);
-                const int pr = below ? 63 - __clzll((long long)below) : -1;
-                pred = inG ? pr : pred;
-                gmask = inG ? m : gmask;
-                pending &= ~m;
-            }
-            const int pi = (pred < 0 ? 0 : pred) * 4;
-            pw = (uint32_t)__builtin_amdgcn_ds_bpermute(pi, (int)w0);   // predecessor's bytes
-            pp = (uint32_t)__builtin_amdgcn_ds_bpermute(pi, (int)p);    // and position
-        }
-        const uint32_t cand = pred >= 0 ? pp : (told & kPosMask);
-        STAMP_ADD(1, ts);
-        const bool cok = live && !isIns && !term && (cand + kDistMax >= p);
-        const bool ok = cok && pred >= 0 && pw == w0;
-        const bool maybe = cok && pred < 0 && (told >> kPosBits) == mytag;
-        uint64_t sm = ballot(term || ok || maybe);
-        const uint64_t mm = ballot(maybe), tmk = ballot(term);
-        STAMP_ADD(2, ts);
-        // ---- first stop; a tag-equal lane is confirmed inside the round trip
-        int w;
-        uint32_t ip = 0, cd = 0, maxb = 0, lim = 0, lit0 = 0, cw = 0, iw = 0, lb = 0, lbo = 0;
-        bool beq = false;
-        for (;;) {
-            w = sm ? __ffsll((long long)sm) - 1 : 64;
-            if (w == 64 || ((tmk >> w) & 1)) break;
-            ip = rdlane(p, w);
-            cd = rdlane(cand, w);
-            const bool wasTest = (uint32_t)w >= hasIns && (uint32_t)w < ns;
-            maxb = wasTest ? 0u : min(ip - anchor, cd);
-            lim = matchlimit - (ip + kMinMatch);
-            lit0 = ip - anchor;
-            // one round trip, every address clamped into the block:
-            //   cw lane 0 = 4 bytes at cd (verify), lanes >= 1 = count words at cd+4+4(L-1)
-            //   iw = the ip side; bi/bc = catch-up bytes; lb = literal L;
-            //   lbo = the literal byte output lane L stores (no catch-up case)
-            const uint32_t ci = cd + 4 * L, ii = ip + 4 * L;
-            cw = gld4u(s + (ci < last4 ? ci : last4));
-            iw = gld4u(s + (ii < last4 ? ii : last4));
-            const bool bOn = L + 1 <= maxb;
-            const uint32_t bi = s[bOn ? ip - L - 1 : 0u], bc = s[bOn ? cd - L - 1 : 0u];
-            const uint32_t la = anchor + L;
-            lb = s[la < last1 ? la : last1];
-            const uint32_t lj = anchor + L - 1 - ext_len(lit0);
-            lbo = s[lj < last1 ? lj : last1];
-            beq = bOn && bi == bc;
-            if (havePe) {   // previous sequence's stores overlap this round trip
-                if (pe.direct) store_seq_direct(pe, peLbo, d);
-                else store_seq(pe, peLb, s, d);
-                havePe = false;
-            }
-            STAMP_ADD(3, ts);
-            if (((mm >> w) & 1) && (ballot(L == 0 && cw != rdlane(w0, w)) & 1)) {   // tag alias
-                if (ST) acc[11] += 1;
-                sm &= ~(1ull << w);
-                continue;
-            }
-            if (ST) acc[12] += (mm >> w) & 1;
-            break;
-        }
-        if (havePe) {
-            if (pe.direct) store_seq_direct(pe, peLbo, d);
-            else store_seq(pe, peLb, s, d);
-            havePe = false;
-        }
-        STAMP_ADD(5, ts);
-        const bool wTerm = (w < 64) && ((tmk >> w) & 1);
-        const int wlim = (w == 64) ? 63 : (wTerm ? w - 1 : w);
-        // ---- table writes: last member of each hash group among lanes <= wlim
-        {
-            const uint64_t upto = wlim < 0 ? 0ull : mask_le((uint32_t)wlim);
-            const bool ins = (int)L <= wlim;
-            const bool lastIns = ins && !(gmask & ~mask_le(L) & upto);
-            const bool restore = !(gmask & upto);   // no member inserts: put the old entry back
-            if (live && (lastIns || restore)) T[h] = ins ? (p | (mytag << kPosBits)) : told;
-        }
-        WAVE_SYNC();
-        STAMP_ADD(6, ts);
-        if (w == 64) {   // no stop: continue the search
-            k0 += 64 - ns;
-            hasIns = 0; hasTest = 0;
-            continue;
-        }
-        if (wTerm) break;
-        const bool wasTest = (uint32_t)w >= hasIns && (uint32_t)w < ns;
-
-        // ---- catch-up and forward count (LZ4_count from the caught-up start
-        // + 4 = back + count from ip + 4; the skipped bytes are known equal)
-        uint32_t back = 0;
-        if (maxb) {
-            for (;;) {
-                const uint64_t fm = ballot(!beq);
-                if (fm) { back += (uint32_t)(__ffsll((long long)fm) - 1); break; }
-                back += 64;
-                if (back >= maxb) { back = maxb; break; }
-                const uint32_t kb = back + L + 1;
-                const bool on = kb <= maxb;
-                beq = on && s[on ? ip - kb : 0u] == s[on ? cd - kb : 0u];
-            }
-        }
-        uint32_t mc;
-        {
-            const uint32_t rel = 4 * L - 4;
-            const uint32_t x = cw ^ iw;
-            uint32_t e = min(x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u, lim - rel);
-            e = (L != 0 && rel < lim) ? e : 0u;
-            const uint64_t nf = ballot(L != 0 && e < 4);
-            if (nf) {
-                const int f = __ffsll((long long)nf) - 1;
-                mc = 4 * (uint32_t)(f - 1) + rdlane(e, f);
-            } else {
-                mc = 252;
-                for (;;) {   // long match: 256 bytes per round
-                    const uint32_t r2 = mc + 4 * L;
-                    const uint32_t a2 = ip + kMinMatch + r2, c2 = cd + kMinMatch + r2;
-                    const uint32_t x2 = gld4u(s + (a2 < last4 ? a2 : last4)) ^ gld4u(s + (c2 < last4 ? c2 : last4));
-                    uint32_t e2 = min(x2 ? ((uint32_t)__builtin_ctz(x2) >> 3) : 4u, lim - r2);
-                    e2 = r2 < lim ? e2 : 0u;
-                    const uint64_t nf2 = ballot(e2 < 4);
-                    if (nf2) {
-                        const int f = __ffsll((long long)nf2) - 1;
-                        mc += 4 * (uint32_t)f + rdlane(e2, f);
-                        break;
-                    }
-                    mc += 256;
-                }
-            }
-        }
-        STAMP_ADD(7, ts);
-        // ---- emit: token | lit ext | literals | offset | ml ext
-        const uint32_t mcf = mc + back;
-        const uint32_t lit = lit0 - back;
-        const uint32_t litExt = ext_len(lit), mlExt = ext_len(mcf);
-        if (limited) {
-            if (!wasTest && op + 1 + lit + 8 + lit / 255 > cap) return 0;
-            if (op + 1 + litExt + lit + 2 + 6 + (mcf + 240) / 255 > cap) return 0;
-        }
-        {
-            pe.off = ip - cd;
-            pe.token = ((lit < 15 ? lit : 15) << 4) | (mcf < 15 ? mcf : 15);
-            pe.litRem = lit >= 15 ? (lit - 15) % 255 : 0u;
-            pe.mlRem = mcf >= 15 ? (mcf - 15) % 255 : 0u;
-            pe.litExt = litExt;
-            pe.lit = lit;
-            pe.a1 = 1 + litExt;
-            pe.a2 = pe.a1 + lit;
-            pe.total = pe.a2 + 2 + mlExt;
-            pe.op = op;
-            pe.anchor = anchor;
-            // lbo (loaded for lit0) is still each output lane's literal after a
-            // catch-up unless the literal-length extension changed size
-            pe.direct = pe.total <= 64 && litExt == ext_len(lit0);
-            peLb = lb;
-            peLbo = lbo;
-            asm volatile("" : "+v"(peLb), "+v"(peLbo));   // settle them here, not under the next round trip
-            havePe = true;
-            op += pe.total;
-        }
-        STAMP_ADD(8, ts);
-        const uint32_t ipe = ip + kMinMatch + mc;
-        anchor = ipe;
-        if (ipe >= mflimitP1) break;
-        hasIns = 1; hasTest = 1; insPos = ipe - 2; testPos = ipe; sPos = ipe + 1; k0 = 0;
-    }
-    if (havePe) {
-        if (pe.direct) store_seq_direct(pe, peLbo, d);
-        else store_seq(pe, peLb, s, d);
-    }
-    // ---- last literals
-    {
-        const uint32_t run = n - anchor;
-        if (limited && op + run + 1 + (run + 240) / 255 > cap) return 0;
-        const uint32_t ext = ext_len(run), rem = run >= 15 ? (run - 15) % 255 : 0u;
-        if (L == 0) d[op] = (uint8_t)((run < 15 ? run : 15) << 4);
-        for (uint32_t x = L; x < ext; x += 64) d[op + 1 + x] = (uint8_t)(x + 1 < ext ? 255u : rem);
-        op += 1 + ext;
-        for (uint32_t x = L; x < run; x += 64) d[op + x] = s[anchor + x];
-        op += run;
-    }
-    return (int32_t)op;
-}
-
 // ---------------------------------------------------------------------------
 // Encoder v5: the frame path's encoder for 65547 <= n <= 4 MiB (same parse
-// and bytes as encode_block / encode_block_t, LZ4 1.9.3 SURVEY.md App. A),
+// and bytes as encode_block, LZ4 1.9.3 SURVEY.md App. A),
 // laid out for the fewest instructions per window:
 //   * fixed lane roles: lane 0 INSERT, lane 1 TEST, lanes 2..63 SEARCH
 //     probes k0 .. k0+61 (step 1 for the first 64 probes: p = sPos + L - 2)
@@ -1267,7 +985,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
 //   [0, 16 KiB)          hash table (4096 x u32, or 8192 x u16)
 //   [16 KiB, 17 KiB)     dedup scratch (encode_block) / dummy slots (v5)
 //   [17 KiB, 20 KiB)     encode_block: 2 KiB source ring + 1 KiB output ring;
-//                        encode_block_t / v5: 2 KiB + 64 B mirrored source ring
+//                        v5: 2 KiB + 64 B mirrored source ring
 #define ENCODE_LDS                                                     \
     __shared__ __attribute__((aligned(16))) uint32_t ELDS[5120];       \
     uint32_t* const T = ELDS;                                          \
@@ -1294,11 +1012,7 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
     if (n < (uint32_t)kLimit64K)
         r = encode_block<true, false, false>(s, n, d, cap, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
     else if (n <= (1u << kPosBits))
-#ifdef LZ4MT_ENC_T
-        r = encode_block_t<false>(s, n, d, cap, Tl, Sl, Xl, nullptr);
-#else
         r = encode_block_v5<false, false>(s, n, d, cap, Tl, Xl, nullptr);
-#endif
     else
         r = encode_block<false, false, false>(s, n, d, cap, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
     if (laneid() == 0) csize[b] = r;
@@ -1321,11 +1035,7 @@ __global__ void __launch_bounds__(64) k_encode_stats(const uint8_t* __restrict__
     if (n < (uint32_t)kLimit64K)
         r = encode_block<true, false, true>(s, n, d, n, (l_u32*)T, (l_u8*)S, (l_u32*)Xl, Xl + kRingE, acc);
     else if (n <= (1u << kPosBits))
-#ifdef LZ4MT_ENC_T
-        r = encode_block_t<true>(s, n, d, n, (l_u32*)T, (l_u8*)S, Xl, acc);
-#else
         r = encode_block_v5<true, false>(s, n, d, n, (l_u32*)T, Xl, acc);
-#endif
     else
         r = encode_block<false, false, true>(s, n, d, n, (l_u32*)T, (l_u8*)S, (l_u32*)Xl, Xl + kRingE, acc);
     if (laneid() == 0) {
