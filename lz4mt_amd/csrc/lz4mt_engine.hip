@@ -289,7 +289,29 @@ struct DecodeBuffers {
     ~DecodeBuffers() { release(); }
     WalkScratch ws{};
     uint64_t wsChunks = 0, wsCap = 0, wsNodes = 0;
+    // second stream for the block checksums, which run beside the decode
+    // (they only read the frame; 2 KiB of LDS per wave still fits next to
+    // eight 19.7 KiB decode waves on a CU)
+    hipStream_t aux = nullptr;
+    hipEvent_t evRecs = nullptr, evSums = nullptr;
+    bool aux_ready() {
+        if (aux) return true;
+        if (hipStreamCreateWithFlags(&aux, hipStreamNonBlocking) != hipSuccess) { aux = nullptr; return false; }
+        if (hipEventCreateWithFlags(&evRecs, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&evSums, hipEventDisableTiming) != hipSuccess) {
+            release_aux();
+            return false;
+        }
+        return true;
+    }
+    void release_aux() {
+        if (aux) { hipStreamSynchronize(aux); hipStreamDestroy(aux); }
+        if (evRecs) hipEventDestroy(evRecs);
+        if (evSums) hipEventDestroy(evSums);
+        aux = nullptr; evRecs = nullptr; evSums = nullptr;
+    }
     void release() {
+        release_aux();
         hipFree(recs); hipFree(digest); hipFree(dsize); hipFree(status); hipFree(info); hipFree(ssum);
         recs = nullptr; digest = nullptr; dsize = nullptr; status = nullptr; info = nullptr; ssum = nullptr; cap = 0;
         release_walk();
@@ -361,7 +383,7 @@ Lz4MtResult walk_frame(const uint8_t* frame, uint64_t frameSize, uint64_t bodyPo
     const char* fe = getenv("LZ4MT_AMD_WALK");
     const int force = !fe ? 0 : (strcmp(fe, "serial") == 0 ? 1 : (strcmp(fe, "parallel") == 0 ? 2 : 0));
     const bool autoPar = bm <= (1u << 20) && frameSize - bodyPos >= (64ull << 20);
-    const bool par = frameSize < (1ull << 40) && (force == 2 || (force == 0 && autoPar));
+    const bool par = frameSize < (1ull << 40) && frameSize >= bodyPos + 8 && (force == 2 || (force == 0 && autoPar));
     for (int attempt = 0; attempt < 2; ++attempt) {
         if (!B.ensure(guess)) return LZ4MT_RESULT_ERROR;
         wi.result = -1;
@@ -489,9 +511,17 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
             targetCap = std::min<uint64_t>(room, nb * bm);
         }
         g_timing.mark(1, st);
+        const bool aux = bck && B.aux_ready();   // block checksums beside the decode
+        if (aux) {
+            HIPCHK(hipEventRecord(B.evRecs, st));
+            HIPCHK(hipStreamWaitEvent(B.aux, B.evRecs, 0));
+            HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, B.aux));
+            HIPCHK(hipEventRecord(B.evSums, B.aux));
+        }
         HIPCHK(launch_decode(f, B.recs, (uint32_t)nb, bm, target, targetCap, B.dsize, st));
         g_timing.mark(2, st);
-        if (bck) HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, st));
+        if (bck && !aux) HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, st));
+        if (aux) HIPCHK(hipStreamWaitEvent(st, B.evSums, 0));
         HIPCHK(launch_block_verify(B.recs, (uint32_t)nb, B.digest, B.dsize, bm, bck, B.status, st));
         g_timing.mark(3, st);
         std::vector<int32_t> ds(nb), stv(nb);
