@@ -44,6 +44,17 @@ struct WalkScratch {
     uint32_t* P;         // maxBlocks + 1 (path)
 };
 
+// A side stream + two events (per thread, re-made when the device changes)
+// for work that can run beside the main stream.
+struct AuxStream {
+    hipStream_t st = nullptr;
+    hipEvent_t evIn = nullptr, evOut = nullptr;
+    int dev = -1;
+    bool ensure();
+    void release();
+    ~AuxStream() { release(); }
+};
+
 // ---- kernel launchers (lz4mt_kernels.hip) ----
 hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                          uint8_t* slots, uint64_t slotStride, uint32_t capOverride, int32_t* csize,
@@ -63,6 +74,11 @@ hipError_t launch_frame_assemble(const uint8_t* src, const uint8_t* slots, uint6
                                  uint32_t nBlocks, const int32_t* csize, const uint32_t* bsum,
                                  const uint64_t* recOff, int blockChecksum, uint8_t* frame, uint32_t hdrLen,
                                  hipStream_t st);
+// blockChecksum for launch_frame_assemble: 0 none, 1 write the words, 2 leave
+// them to launch_frame_sums
+hipError_t launch_frame_sums(const int32_t* csize, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                             const uint32_t* bsum, const uint64_t* recOff, uint8_t* frame, uint32_t hdrLen,
+                             hipStream_t st);
 hipError_t launch_frame_finalize(uint8_t* frame, const uint8_t* hdr, uint32_t hdrLen, const uint64_t* recOff,
                                  uint32_t nBlocks, const uint32_t* streamSum, uint64_t* frameSize,
                                  hipStream_t st);

@@ -119,20 +119,58 @@ namespace lz4mt {
 // Compresses nb blocks (block b = src[b*bm, ...), last block short) into a
 // frame BODY (records only) at `body`; total body size written to
 // d_bodySize.  Used by the frame call and by the batched DEVICE mode.
+// With an AuxStream the block checksums run on it, beside the scan and the
+// assembly (both only read the encoded slots); the checksum words are
+// written once both are done.
 Lz4MtResult device_compress_body(const uint8_t* src, uint64_t n, uint32_t bm, int blockChecksum, uint8_t* ws,
-                                 uint8_t* body, uint32_t hdrLen, hipStream_t st, uint64_t** d_recOffOut) {
+                                 uint8_t* body, uint32_t hdrLen, hipStream_t st, uint64_t** d_recOffOut,
+                                 const AuxStream* aux) {
     const uint64_t nb = (n + bm - 1) / bm;
     CompressWs w = carve_compress(ws, nb, bm);
     g_timing.mark(0, st);
     HIPCHK(launch_encode(src, n, bm, (uint32_t)nb, w.slots, bm, 0xFFFFFFFFu, w.csize, st));
     g_timing.mark(1, st);
-    if (blockChecksum) HIPCHK(launch_xxh32_stored(src, w.slots, n, bm, (uint32_t)nb, w.csize, w.bsum, st));
+    const bool side = blockChecksum && aux && aux->st;
+    if (side) {
+        HIPCHK(hipEventRecord(aux->evIn, st));
+        HIPCHK(hipStreamWaitEvent(aux->st, aux->evIn, 0));
+        HIPCHK(launch_xxh32_stored(src, w.slots, n, bm, (uint32_t)nb, w.csize, w.bsum, aux->st));
+        HIPCHK(hipEventRecord(aux->evOut, aux->st));
+    } else if (blockChecksum) {
+        HIPCHK(launch_xxh32_stored(src, w.slots, n, bm, (uint32_t)nb, w.csize, w.bsum, st));
+    }
     g_timing.mark(2, st);
     HIPCHK(launch_frame_scan(w.csize, n, bm, (uint32_t)nb, blockChecksum, w.recOff, st));
-    HIPCHK(launch_frame_assemble(src, w.slots, n, bm, (uint32_t)nb, w.csize, w.bsum, w.recOff, blockChecksum, body,
-                                 hdrLen, st));
+    HIPCHK(launch_frame_assemble(src, w.slots, n, bm, (uint32_t)nb, w.csize, w.bsum, w.recOff,
+                                 side ? 2 : blockChecksum, body, hdrLen, st));
+    if (side) {
+        HIPCHK(hipStreamWaitEvent(st, aux->evOut, 0));
+        HIPCHK(launch_frame_sums(w.csize, n, bm, (uint32_t)nb, w.bsum, w.recOff, body, hdrLen, st));
+    }
     if (d_recOffOut) *d_recOffOut = w.recOff;
     return LZ4MT_RESULT_OK;
+}
+
+bool AuxStream::ensure() {
+    int d = -1;
+    if (hipGetDevice(&d) != hipSuccess) return false;
+    if (st && d == dev) return true;
+    release();
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) { st = nullptr; return false; }
+    if (hipEventCreateWithFlags(&evIn, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&evOut, hipEventDisableTiming) != hipSuccess) {
+        release();
+        return false;
+    }
+    dev = d;
+    return true;
+}
+
+void AuxStream::release() {
+    if (st) { hipStreamSynchronize(st); hipStreamDestroy(st); }
+    if (evIn) hipEventDestroy(evIn);
+    if (evOut) hipEventDestroy(evOut);
+    st = nullptr; evIn = nullptr; evOut = nullptr; dev = -1;
 }
 
 uint64_t compress_ws_bytes(uint64_t n, uint32_t bm) { return carve_compress(nullptr, (n + bm - 1) / bm, bm).bytes; }
@@ -223,8 +261,10 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
     uint8_t hdr[kMaxHeader];
     const int hdrLen = build_header(sd, hdr);
     uint64_t* recOff = nullptr;
+    thread_local AuxStream aux;
     const Lz4MtResult r = device_compress_body(static_cast<const uint8_t*>(d_src), srcSize, bm, sd->flg.blockChecksum,
-                                               ws, static_cast<uint8_t*>(d_frame), (uint32_t)hdrLen, st, &recOff);
+                                               ws, static_cast<uint8_t*>(d_frame), (uint32_t)hdrLen, st, &recOff,
+                                               aux.ensure() ? &aux : nullptr);
     if (r != LZ4MT_RESULT_OK) return r;
     CompressWs w = carve_compress(ws, (srcSize + bm - 1) / bm, bm);
     if (sd->flg.streamChecksum)

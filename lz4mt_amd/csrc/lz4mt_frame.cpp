@@ -42,7 +42,8 @@
 
 namespace lz4mt {
 Lz4MtResult device_compress_body(const uint8_t* src, uint64_t n, uint32_t bm, int blockChecksum, uint8_t* ws,
-                                 uint8_t* body, uint32_t hdrLen, hipStream_t st, uint64_t** d_recOffOut);
+                                 uint8_t* body, uint32_t hdrLen, hipStream_t st, uint64_t** d_recOffOut,
+                                 const AuxStream* aux);
 uint64_t compress_ws_bytes(uint64_t n, uint32_t bm);
 }  // namespace lz4mt
 
@@ -511,7 +512,7 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
         uint64_t* dRecOff = nullptr;
         const uint64_t nb = (total + bm - 1) / bm;
         if (hipMemcpyAsync(S.dIn, S.hIn, total, hipMemcpyHostToDevice, S.st) != hipSuccess ||
-            device_compress_body(S.dIn, total, bm, bck, S.dWs, S.dOut, 0, S.st, &dRecOff) != LZ4MT_RESULT_OK ||
+            device_compress_body(S.dIn, total, bm, bck, S.dWs, S.dOut, 0, S.st, &dRecOff, nullptr) != LZ4MT_RESULT_OK ||
             hipMemcpyAsync(S.hMeta, dRecOff + nb, 8, hipMemcpyDeviceToHost, S.st) != hipSuccess) {
             s.quit(LZ4MT_RESULT_ERROR);
             return false;

@@ -1986,7 +1986,8 @@ __global__ void __launch_bounds__(256) k_frame_assemble(const uint8_t* __restric
     g_u8* rec = gptr(frame) + hdrLen + recOff[b];
     g_u8* D = rec + 4;
     if (t < 4) rec[t] = (uint8_t)(bits >> (8 * t));
-    if (blockChecksum && t >= 4 && t < 8) D[L + (t - 4)] = (uint8_t)(bsum[b] >> (8 * (t - 4)));
+    // blockChecksum 2: the words are written later by k_frame_sums
+    if (blockChecksum == 1 && t >= 4 && t < 8) D[L + (t - 4)] = (uint8_t)(bsum[b] >> (8 * (t - 4)));
     const uintptr_t Da = reinterpret_cast<uintptr_t>(D);
     const uintptr_t A0 = (Da + 15) & ~uintptr_t(15);
     const uintptr_t E = Da + L, E0 = E & ~uintptr_t(15);
@@ -2044,6 +2045,32 @@ hipError_t launch_frame_assemble(const uint8_t* src, const uint8_t* slots, uint6
     if (nBlocks == 0) return hipSuccess;
     hipLaunchKernelGGL(k_frame_assemble, dim3(nBlocks), dim3(256), 0, st, src, slots, srcSize, blockSize, csize, bsum,
                        recOff, blockChecksum, frame, hdrLen);
+    return hipGetLastError();
+}
+
+// block checksum words of an assembled frame (when the checksums were
+// computed beside the assembly, on another stream)
+__global__ void __launch_bounds__(256) k_frame_sums(const int32_t* __restrict__ csize, uint64_t srcSize,
+                                                    uint32_t blockSize, uint32_t nBlocks,
+                                                    const uint32_t* __restrict__ bsum,
+                                                    const uint64_t* __restrict__ recOff, uint8_t* __restrict__ frame,
+                                                    uint32_t hdrLen) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nBlocks) return;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
+    const int32_t cs = csize[b];
+    g_u8* w = gptr(frame) + hdrLen + recOff[b] + 4 + (cs > 0 ? (uint64_t)cs : n);
+    const uint32_t v = bsum[b];
+    w[0] = (uint8_t)v; w[1] = (uint8_t)(v >> 8); w[2] = (uint8_t)(v >> 16); w[3] = (uint8_t)(v >> 24);
+}
+
+hipError_t launch_frame_sums(const int32_t* csize, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                             const uint32_t* bsum, const uint64_t* recOff, uint8_t* frame, uint32_t hdrLen,
+                             hipStream_t st) {
+    if (nBlocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_frame_sums, dim3((nBlocks + 255) / 256), dim3(256), 0, st, csize, srcSize, blockSize, nBlocks,
+                       bsum, recOff, frame, hdrLen);
     return hipGetLastError();
 }
 
