@@ -329,29 +329,7 @@ struct DecodeBuffers {
     ~DecodeBuffers() { release(); }
     WalkScratch ws{};
     uint64_t wsChunks = 0, wsCap = 0, wsNodes = 0;
-    // second stream for the block checksums, which run beside the decode
-    // (they only read the frame; 2 KiB of LDS per wave still fits next to
-    // eight 19.7 KiB decode waves on a CU)
-    hipStream_t aux = nullptr;
-    hipEvent_t evRecs = nullptr, evSums = nullptr;
-    bool aux_ready() {
-        if (aux) return true;
-        if (hipStreamCreateWithFlags(&aux, hipStreamNonBlocking) != hipSuccess) { aux = nullptr; return false; }
-        if (hipEventCreateWithFlags(&evRecs, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&evSums, hipEventDisableTiming) != hipSuccess) {
-            release_aux();
-            return false;
-        }
-        return true;
-    }
-    void release_aux() {
-        if (aux) { hipStreamSynchronize(aux); hipStreamDestroy(aux); }
-        if (evRecs) hipEventDestroy(evRecs);
-        if (evSums) hipEventDestroy(evSums);
-        aux = nullptr; evRecs = nullptr; evSums = nullptr;
-    }
     void release() {
-        release_aux();
         hipFree(recs); hipFree(digest); hipFree(dsize); hipFree(status); hipFree(info); hipFree(ssum);
         recs = nullptr; digest = nullptr; dsize = nullptr; status = nullptr; info = nullptr; ssum = nullptr; cap = 0;
         release_walk();
@@ -551,17 +529,13 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
             targetCap = std::min<uint64_t>(room, nb * bm);
         }
         g_timing.mark(1, st);
-        const bool aux = bck && B.aux_ready();   // block checksums beside the decode
-        if (aux) {
-            HIPCHK(hipEventRecord(B.evRecs, st));
-            HIPCHK(hipStreamWaitEvent(B.aux, B.evRecs, 0));
-            HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, B.aux));
-            HIPCHK(hipEventRecord(B.evSums, B.aux));
-        }
+        // (the block checksums stay behind the decode on the same stream: run
+        // beside it, a checksum wave that lands first on a CU takes the LDS
+        // of one of its eight 20 KiB decode waves, and the decode then needs a
+        // second round -- 54 ms instead of 30 in one measured run)
         HIPCHK(launch_decode(f, B.recs, (uint32_t)nb, bm, target, targetCap, B.dsize, st));
         g_timing.mark(2, st);
-        if (bck && !aux) HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, st));
-        if (aux) HIPCHK(hipStreamWaitEvent(st, B.evSums, 0));
+        if (bck) HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, st));
         HIPCHK(launch_block_verify(B.recs, (uint32_t)nb, B.digest, B.dsize, bm, bck, B.status, st));
         g_timing.mark(3, st);
         std::vector<int32_t> ds(nb), stv(nb);
