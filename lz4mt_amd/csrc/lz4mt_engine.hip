@@ -261,10 +261,14 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
     uint8_t hdr[kMaxHeader];
     const int hdrLen = build_header(sd, hdr);
     uint64_t* recOff = nullptr;
+    // side stream for the block checksums, except while `st` is being
+    // captured into a graph (no stream creation inside a capture)
     thread_local AuxStream aux;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    const bool capturing = hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone;
     const Lz4MtResult r = device_compress_body(static_cast<const uint8_t*>(d_src), srcSize, bm, sd->flg.blockChecksum,
                                                ws, static_cast<uint8_t*>(d_frame), (uint32_t)hdrLen, st, &recOff,
-                                               aux.ensure() ? &aux : nullptr);
+                                               !capturing && aux.ensure() ? &aux : nullptr);
     if (r != LZ4MT_RESULT_OK) return r;
     CompressWs w = carve_compress(ws, (srcSize + bm - 1) / bm, bm);
     if (sd->flg.streamChecksum)
