@@ -305,7 +305,7 @@ int env_int(const char* name, int dflt, int lo, int hi) {
 }
 // Pipeline shape per direction.  An encode batch of any size takes about one
 // block latency (~150-190 ms for 4 MiB blocks), so compress
-// needs GiBs in flight to approach the kernel rate: 4 slots of up to 2 GiB.
+// needs GiBs in flight to approach the kernel rate: 4 slots of up to 4 GiB.
 // Decode latency is ~6x shorter: 8 slots of up to 1 GiB.  Batches start at
 // 256 MiB and double per fill, so small inputs stage little.
 struct PipeShape {
@@ -313,13 +313,15 @@ struct PipeShape {
     uint64_t maxBatch;   // bytes of uncompressed data per batch
 };
 PipeShape pipe_shape(bool compress) {
-    const int dS = compress ? 4 : 8, dM = compress ? 2048 : 1024;
+    const int dS = compress ? 4 : 8, dM = compress ? 4096 : 1024;
     return PipeShape{env_int("LZ4MT_AMD_SLOTS", dS, 1, kSlots),
                      (uint64_t)env_int("LZ4MT_AMD_BATCH_MIB", dM, 1, 16384) << 20};
 }
-// blocks of batch number `i` (0, 1, ...): 256 MiB << i, capped, >= 1 block
+// blocks of batch number `i` (0, 1, ...): first << i, capped, >= 1 block
+// (first = 256 MiB, LZ4MT_AMD_BATCH0_MIB overrides)
 uint64_t batch_blocks(const PipeShape& P, uint32_t bm, uint64_t i) {
-    const uint64_t want = std::min<uint64_t>(P.maxBatch, (256ull << 20) << std::min<uint64_t>(i, 8));
+    const uint64_t first = (uint64_t)env_int("LZ4MT_AMD_BATCH0_MIB", 256, 1, 16384) << 20;
+    const uint64_t want = std::min<uint64_t>(P.maxBatch, first << std::min<uint64_t>(i, 16));
     return std::max<uint64_t>(1, want / bm);
 }
 
