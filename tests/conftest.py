@@ -34,3 +34,14 @@ def golden_inputs(golden):
 @pytest.fixture(scope="session")
 def decode_blob():
     return read_golden("decode_blocks.bin")
+
+
+def with_stream_size(frame, n):
+    """The same frame with FLG.3 set and the u64 content size in the header
+    (src/lz4mt.cpp:335-369: magic, FLG, BD, [size], HC over FLG..size)."""
+    import struct
+    import xxhash
+    flg, bd = frame[4] | 0x08, frame[5]
+    desc = bytes([flg, bd]) + struct.pack("<Q", n)
+    hc = (xxhash.xxh32(desc, seed=0).intdigest() >> 8) & 0xFF
+    return frame[:4] + desc + bytes([hc]) + frame[7:]

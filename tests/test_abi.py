@@ -17,7 +17,7 @@ import subprocess
 
 import pytest
 
-from conftest import ROOT, read_golden
+from conftest import ROOT, read_golden, with_stream_size
 
 import lz4mt_amd as L
 from lz4mt_amd import _abi
@@ -227,3 +227,19 @@ def test_large_transfers_through_io_bindings(tmp_path):
         assert wr(ctypes.byref(ctx), ctypes.cast(buf, ctypes.c_void_p), n) == n
     assert io.eof == 1 and io.inPos == len(data) and io.outPos == len(data)
     assert outb.raw[:len(data)] == data
+
+
+@pytest.mark.parametrize("mode", [L.MODE_SEQUENTIAL, L.MODE_PARALLEL])
+def test_host_engine_stream_size_field(golden_inputs, cpu_codec, mode):
+    """FLG.3 (content size): header written as the reference does, frame
+    decodes and reports the size back in the descriptor."""
+    comp, decomp = cpu_codec
+    data = golden_inputs["text20k"]
+    plain = L.compress(data, L.make_sd(7, True, True), mode=mode, compress_cb=comp)[1]
+    sd = L.make_sd(7, True, True)
+    sd.flg.streamSize = 1
+    sd.streamSize = len(data)
+    r, frame = L.compress(data, sd, mode=mode, compress_cb=comp)
+    assert r == 0 and frame == with_stream_size(plain, len(data))
+    r, out, sd2 = L.decompress(frame, len(data) + 64, mode=mode, decompress_cb=decomp)
+    assert r == 0 and out == data and sd2.flg.streamSize == 1 and sd2.streamSize == len(data)

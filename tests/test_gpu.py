@@ -16,7 +16,7 @@ import torch
 import xxhash
 
 import oracle
-from conftest import read_golden
+from conftest import read_golden, with_stream_size
 
 pytestmark = pytest.mark.gpu
 
@@ -327,3 +327,21 @@ def test_compress_frame_async_in_hip_graph(golden_inputs):
     g.replay()
     torch.cuda.synchronize()
     assert host(frame[:int(fsz[0].item())]) == want
+
+
+def test_frame_engine_stream_size_field(golden_inputs):
+    """FLG.3 through the device frame engine and the DEVICE host mode: same
+    header as the reference writes (size + HC), same body, size reported back."""
+    data = golden_inputs["syn300k"]
+    plain = host(L.compress_frame(dev(data), L.make_sd(5, False, True)))
+    sd = L.make_sd(5, False, True)
+    sd.flg.streamSize = 1
+    sd.streamSize = len(data)
+    want = with_stream_size(plain, len(data))
+    assert host(L.compress_frame(dev(data), sd)) == want
+    r, frame = L.compress(data, sd, mode=L.MODE_DEVICE)
+    assert r == 0 and frame == want
+    out, r = L.decompress_frame(dev(want))
+    assert r == 0 and host(out) == data
+    r, out2, sd2 = L.decompress(want, len(data) + 64, mode=L.MODE_DEVICE)
+    assert r == 0 and out2 == data and sd2.flg.streamSize == 1 and sd2.streamSize == len(data)
