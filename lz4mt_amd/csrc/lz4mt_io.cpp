@@ -145,6 +145,12 @@ bool regular(FILE* fp) {
     struct stat st;
     return fstat(fileno(fp), &st) == 0 && S_ISREG(st.st_mode);
 }
+// positional writes only where they land where fwrite would: not on
+// O_APPEND descriptors (Linux appends every pwrite there, in any order)
+bool positional_out(FILE* fp) {
+    const int fl = fcntl(fileno(fp), F_GETFL);
+    return fl != -1 && !(fl & O_APPEND) && regular(fp);
+}
 
 FILE* in_fp(const Lz4MtContext* c) { return static_cast<FILE*>(c->readCtx); }
 FILE* out_fp(const Lz4MtContext* c) { return static_cast<FILE*>(c->writeCtx); }
@@ -218,7 +224,7 @@ extern "C" int lz4mtIoWrite(const Lz4MtContext* ctx, const void* src, int srcSiz
     if (is_null_sink(ctx)) return srcSize;
     FILE* fp = out_fp(ctx);
     if (!fp) return 0;
-    if (srcSize >= (int)kParMin && regular(fp) && fflush(fp) == 0) {   // parallel pwrite at the position
+    if (srcSize >= (int)kParMin && positional_out(fp) && fflush(fp) == 0) {   // parallel pwrite at the position
         const off_t off = ftello(fp);
         if (off >= 0) {
             const size_t put = par_pio(fileno(fp), const_cast<void*>(src), (size_t)srcSize, off, true);

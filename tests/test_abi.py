@@ -243,3 +243,27 @@ def test_host_engine_stream_size_field(golden_inputs, cpu_codec, mode):
     assert r == 0 and frame == with_stream_size(plain, len(data))
     r, out, sd2 = L.decompress(frame, len(data) + 64, mode=mode, decompress_cb=decomp)
     assert r == 0 and out == data and sd2.flg.streamSize == 1 and sd2.streamSize == len(data)
+
+
+def test_large_writes_to_append_mode_file(tmp_path):
+    """An O_APPEND output (a caller's own FILE*) keeps fwrite order: large
+    writes are not split into positional pieces there."""
+    import random
+    rnd = random.Random(3)
+    base = bytes(rnd.getrandbits(8) for _ in range(1 << 12))
+    chunks = [bytes([i]) + base * (3072 + i) for i in range(6)]   # 12+ MiB each: split into 8 pieces if positional
+    dst = tmp_path / "out.bin"
+    dst.write_bytes(b"head")
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = ctypes.c_void_p
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fclose.argtypes = [ctypes.c_void_p]
+    fp = libc.fopen(str(dst).encode(), b"ab")
+    assert fp
+    ctx = L.init_context()
+    L.lib.lz4mtIoBindCstdio(ctypes.byref(ctx))
+    ctx.writeCtx = fp
+    for c in chunks:
+        assert L.lib.lz4mtIoWrite(ctypes.byref(ctx), c, len(c)) == len(c)
+    libc.fclose(fp)
+    assert dst.read_bytes() == b"head" + b"".join(chunks)
