@@ -345,3 +345,37 @@ def test_frame_engine_stream_size_field(golden_inputs):
     assert r == 0 and host(out) == data
     r, out2, sd2 = L.decompress(want, len(data) + 64, mode=L.MODE_DEVICE)
     assert r == 0 and out2 == data and sd2.flg.streamSize == 1 and sd2.streamSize == len(data)
+
+
+def test_block_decompress_fuzz_vs_oracle(golden_inputs):
+    """Randomly damaged blocks (flipped bytes, truncations, appended or
+    removed ranges) under several output caps: the GPU operator returns the
+    same value as LZ4_decompress_safe 1.9.3 (the oracle; negative error
+    positions included) and the same bytes when it succeeds."""
+    rnd = random.Random(2024)
+    syn = golden_inputs["syn300k"]
+    srcs = [syn[:65536], syn[100_000:300_000], golden_inputs["text20k"],
+            oracle.gen_random(5000, 3) + golden_inputs["zeros300k"][:50_000]]
+    blocks = [oracle.compress_block(s, len(s) + len(s) // 255 + 16) for s in srcs]
+    for it in range(2000):
+        i = rnd.randrange(len(blocks))
+        blk = bytearray(blocks[i])
+        n = len(srcs[i])
+        kind = rnd.randrange(5)
+        if kind == 0:
+            for _ in range(rnd.randrange(1, 5)):
+                blk[rnd.randrange(len(blk))] = rnd.randrange(256)
+        elif kind == 1:
+            del blk[rnd.randrange(1, len(blk)):]
+        elif kind == 2:
+            blk += bytes(rnd.randrange(256) for _ in range(rnd.randrange(1, 40)))
+        elif kind == 3:
+            a = rnd.randrange(len(blk) - 1)
+            del blk[a:a + rnd.randrange(1, 64)]
+        else:
+            a = rnd.randrange(len(blk) - 2)
+            blk[a:a + 2] = rnd.randrange(65536).to_bytes(2, "little")
+        cap = rnd.choice([n, n - 1, n + 100, max(1, n // 2), 4 << 20])
+        got = L.decompress_block(bytes(blk), cap)
+        want = oracle.decompress_block(bytes(blk), cap)
+        assert got == want, (it, i, kind, cap, got[0], want[0])
