@@ -379,3 +379,33 @@ def test_block_decompress_fuzz_vs_oracle(golden_inputs):
         got = L.decompress_block(bytes(blk), cap)
         want = oracle.decompress_block(bytes(blk), cap)
         assert got == want, (it, i, kind, cap, got[0], want[0])
+
+
+@pytest.mark.parametrize("bid,sck,bck", [(4, True, True), (5, False, True), (7, True, False)])
+def test_frame_decompress_fuzz_vs_oracle(golden_inputs, bid, sck, bck):
+    """Randomly damaged frames through lz4mtHipDecompressFrame: the same
+    Lz4MtResult as the oracle's restatement of lz4mt's decompress()
+    (src/lz4mt.cpp:593-734, 938-1011), and the same bytes when it succeeds."""
+    data = golden_inputs["syn300k"] + golden_inputs["random100k"] + golden_inputs["zeros300k"][:70_000]
+    f = oracle.compress_frame(data, oracle.params(bid, sck, bck))
+    rnd = random.Random(bid * 100 + sck * 10 + bck)
+    cap = len(data) + (4 << 20)
+    for it in range(150):
+        b = bytearray(f)
+        kind = rnd.randrange(4)
+        if kind == 0:
+            for _ in range(rnd.randrange(1, 4)):
+                b[rnd.randrange(len(b))] ^= 1 << rnd.randrange(8)
+        elif kind == 1:
+            del b[rnd.randrange(4, len(b)):]
+        elif kind == 2:
+            a = rnd.randrange(7, len(b) - 4)
+            b[a:a + 4] = rnd.randrange(1 << 32).to_bytes(4, "little")
+        else:
+            b += bytes(rnd.randrange(256) for _ in range(rnd.randrange(1, 12)))
+        out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+        o, r = L.decompress_frame(dev(bytes(b)), out=out, check=False)
+        rw, ow = oracle.decompress_frame(bytes(b), cap)
+        assert r == rw, (it, kind, L.result_to_string(r), L.result_to_string(rw))
+        if r == 0:
+            assert host(o) == ow, (it, kind)
