@@ -582,7 +582,16 @@ int orc_frame_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t outC
         parallel_for(nb, nthreads, djob_fn, jobs);
         size_t w = frameOut;
         for (size_t i = 0; i < nb; i++) {
-            if (jobs[i].res != R_OK) { if (result == R_OK || result == R_ERROR) result = jobs[i].res; break; }
+            if (jobs[i].res != R_OK) {
+                /* a checksum mismatch is found after the block was written
+                   (ref src/lz4mt.cpp:665-681); a decode failure before */
+                if (jobs[i].res == R_BCK) {
+                    if (dst + w != jobs[i].out) memmove(dst + w, jobs[i].out, (size_t)jobs[i].dsz);
+                    w += (size_t)jobs[i].dsz;
+                }
+                if (result == R_OK || result == R_ERROR) result = jobs[i].res;
+                break;
+            }
             if (dst + w != jobs[i].out) memmove(dst + w, jobs[i].out, (size_t)jobs[i].dsz);
             w += (size_t)jobs[i].dsz;
         }

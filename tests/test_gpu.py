@@ -409,3 +409,34 @@ def test_frame_decompress_fuzz_vs_oracle(golden_inputs, bid, sck, bck):
         assert r == rw, (it, kind, L.result_to_string(r), L.result_to_string(rw))
         if r == 0:
             assert host(o) == ow, (it, kind)
+
+
+@pytest.mark.parametrize("mode", ["DEVICE", "PARALLEL"])
+def test_callback_decompress_fuzz_vs_oracle(golden_inputs, mode):
+    """The same damaged frames through lz4mtDecompress (callback API) in DEVICE
+    and PARALLEL modes: the oracle's result code, and its bytes on success.
+    What was written before an error is compared for DEVICE only: every block
+    before the failing one, plus the failing block itself on a checksum
+    mismatch (written before the check, src/lz4mt.cpp:665-681).  The
+    reference's PARALLEL mode races there (tasks started after the quit skip
+    their write), so only its result code is pinned."""
+    m = {"DEVICE": L.MODE_DEVICE, "PARALLEL": L.MODE_PARALLEL}[mode]
+    data = golden_inputs["syn300k"] + golden_inputs["random100k"]
+    f = oracle.compress_frame(data, oracle.params(4, True, True))
+    rnd = random.Random(77 if mode == "DEVICE" else 78)
+    cap = len(data) + (1 << 20)
+    for it in range(60):
+        b = bytearray(f)
+        kind = rnd.randrange(3)
+        if kind == 0:
+            b[rnd.randrange(len(b))] ^= 1 << rnd.randrange(8)
+        elif kind == 1:
+            del b[rnd.randrange(4, len(b)):]
+        else:
+            a = rnd.randrange(7, len(b) - 4)
+            b[a:a + 4] = rnd.randrange(1 << 32).to_bytes(4, "little")
+        r, out, _ = L.decompress(bytes(b), cap, mode=m)
+        rw, ow = oracle.decompress_frame(bytes(b), cap)
+        assert r == rw, (it, kind, L.result_to_string(r), L.result_to_string(rw))
+        if r == 0 or mode == "DEVICE":
+            assert out == ow, (it, kind, L.result_to_string(r), len(out), len(ow))
