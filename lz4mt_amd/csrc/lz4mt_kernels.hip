@@ -756,7 +756,9 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         // most once inside a window (at j = j1; never in the k0 = 0 window)
         const uint32_t j = L - 2;
         const int32_t jx = (int32_t)j - (int32_t)j1;
-        uint32_t p = sBase + j * s0 + (uint32_t)max(jx, 0);
+        // j < 62 and the step s0 < 2^24: a full-rate 24-bit multiply (lanes 0
+        // and 1 wrap j, but take the INSERT / TEST position below)
+        uint32_t p = sBase + __umul24(j, s0) + (uint32_t)max(jx, 0);
         const uint32_t step = s0 + (jx >= 0 ? 1u : 0u);
         const uint32_t sHi = sBase + 61 * s0 + (61 > j1 ? 61 - j1 : 0u);
         const bool insOn = mode != 0, testOn = mode == 1;
