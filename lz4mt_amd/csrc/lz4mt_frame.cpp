@@ -687,6 +687,18 @@ extern "C" Lz4MtStreamDescriptor lz4mtInitStreamDescriptor(void) {
     return d;
 }
 
+// The batched device engine runs for LZ4MT_MODE_DEVICE, and also for the
+// reference's default PARALLEL mode when the codec callback of that
+// direction is null -- i.e. when every block would go to this library's GPU
+// block operator one launch at a time (a relinked lz4mt caller).  Same
+// frames, same callback protocol; HC levels keep the per-block path (the
+// operator stores those blocks raw).
+bool use_device_engine(const Lz4MtContext* ctx, bool compress) {
+    if (ctx->mode & LZ4MT_MODE_DEVICE) return true;
+    if (ctx->mode != LZ4MT_MODE_PARALLEL) return false;
+    return compress ? (!ctx->compress && ctx->compressionLevel < 3) : !ctx->decompress;
+}
+
 extern "C" Lz4MtResult lz4mtCompress(Lz4MtContext* ctx, const Lz4MtStreamDescriptor* sd) {
     if (!ctx || !sd) return LZ4MT_RESULT_BAD_ARG;
     Session s(ctx);
@@ -698,7 +710,7 @@ extern "C" Lz4MtResult lz4mtCompress(Lz4MtContext* ctx, const Lz4MtStreamDescrip
     if (!ctx->write || ctx->write(ctx, hdr, hl) != hl) return s.quit(LZ4MT_RESULT_CANNOT_WRITE_HEADER);
     if (!sd->flg.blockIndependence) return s.quit(LZ4MT_RESULT_BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET);
     HostXxh32 xs(0);
-    if (ctx->mode & LZ4MT_MODE_DEVICE) compress_device(s, sd, xs);
+    if (use_device_engine(ctx, true)) compress_device(s, sd, xs);
     else compress_host(s, sd, xs);
     if (s.result() != LZ4MT_RESULT_OK) return s.result();
     if (!s.writeU32(0)) return s.quit(LZ4MT_RESULT_CANNOT_WRITE_EOS);
@@ -746,7 +758,7 @@ extern "C" Lz4MtResult lz4mtDecompress(Lz4MtContext* ctx, Lz4MtStreamDescriptor*
         if (hr != LZ4MT_RESULT_OK) { s.quit(hr); break; }
         if (!sd->flg.blockIndependence) { s.quit(LZ4MT_RESULT_BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET); break; }
         HostXxh32 xs(0);
-        const bool eos = (ctx->mode & LZ4MT_MODE_DEVICE) ? decompress_device(s, sd, xs) : decompress_host(s, sd, xs);
+        const bool eos = use_device_engine(ctx, false) ? decompress_device(s, sd, xs) : decompress_host(s, sd, xs);
         if (s.error() || s.quitting()) break;
         if (!eos) { s.quit(LZ4MT_RESULT_CANNOT_READ_BLOCK_SIZE); break; }
         if (sd->flg.streamChecksum) {

@@ -411,7 +411,7 @@ def test_frame_decompress_fuzz_vs_oracle(golden_inputs, bid, sck, bck):
             assert host(o) == ow, (it, kind)
 
 
-@pytest.mark.parametrize("mode", ["DEVICE", "PARALLEL"])
+@pytest.mark.parametrize("mode", ["DEVICE", "PARALLEL", "PARALLEL_OPS"])
 def test_callback_decompress_fuzz_vs_oracle(golden_inputs, mode):
     """The same damaged frames through lz4mtDecompress (callback API) in DEVICE
     and PARALLEL modes: the oracle's result code, and its bytes on success.
@@ -420,7 +420,10 @@ def test_callback_decompress_fuzz_vs_oracle(golden_inputs, mode):
     mismatch (written before the check, src/lz4mt.cpp:665-681).  The
     reference's PARALLEL mode races there (tasks started after the quit skip
     their write), so only its result code is pinned."""
-    m = {"DEVICE": L.MODE_DEVICE, "PARALLEL": L.MODE_PARALLEL}[mode]
+    m = {"DEVICE": L.MODE_DEVICE, "PARALLEL": L.MODE_PARALLEL, "PARALLEL_OPS": L.MODE_PARALLEL}[mode]
+    # PARALLEL with null codecs runs the device engine; with the GPU block
+    # operator set explicitly (INTEGRATION.md section 2) it runs block by block
+    ops = (lambda src, dst, n, cap: L.lib.lz4mtHipDecompressBlock(src, dst, n, cap)) if mode == "PARALLEL_OPS" else None
     data = golden_inputs["syn300k"] + golden_inputs["random100k"]
     f = oracle.compress_frame(data, oracle.params(4, True, True))
     rnd = random.Random(77 if mode == "DEVICE" else 78)
@@ -435,8 +438,8 @@ def test_callback_decompress_fuzz_vs_oracle(golden_inputs, mode):
         else:
             a = rnd.randrange(7, len(b) - 4)
             b[a:a + 4] = rnd.randrange(1 << 32).to_bytes(4, "little")
-        r, out, _ = L.decompress(bytes(b), cap, mode=m)
+        r, out, _ = L.decompress(bytes(b), cap, mode=m, decompress_cb=ops)
         rw, ow = oracle.decompress_frame(bytes(b), cap)
         assert r == rw, (it, kind, L.result_to_string(r), L.result_to_string(rw))
-        if r == 0 or mode == "DEVICE":
+        if r == 0 or mode != "PARALLEL_OPS":
             assert out == ow, (it, kind, L.result_to_string(r), len(out), len(ow))
