@@ -61,8 +61,6 @@ hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSiz
                          hipStream_t st);
 hipError_t launch_decode(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax,
                          uint8_t* out, uint64_t outCap, int32_t* dsize, hipStream_t st);
-hipError_t launch_xxh32_blocks(const uint8_t* base, const uint64_t* offs, const uint32_t* lens, uint32_t nBlocks,
-                               uint32_t* digest, hipStream_t st);
 hipError_t launch_xxh32_stored(const uint8_t* src, const uint8_t* slots, uint64_t srcSize, uint32_t blockSize,
                                uint32_t nBlocks, const int32_t* csize, uint32_t* digest, hipStream_t st);
 hipError_t launch_xxh32_frame_blocks(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t* digest,

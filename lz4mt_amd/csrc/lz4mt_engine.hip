@@ -485,6 +485,7 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
     bool seen = false;
     Lz4MtResult result = LZ4MT_RESULT_OK;
     DecodeBuffers& B = decode_cache();
+    thread_local AuxStream aux;   // block checksums beside the decode
     uint8_t* tmp = nullptr;   // staging when a frame's output is unaligned or needs compaction
     uint64_t tmpCap = 0;
     if (outSize) *outSize = 0;
@@ -532,14 +533,21 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
             target = tmp;
             targetCap = std::min<uint64_t>(room, nb * bm);
         }
+        // The block checksums run on a side stream beside the decode: the
+        // checksum kernel uses no LDS (16 blocks per wave), so its waves do
+        // not take a slot from the decode's eight 20 KiB waves per CU.
+        const bool side = bck && nb && aux.ensure();
+        if (side) {
+            HIPCHK(hipEventRecord(aux.evIn, st));
+            HIPCHK(hipStreamWaitEvent(aux.st, aux.evIn, 0));
+            HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, aux.st));
+            HIPCHK(hipEventRecord(aux.evOut, aux.st));
+        }
         g_timing.mark(1, st);
-        // (the block checksums stay behind the decode on the same stream: run
-        // beside it, a checksum wave that lands first on a CU takes the LDS
-        // of one of its eight 20 KiB decode waves, and the decode then needs a
-        // second round -- 54 ms instead of 30 in one measured run)
         HIPCHK(launch_decode(f, B.recs, (uint32_t)nb, bm, target, targetCap, B.dsize, st));
         g_timing.mark(2, st);
-        if (bck) HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, st));
+        if (side) HIPCHK(hipStreamWaitEvent(st, aux.evOut, 0));
+        else if (bck) HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, st));
         HIPCHK(launch_block_verify(B.recs, (uint32_t)nb, B.digest, B.dsize, bm, bck, B.status, st));
         g_timing.mark(3, st);
         std::vector<int32_t> ds(nb), stv(nb);
