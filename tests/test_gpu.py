@@ -443,3 +443,38 @@ def test_callback_decompress_fuzz_vs_oracle(golden_inputs, mode):
         assert r == rw, (it, kind, L.result_to_string(r), L.result_to_string(rw))
         if r == 0 or mode != "PARALLEL_OPS":
             assert out == ow, (it, kind, L.result_to_string(r), len(out), len(ow))
+
+
+# ---------------------------------------------------------------------------
+# block checksums (k_xxh32_frame_blocks: 16 blocks per wave, a lane quad per
+# block): ragged stored lengths (0-40 B and full 64 KiB), every byte
+# alignment of the payload inside the frame, block counts that are not a
+# multiple of 16; a flipped checksum word gives the oracle's result code
+# ---------------------------------------------------------------------------
+def _raw_block_frame(payloads, bad=None):
+    import struct
+    head = oracle.compress_frame(b"", oracle.params(4, False, True))[:-4]   # header only (no stream checksum)
+    out = bytearray(head)
+    for i, p in enumerate(payloads):
+        ck = xxhash.xxh32(p).intdigest() ^ (1 if i == bad else 0)
+        out += struct.pack("<I", len(p) | 0x80000000) + p + struct.pack("<I", ck)
+    out += b"\0\0\0\0"
+    return bytes(out)
+
+
+@pytest.mark.parametrize("count", [1, 15, 17, 33, 50])
+def test_block_checksums_ragged(count):
+    rnd = random.Random(count)
+    payloads = []
+    for i in range(count):
+        n = 65536 if i % 7 == 3 else rnd.randrange(1, 41)
+        payloads.append(bytes(rnd.randrange(256) for _ in range(n)) if n < 100 else os.urandom(n))
+    data = b"".join(payloads)
+    for bad in (None, count // 2):
+        fr = _raw_block_frame(payloads, bad)
+        want_r, want = oracle.decompress_frame(fr, len(data) + 64)
+        out, r = L.decompress_frame(dev(fr), check=False)
+        assert r == want_r, (count, bad, r, want_r)
+        assert (bad is not None) or host(out) == data == want
+        r2, out2, _ = L.decompress(fr, len(data) + 64, mode=L.MODE_DEVICE)
+        assert r2 == want_r and (bad is not None or out2 == data), (count, bad, r2)
