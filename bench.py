@@ -3,19 +3,32 @@
 Workload (BASELINE.json configs[1]): 8 GiB synthetic buffer per GPU
 (SURVEY.md App. F generator), 4 MiB independent blocks, -Sx -BX frames
 (block XXH32 on, serial content checksum off), compress + decompress +
-XXH32, inputs resident in HBM when the timed region starts.  One step =
-compress the buffer into one lz4mt frame, then decompress that frame (block
-checksums verified by the decoder).  At N>1 each rank owns a contiguous
-block range (its 8 GiB shard of the 8N GiB stream, weak scaling) and the
-compressed shards are gathered to rank 0 over RCCL (the only exchange step
-the path has); decompression is sharded with no collective.  The gather is
-enqueued before the local decompress and runs over xGMI while each rank
-decodes its own shard (both only read the compressed frame), so at N>1
-compress_GiBps covers the encode and decompress_GiBps the decode + gather.
+XXH32, inputs resident in HBM when the timed region starts.
 
-Prints ONE JSON line on rank 0 (value = uncompressed GiB of the whole job /
-(compress + decompress time), plus the per-direction rates, the encode
-kernel's roofline and the CPU baseline).
+One step at N = 1: compress the buffer into one lz4mt frame, then decompress
+that frame (block checksums verified by the decoder).
+
+One step at N > 1 (one process per GPU, RCCL): each
+rank owns a contiguous block range (its 8 GiB shard of the 8N GiB stream,
+weak scaling).
+  compress   = local encode + the RCCL gather of every shard's records into
+               ONE frame on rank 0 ("from the first launch to the completed
+               gather on the root"); ``gather_ms`` reports the gather alone;
+  scatter    = rank 0 walks that frame on the device and sends each rank its
+               run of whole records (lz4mt_amd.dist.scatter_frame); timed and
+               reported as ``scatter_ms``, outside ``value`` (it moves
+               compressed bytes root -> peers; the decompress figure is the
+               decoder's);
+  decompress = every rank decodes the piece it received.
+After the timed steps rank 0 decodes the stitched frame once (untimed) and
+compares every shard's chunk digests with the ranks' own (exit 1 on a
+mismatch); each rank also compares its decoded piece with its source.
+
+Prints ONE JSON line on rank 0: value = uncompressed GiB of the whole job /
+(compress + decompress time), the per-direction rates, the encode kernel's
+roofline (HIP events on the library's launch stream; HBM traffic from the
+committed PMC profile of this same configuration, calibrated) and the CPU
+baseline (lz4mt-shaped pipeline on the host cores over liblz4 when present).
 """
 import argparse
 import ctypes
@@ -36,6 +49,7 @@ from lz4mt_amd import dist as D  # noqa: E402
 GiB = float(1 << 30)
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 GOLDEN = 0x9E3779B97F4A7C15
+PMC_PROFILE = os.path.join(ROOT, "profiles", "pmc_current.json")
 
 
 def parse():
@@ -45,8 +59,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--gib", type=float, default=8.0, help="GiB per GPU")
     p.add_argument("--block-id", type=int, default=7, help="4..7 = 64 KiB..4 MiB")
+    p.add_argument("--stream-checksum", action="store_true",
+                   help="default lz4mt flags (FLG.2 content checksum, no block checksum) instead of -Sx -BX")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-mib", type=int, default=256, help="CPU baseline sample (MiB)")
+    p.add_argument("--cpu-mib", type=int, default=1024, help="CPU baseline sample (MiB, all threads)")
     p.add_argument("--decompress-only", action="store_true",
                    help="configs[2]: time only the decompression of a pre-compressed stream (use --gib 32)")
     return p.parse_args()
@@ -59,42 +75,6 @@ def timings():
     return list(ms)
 
 
-def cpu_baseline(mib, block_id):
-    """lz4mt-shaped CPU pipeline (oracle 'port'), bounded sample, rank 0 only."""
-    import oracle
-    n = mib << 20
-    buf = ctypes.create_string_buffer(n)
-    oracle.lib.orc_gen_synthetic(buf, n, 42)
-    p = oracle.params(block_id, stream_checksum=False, block_checksum=True)
-    threads = min(16, os.cpu_count() or 1)
-    tc1, td1, fs = oracle.pipeline_roundtrip(buf, n, p, 1)
-    tcN, tdN, _ = oracle.pipeline_roundtrip(buf, n, p, threads)
-    return {
-        "value": round(n / GiB / (tcN + tdN), 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-        "sample": f"{mib} MiB App.F synthetic, B{block_id} -Sx -BX, compress+decompress, lz4mt-shaped pipeline "
-                  f"(nPool=threads+1, in-order writer) over the oracle codec",
-        "compress_GiBps": round(n / GiB / tcN, 3), "decompress_GiBps": round(n / GiB / tdN, 3),
-        "single_thread_compress_GiBps": round(n / GiB / tc1, 3),
-        "single_thread_decompress_GiBps": round(n / GiB / td1, 3),
-        "cpu_model": _cpu_model(),
-    }
-
-
-def pmc_traffic(kernel, n, bm):
-    """HBM-side bytes per launch of `kernel` from the newest committed PMC
-    summary (profiles/*_pmc.json, written by tools/prof.sh + tools/pmcsum.py on
-    the same 8 GiB / 4 MiB-block workload); None when absent or not comparable."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))   # round tags sort by name
-    if not files or n != 8 << 30 or bm != 4 << 20:
-        return None, None
-    try:
-        k = json.load(open(files[-1]))["kernels"][kernel]
-    except (OSError, KeyError, ValueError):
-        return None, None
-    return k["fetch_bytes"] + k["write_bytes"], os.path.basename(files[-1])
-
-
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -103,6 +83,85 @@ def _cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def usable_cores():
+    """Threads the reference's pool would get here: hardware_concurrency()
+    (src/lz4mt_compat.cpp, nPool = hw + 1, src/lz4mt.cpp:281), bounded by
+    this process's affinity, its cgroup CPU quota and the pool's thread
+    share (OMP_NUM_THREADS / MAX_JOBS on the GPU box) -- threads beyond the
+    CPUs the process may run on only contend."""
+    hw = os.cpu_count() or 1
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else hw
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
+        v = os.environ.get(var, "")
+        if v.isdigit() and int(v) > 0:
+            n = min(n, int(v))
+    return max(1, n), hw
+
+
+def cpu_baseline(mib, block_id, sck):
+    """lz4mt-shaped CPU pipeline (one task per block, nPool = threads + 1,
+    in-order writer, block/stream XXH32) over liblz4 (the codec lz4mt links)
+    when the box has it, else over the oracle's restatement.  Rank 0, N = 1,
+    bounded sample; best of 3 at full width, one pass single-threaded."""
+    import oracle
+    threads, hw = usable_cores()
+    n = mib << 20
+    buf = ctypes.create_string_buffer(n)
+    oracle.lib.orc_gen_synthetic(buf, n, 42)
+    p = oracle.params(block_id, stream_checksum=sck, block_checksum=not sck)
+    lz = oracle.liblz4_codec()
+    codec, codec_name = (lz[0], f"liblz4 {lz[1]}") if lz else (None, "oracle restatement")
+    n1 = min(n, 256 << 20)
+    tc1, td1, _ = oracle.pipeline_roundtrip(buf, n1, p, 1, codec)
+    best = None
+    for _ in range(3):
+        tc, td, _ = oracle.pipeline_roundtrip(buf, n, p, threads, codec)
+        if best is None or tc + td < best[0] + best[1]:
+            best = (tc, td)
+    tcN, tdN = best
+    return {
+        "value": round(n / GiB / (tcN + tdN), 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "codec": codec_name,
+        "sample": f"{mib} MiB App.F synthetic, B{block_id} {'default flags' if sck else '-Sx -BX'}, compress+decompress "
+                  f"through an lz4mt-shaped pipeline (nPool=threads+1, in-order writer, checksums) over {codec_name}; "
+                  f"best of 3; single thread on {n1 >> 20} MiB",
+        "compress_GiBps": round(n / GiB / tcN, 3), "decompress_GiBps": round(n / GiB / tdN, 3),
+        "single_thread_compress_GiBps": round(n1 / GiB / tc1, 3),
+        "single_thread_decompress_GiBps": round(n1 / GiB / td1, 3),
+        "hardware_concurrency": hw, "cpu_model": _cpu_model(),
+    }
+
+
+def pmc_traffic(kernel, n, bm, flg):
+    """HBM bytes per launch of ``kernel`` from profiles/pmc_current.json, which
+    tools/prof.sh + tools/pmcsum.py write for one named configuration; used
+    only when that configuration is this run's (else None + the reason).
+    FETCH_SIZE is divided by the calibration the profile measured on a known
+    byte count (MI355X_MICROARCH.md: gfx950 FETCH_SIZE is ~1/2 of wide
+    streaming reads; other widths need their own calibration)."""
+    try:
+        prof = json.load(open(PMC_PROFILE))
+    except (OSError, ValueError):
+        return None, "no profiles/pmc_current.json"
+    cfg = prof.get("config", {})
+    if (cfg.get("bytes"), cfg.get("block_bytes"), cfg.get("flg")) != (n, bm, flg):
+        return None, f"profile config {cfg} is not this run's"
+    k = prof.get("kernels", {}).get(kernel)
+    if not k:
+        return None, f"{kernel} not in the profile"
+    cal = prof.get("calibration", {}).get(kernel) or prof.get("calibration", {}).get("default")
+    f = cal["fetch_factor"] if cal else 0.5
+    return {"bytes": k["fetch_bytes"] / f + k["write_bytes"], "fetch_raw": k["fetch_bytes"],
+            "write": k["write_bytes"], "fetch_factor": f, "calibration": cal.get("how") if cal else "guide x2",
+            "source": "profiles/pmc_current.json (" + prof.get("tag", "?") + ")"}, None
 
 
 def main():
@@ -121,11 +180,15 @@ def main():
     segs_per_rank = n // 65536
     seed = (42 + rank * segs_per_rank * GOLDEN) % (1 << 64)   # rank r = shard r of one global stream
     src = L.gen_synthetic(n, seed=seed, device=dev)
-    sd = L.make_sd(a.block_id, stream_checksum=False, block_checksum=True)
+    sck = a.stream_checksum
+    if sck and world > 1:
+        raise SystemExit("the content checksum (FLG.2) is one serial chain over the whole stream: it does not shard")
+    sd = L.make_sd(a.block_id, stream_checksum=sck, block_checksum=not sck)
+    flg = 0x64 if sck else 0x70
     cap = L.frame_bound(n, sd)
     frame_buf = torch.empty(cap, dtype=torch.uint8, device=dev)
     ws = L.compress_workspace(n, sd, device=dev)
-    out = torch.empty(n, dtype=torch.uint8, device=dev)
+    out = torch.empty(n + (1 << 20), dtype=torch.uint8, device=dev)
     fsz = torch.zeros(2, dtype=torch.int64, device=dev)
 
     def compress():
@@ -136,70 +199,79 @@ def main():
         if r != 0:
             raise L.Lz4MtError(r, "compress")
 
-    stitched = {"len": 0}
-
-    def gather_to_root(flen):
-        # one frame for the whole 8N GiB stream on rank 0 (lz4mt_amd/dist.py);
-        # enqueued only: it runs over xGMI while this rank decodes its shard
-        full, works = D.gather_frame(frame_buf, flen, dst=0, async_op=True)
-        return full, works
-
-    def decompress(flen):
+    def decompress(fr, flen):
         osz = ctypes.c_uint64(0)
         sdo = L.init_stream_descriptor()
-        r = L.lib.lz4mtHipDecompressFrame(ctypes.c_void_p(frame_buf.data_ptr()), flen,
+        r = L.lib.lz4mtHipDecompressFrame(ctypes.c_void_p(fr.data_ptr()), flen,
                                           ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.byref(osz),
                                           ctypes.byref(sdo), ctypes.c_void_p(stream.cuda_stream))
         if r != 0 or osz.value != n:
             raise L.Lz4MtError(r, f"decompress ({osz.value} of {n} bytes)")
 
+    def sync_all():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter()
+
     if a.decompress_only:   # compress once, untimed
         compress()
         torch.cuda.synchronize()
     L.lib.lz4mtHipSetTiming(1)
-    tc = td = 0.0
+    tc = td = ts = tg = 0.0
     enc_ms, dec_ms, frame_len = [], [], 0
+    full = piece = None
     for it in range(a.warmup + a.steps):
         timed = it >= a.warmup
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
+        t0 = sync_all()
         tm = None
         if not a.decompress_only:
             compress()
         frame_len = int(fsz[0].item())          # synchronises the stream
         if not a.decompress_only:
             tm = timings()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        full, works = gather_to_root(frame_len) if world > 1 and not a.decompress_only else (None, [])
-        decompress(frame_len)
-        tmd = timings()
-        for w in works:
-            w.wait()
-        if full is not None:
-            stitched["len"] = full.numel()
-        torch.cuda.synchronize()
+        tl = time.perf_counter()
+        if world > 1:   # the gather belongs to compress
+            full = D.gather_frame(frame_buf, frame_len, dst=0)
+            torch.cuda.synchronize()
+        t1 = sync_all()
+        tgr = time.perf_counter() - tl if world > 1 else 0.0
         if world > 1:
-            dist.barrier()
-        t2 = time.perf_counter()
+            piece = D.scatter_frame(full if rank == 0 else None, full.numel() if rank == 0 else 0, src=0)
+            torch.cuda.synchronize()
+            t2 = sync_all()
+        else:
+            piece, t2 = frame_buf, t1
+        decompress(piece, piece.numel() if world > 1 else frame_len)
+        tmd = timings()
+        t3 = sync_all()
         if timed:
             tc += t1 - t0
-            td += t2 - t1
+            ts += t2 - t1
+            td += t3 - t2
+            tg += tgr
             if tm:
                 enc_ms.append(tm[0])
             if tmd:
                 dec_ms.append(tmd[1])
     L.lib.lz4mtHipSetTiming(0)
 
-    # correctness of the last step (not timed)
-    ok = bool(torch.equal(out, src))
+    # correctness (not timed): this rank's decoded piece == its source; at
+    # N > 1 the root decodes the stitched frame and checks every shard
+    ok = bool(torch.equal(out[:n], src))
+    stitched_ok = None
     if world > 1:
-        t = torch.tensor([tc, td, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+        def digests(t):
+            return L.xxh32_chunks(t, 16 << 20).to(torch.int64)
+
+        def decode_full(f):
+            o, r = L.decompress_frame(f)
+            return o if r == 0 else o[:0]
+        stitched_ok = D.verify_stitched(full if rank == 0 else None, src, decode_full, digests)
+        t = torch.tensor([tc, td, ts, tg, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        tc, td, bad = t.tolist()
-        ok = bad == 0.0
+        tc, td, ts, tg, bad = t.tolist()
+        ok = bad == 0.0 and stitched_ok
     K = a.steps
     total = n * world * K
     comp_gibps = None if a.decompress_only else total / GiB / tc
@@ -208,32 +280,30 @@ def main():
 
     enc_avg = sum(enc_ms) / len(enc_ms) if enc_ms else None
     dec_avg = sum(dec_ms) / len(dec_ms) if dec_ms else None
-    body = frame_len - 7 - 4
-    roof = None
+    body = frame_len - 7 - 4 - (4 if sck else 0)
+    alg = n + body                           # algorithmic bytes per launch: in + out
+    roof = dec_roof = None
     if enc_avg:
-        alg = n + body                          # algorithmic bytes per encode launch
         ach = alg / (enc_avg * 1e-3) / 1e9
-        traffic, tsrc = pmc_traffic("k_encode", n, bm)
+        tr, why = pmc_traffic("k_encode", n, bm, flg)
         roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBPS, 5), "traffic": traffic, "kernel": "k_encode",
-                "kernel_ms": round(enc_avg, 3), "algorithmic_bytes": alg,
-                "traffic_source": f"profiles/{tsrc}: FETCH_SIZE + WRITE_SIZE per launch (raw counters)" if tsrc else None}
-    dec_roof = None
+                "frac": round(ach / HBM_PEAK_GBPS, 5), "traffic": round(tr["bytes"]) if tr else None,
+                "kernel": "k_encode", "kernel_ms": round(enc_avg, 3), "algorithmic_bytes": alg,
+                "traffic_detail": tr or why}
     if dec_avg:
-        alg = n + body
         ach = alg / (dec_avg * 1e-3) / 1e9
-        dtraffic, _ = pmc_traffic("k_decode", n, bm)
-        dec_roof = {"kernel": "k_decode", "kernel_ms": round(dec_avg, 3), "achieved": round(ach, 2),
-                    "frac": round(ach / HBM_PEAK_GBPS, 5), "traffic": dtraffic}
-
+        tr, why = pmc_traffic("k_decode", n, bm, flg)
+        dec_roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBPS, 5), "traffic": round(tr["bytes"]) if tr else None,
+                    "kernel": "k_decode", "kernel_ms": round(dec_avg, 3), "algorithmic_bytes": alg,
+                    "traffic_detail": tr or why}
     if a.decompress_only and dec_roof:   # the decode kernel is the dominant one here
-        roof = {"bound": "hbm", "achieved": dec_roof["achieved"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": dec_roof["frac"], "traffic": dec_roof["traffic"], "kernel": "k_decode",
-                "kernel_ms": dec_roof["kernel_ms"], "algorithmic_bytes": n + body}
+        roof = dec_roof
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
-            cpu = cpu_baseline(a.cpu_mib, a.block_id)
+            cpu = cpu_baseline(a.cpu_mib, a.block_id, sck)
+        flags = "default flags (FLG.2 content checksum)" if sck else "-Sx -BX"
         line = {
             "metric": "device-resident LZ4 GiB/s (compress, decompress) on 4 MiB blocks at 1/2/4/8 MI355X",
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": K, "warmup": a.warmup,
@@ -242,16 +312,20 @@ def main():
             "config": {"workload": (f"configs[2]: {a.gib:g} GiB/GPU pre-compressed synthetic stream, "
                                     f"{bm >> 10} KiB blocks, decompress+XXH32 verify only, device-resident")
                                    if a.decompress_only else
-                                   (f"configs[1]: {a.gib:g} GiB/GPU synthetic, {bm >> 10} KiB independent blocks, "
-                                    "-Sx -BX frame, compress+decompress+XXH32, device-resident"),
-                       "bytes_per_gpu": n, "block_bytes": bm, "parallelism": f"block-sharded x{world}"
-                                                                                + (", RCCL gather overlapped with decompress" if world > 1 else "")},
+                                   (f"configs[{1 if world == 1 else 3}]: {a.gib:g} GiB/GPU synthetic, {bm >> 10} KiB "
+                                    f"independent blocks, {flags} frame, compress+decompress+XXH32, device-resident"),
+                       "bytes_per_gpu": n, "block_bytes": bm,
+                       "parallelism": f"block-sharded x{world}" + (", RCCL gather to one frame on rank 0 (in compress)"
+                                                                   if world > 1 else "")},
             "compress_GiBps": round(comp_gibps, 3) if comp_gibps else None,
             "decompress_GiBps": round(decomp_gibps, 3),
             "ratio": round(n / frame_len, 4), "frame_bytes": frame_len,
-            "stitched_frame_bytes": stitched["len"] if world > 1 else frame_len, "roundtrip_ok": ok,
-            "roofline": roof, "decode_roofline": dec_roof, "cpu_baseline": cpu,
+            "roundtrip_ok": ok, "roofline": roof, "decode_roofline": dec_roof, "cpu_baseline": cpu,
         }
+        if world > 1:
+            line.update({"gather_ms": round(tg / K * 1e3, 3), "scatter_ms": round(ts / K * 1e3, 3),
+                         "stitched_frame_bytes": full.numel(), "stitched_frame_ok": stitched_ok,
+                         "roundtrip_with_scatter_GiBps": round(total / GiB / (tc + ts + td), 3)})
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

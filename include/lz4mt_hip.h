@@ -75,13 +75,37 @@ Lz4MtResult lz4mtHipFrameInfo(const void* d_frame, uint64_t frameSize, Lz4MtStre
 Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t frameSize, void* d_out, uint64_t outCap,
                                     uint64_t* outSize, Lz4MtStreamDescriptor* sd, void* stream);
 
+/* Upper bound of the decoded size of every frame in d_frame[0..frameSize)
+ * (concatenated and skippable frames included): the out capacity
+ * lz4mtHipDecompressFrame needs.  Walks each frame's size words. */
+Lz4MtResult lz4mtHipStreamBound(const void* d_frame, uint64_t frameSize, uint64_t* decodedBound, void* stream);
+/* Record table of the single frame at d_frame: recordStart[i] = frame
+ * offset of block i's size word (i < *nBlocks), recordStart[*nBlocks] = the
+ * EOS word; *hdrLen = header bytes incl. magic.  `cap` entries of host
+ * memory (>= blocks + 1; recordStart NULL = count only).  The device walk of
+ * lz4mtHipDecompressFrame; used to cut a frame into per-GPU sub-frames of
+ * whole records (the multi-GPU decompress scatter). */
+Lz4MtResult lz4mtHipFrameRecords(const void* d_frame, uint64_t frameSize, uint64_t* recordStart, uint64_t cap,
+                                 uint64_t* nBlocks, int* hdrLen, Lz4MtStreamDescriptor* sd, void* stream);
+
 /* ---- 3. utilities ------------------------------------------------------- */
 /* SURVEY.md App. F generator, bit-identical to the CPU oracle. */
 int lz4mtHipGenSynthetic(void* d_dst, uint64_t n, uint64_t seed, void* stream);
-/* XXH32 (seed 0) of device memory; synchronises the stream. */
+/* XXH32 (seed 0) of device memory; synchronises the stream.  One serial
+ * chain (one wavefront): use it for small ranges. */
 uint32_t lz4mtHipXxh32(const void* d_src, uint64_t len, void* stream);
+/* XXH32 of each consecutive chunkBytes piece of d_src (the last one short)
+ * into d_digests[ceil(len / chunkBytes)] (device memory), in parallel;
+ * asynchronous.  Returns 0, or -1 without a device / on bad arguments. */
+int lz4mtHipXxh32Chunks(const void* d_src, uint64_t len, uint32_t chunkBytes, uint32_t* d_digests, void* stream);
 /* Number of HIP devices visible (0 = none: every compute entry point errors). */
 int lz4mtHipDeviceCount(void);
+/* Frees the calling thread's cached engine memory (the DEVICE mode's pinned
+ * staging slots and device buffers, the decode scratch) and the idle
+ * scratch of the block operators.  LZ4MT_MODE_DEVICE callers keep their
+ * slots between calls (no re-pinning); relinked default-PARALLEL callers
+ * have them freed at the end of every call. */
+void lz4mtHipReleaseCaches(void);
 
 /* Per-stage device timings (ms, hipEvents) of the last frame call on this
  * thread: [0] encode/decode kernel, [1] checksum kernel(s), [2] scan +

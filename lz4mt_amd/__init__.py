@@ -24,7 +24,7 @@ __all__ = [
     "init_context", "init_stream_descriptor", "result_to_string", "result_to_exit_code", "make_sd",
     "compress", "decompress", "compress_block", "decompress_block", "compress_bound",
     "compress_frame", "decompress_frame", "frame_info", "frame_bound", "gen_synthetic", "xxh32",
-    "device_count",
+    "device_count", "stream_bound", "frame_records", "xxh32_chunks",
 ]
 
 lib = _abi.load()
@@ -33,7 +33,8 @@ lib = _abi.load()
 class Lz4MtError(RuntimeError):
     def __init__(self, code, what=""):
         self.code = int(code)
-        super().__init__(f"{what}: {result_to_string(code)} ({code})")
+        name = RESULT_NAMES[code] if 0 <= code < len(RESULT_NAMES) else result_to_string(code)
+        super().__init__(f"{what}: {name} ({code})")
 
 
 def init_context():
@@ -193,12 +194,50 @@ def frame_info(frame, stream=None):
     return sd, bound.value, nb.value
 
 
+def stream_bound(frame, stream=None):
+    """Decoded-size bound of every frame in the device bytes (concatenated and skippable frames included)."""
+    _check_dev(frame, "frame")
+    b = ctypes.c_uint64(0)
+    r = lib.lz4mtHipStreamBound(ctypes.c_void_p(frame.data_ptr()), frame.numel(), ctypes.byref(b), _stream(stream))
+    if r != Result.OK:
+        raise Lz4MtError(r, "lz4mtHipStreamBound")
+    return b.value
+
+
+def frame_records(frame, frame_len=None, stream=None):
+    """(header length, [record start offsets..., EOS offset], descriptor) of one device frame (device walk)."""
+    _check_dev(frame, "frame")
+    n = frame.numel() if frame_len is None else int(frame_len)
+    sd = init_stream_descriptor()
+    nb, hl = ctypes.c_uint64(0), ctypes.c_int(0)
+    r = lib.lz4mtHipFrameRecords(ctypes.c_void_p(frame.data_ptr()), n, None, 0, ctypes.byref(nb), ctypes.byref(hl),
+                                 ctypes.byref(sd), _stream(stream))
+    if r != Result.OK:
+        raise Lz4MtError(r, "lz4mtHipFrameRecords")
+    recs = (ctypes.c_uint64 * (nb.value + 1))()
+    r = lib.lz4mtHipFrameRecords(ctypes.c_void_p(frame.data_ptr()), n, recs, nb.value + 1, ctypes.byref(nb),
+                                 ctypes.byref(hl), ctypes.byref(sd), _stream(stream))
+    if r != Result.OK:
+        raise Lz4MtError(r, "lz4mtHipFrameRecords")
+    return hl.value, list(recs), sd
+
+
+def xxh32_chunks(t, chunk=16 << 20, stream=None):
+    """XXH32 of each consecutive ``chunk``-byte piece of a device tensor (int32 tensor of digests, same device)."""
+    _check_dev(t, "tensor")
+    nc = (t.numel() + chunk - 1) // chunk
+    d = torch.empty(max(nc, 1), dtype=torch.int32, device=t.device)
+    if nc and lib.lz4mtHipXxh32Chunks(ctypes.c_void_p(t.data_ptr()), t.numel(), chunk, ctypes.c_void_p(d.data_ptr()),
+                                      _stream(stream)) != 0:
+        raise Lz4MtError(Result.ERROR, "lz4mtHipXxh32Chunks")
+    return d[:nc]
+
+
 def decompress_frame(frame, out=None, stream=None, check=True):
     """Decompresses device frame bytes; returns (decoded tensor view, result code)."""
     _check_dev(frame, "frame")
     if out is None:
-        _, bound, _ = frame_info(frame, stream)
-        out = torch.empty(max(bound, 1), dtype=torch.uint8, device=frame.device)
+        out = torch.empty(max(stream_bound(frame, stream), 1), dtype=torch.uint8, device=frame.device)
     sd = init_stream_descriptor()
     osz = ctypes.c_uint64(0)
     r = lib.lz4mtHipDecompressFrame(ctypes.c_void_p(frame.data_ptr()), frame.numel(),

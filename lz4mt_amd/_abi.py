@@ -99,9 +99,14 @@ PROTOTYPES = {
                                   c_void_p]),
     "lz4mtHipDecompressFrame": (c_int, [c_void_p, c_uint64, c_void_p, c_uint64, ctypes.POINTER(c_uint64), SD_P,
                                         c_void_p]),
+    "lz4mtHipStreamBound": (c_int, [c_void_p, c_uint64, ctypes.POINTER(c_uint64), c_void_p]),
+    "lz4mtHipFrameRecords": (c_int, [c_void_p, c_uint64, ctypes.POINTER(c_uint64), c_uint64,
+                                     ctypes.POINTER(c_uint64), ctypes.POINTER(c_int), SD_P, c_void_p]),
     "lz4mtHipGenSynthetic": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p]),
+    "lz4mtHipXxh32Chunks": (c_int, [c_void_p, c_uint64, c_uint32, c_void_p, c_void_p]),
     "lz4mtHipXxh32": (c_uint32, [c_void_p, c_uint64, c_void_p]),
     "lz4mtHipDeviceCount": (c_int, []),
+    "lz4mtHipReleaseCaches": (None, []),
     "lz4mtHipSetTiming": (None, [c_int]),
     "lz4mtHipGetTimings": (c_int, [ctypes.POINTER(c_float)]),
     "lz4mtHipDebugEncodeStats": (c_int, [c_void_p, c_uint64, c_uint32, ctypes.POINTER(c_uint64), c_void_p]),

@@ -66,6 +66,7 @@ hipError_t launch_xxh32_stored(const uint8_t* src, const uint8_t* slots, uint64_
 hipError_t launch_xxh32_frame_blocks(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t* digest,
                                      hipStream_t st);
 hipError_t launch_xxh32_stream(const uint8_t* p, uint64_t len, uint32_t* digest, hipStream_t st);
+hipError_t launch_xxh32_chunks(const uint8_t* p, uint64_t len, uint32_t chunk, uint32_t* digest, hipStream_t st);
 hipError_t launch_frame_scan(const int32_t* csize, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                              int blockChecksum, uint64_t* recOff, hipStream_t st);
 hipError_t launch_frame_assemble(const uint8_t* src, const uint8_t* slots, uint64_t srcSize, uint32_t blockSize,

@@ -78,7 +78,12 @@ CompressWs carve_compress(uint8_t* base, uint64_t nb, uint64_t bm) {
     return w;
 }
 
-// ---- thread-local scratch for the block operators -------------------------
+// ---- scratch for the block operators --------------------------------------
+// A process-wide pool, not one per thread: the reference's scheduler runs
+// each block on a fresh std::async thread (src/lz4mt.cpp:448,722), so a
+// thread_local cache would leak a stream and two buffers per block.  Each
+// call borrows a scratch object and returns it; the pool holds at most as
+// many as ever ran concurrently.
 struct BlockScratch {
     hipStream_t st = nullptr;
     uint8_t* dIn = nullptr;
@@ -86,11 +91,22 @@ struct BlockScratch {
     uint64_t capIn = 0, capOut = 0;
     int32_t* dRes = nullptr;
     BlockRec* dRec = nullptr;
+    int dev = -1;
+    void release() {
+        if (st) hipStreamSynchronize(st);
+        hipFree(dIn); hipFree(dOut); hipFree(dRes); hipFree(dRec);
+        if (st) hipStreamDestroy(st);
+        *this = BlockScratch();
+    }
     bool init() {
-        if (st) return true;
-        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
-        if (hipMalloc(&dRes, 256) != hipSuccess) return false;
-        if (hipMalloc(&dRec, 256) != hipSuccess) return false;
+        int d = -1;
+        if (hipGetDevice(&d) != hipSuccess) return false;
+        if (st && d == dev) return true;
+        release();
+        dev = d;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) { st = nullptr; return false; }
+        if (hipMalloc(&dRes, 256) != hipSuccess) { dRes = nullptr; return false; }
+        if (hipMalloc(&dRec, 256) != hipSuccess) { dRec = nullptr; return false; }
         return true;
     }
     bool ensure(uint64_t in, uint64_t out) {
@@ -107,7 +123,85 @@ struct BlockScratch {
         return true;
     }
 };
-thread_local BlockScratch g_blk;
+
+class ScratchPool {
+public:
+    BlockScratch* get() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            if (!free_.empty()) {
+                BlockScratch* b = free_.back();
+                free_.pop_back();
+                return b;
+            }
+        }
+        return new BlockScratch();
+    }
+    void put(BlockScratch* b) {
+        std::lock_guard<std::mutex> g(mu_);
+        free_.push_back(b);
+    }
+    void clear() {
+        std::vector<BlockScratch*> v;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            v.swap(free_);
+        }
+        for (BlockScratch* b : v) { b->release(); delete b; }
+    }
+    size_t idle() {
+        std::lock_guard<std::mutex> g(mu_);
+        return free_.size();
+    }
+
+private:
+    std::mutex mu_;
+    std::vector<BlockScratch*> free_;
+};
+// never destroyed: its buffers must not be freed after the HIP runtime's own
+// teardown at exit
+ScratchPool& scratch_pool() {
+    static ScratchPool* p = new ScratchPool();
+    return *p;
+}
+struct ScratchLease {
+    BlockScratch* b;
+    ScratchLease() : b(scratch_pool().get()) {}
+    ~ScratchLease() { scratch_pool().put(b); }
+    BlockScratch* operator->() { return b; }
+};
+
+// device buffer freed on every return path
+struct DevBuf {
+    uint8_t* p = nullptr;
+    uint64_t cap = 0;
+    ~DevBuf() { hipFree(p); }
+    bool ensure(uint64_t n) {
+        if (p && n <= cap) return true;
+        hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&p), n + 64) != hipSuccess) { p = nullptr; return false; }
+        cap = n;
+        return true;
+    }
+};
+
+// A few bytes of device memory per thread (frame-size / digest results),
+// re-made when the thread's device changes: no hipMalloc/hipFree per call
+// (hipFree waits for the whole device).
+uint8_t* small_dev() {
+    thread_local uint8_t* p = nullptr;
+    thread_local int dev = -1;
+    int d = -1;
+    if (hipGetDevice(&d) != hipSuccess) return nullptr;
+    if (!p || d != dev) {
+        p = nullptr;   // a buffer of another device is left to that device
+        if (hipMalloc(reinterpret_cast<void**>(&p), 256) != hipSuccess) { p = nullptr; return nullptr; }
+        dev = d;
+    }
+    return p;
+}
 
 }  // namespace
 
@@ -188,40 +282,44 @@ extern "C" int lz4mtHipCompressBlock(const char* src, char* dst, int isize, int 
     if (compressionLevel >= 3) return 0;   // no GPU LZ4-HC: caller stores the block raw
     if (isize < 0 || (unsigned)isize > 0x7E000000u) return 0;
     if (maxOutputSize < 0) maxOutputSize = 0;
-    if (!have_device() || !g_blk.init()) return -1;
+    if (!have_device()) return -1;
+    ScratchLease g_blk;
+    if (!g_blk->init()) return -1;
     const int bound = lz4mtHipCompressBound(isize);
     const uint64_t outMax = (uint64_t)std::min(maxOutputSize, bound) + 16;
-    if (!g_blk.ensure((uint64_t)isize, outMax)) return -1;
-    if (isize && hipMemcpyAsync(g_blk.dIn, src, (size_t)isize, hipMemcpyHostToDevice, g_blk.st) != hipSuccess) return -1;
-    if (launch_encode(g_blk.dIn, (uint64_t)isize, (uint32_t)std::max(isize, 1), 1, g_blk.dOut, 0,
-                      (uint32_t)maxOutputSize, g_blk.dRes, g_blk.st) != hipSuccess)
+    if (!g_blk->ensure((uint64_t)isize, outMax)) return -1;
+    if (isize && hipMemcpyAsync(g_blk->dIn, src, (size_t)isize, hipMemcpyHostToDevice, g_blk->st) != hipSuccess) return -1;
+    if (launch_encode(g_blk->dIn, (uint64_t)isize, (uint32_t)std::max(isize, 1), 1, g_blk->dOut, 0,
+                      (uint32_t)maxOutputSize, g_blk->dRes, g_blk->st) != hipSuccess)
         return -1;
     int32_t r = 0;
-    if (hipMemcpyAsync(&r, g_blk.dRes, 4, hipMemcpyDeviceToHost, g_blk.st) != hipSuccess) return -1;
-    if (hipStreamSynchronize(g_blk.st) != hipSuccess) return -1;
+    if (hipMemcpyAsync(&r, g_blk->dRes, 4, hipMemcpyDeviceToHost, g_blk->st) != hipSuccess) return -1;
+    if (hipStreamSynchronize(g_blk->st) != hipSuccess) return -1;
     if (r > 0) {
-        if (hipMemcpyAsync(dst, g_blk.dOut, (size_t)r, hipMemcpyDeviceToHost, g_blk.st) != hipSuccess) return -1;
-        if (hipStreamSynchronize(g_blk.st) != hipSuccess) return -1;
+        if (hipMemcpyAsync(dst, g_blk->dOut, (size_t)r, hipMemcpyDeviceToHost, g_blk->st) != hipSuccess) return -1;
+        if (hipStreamSynchronize(g_blk->st) != hipSuccess) return -1;
     }
     return r;
 }
 
 extern "C" int lz4mtHipDecompressBlock(const char* src, char* dst, int isize, int maxOutputSize) {
     if (isize < 0 || maxOutputSize < 0) return -1;
-    if (!have_device() || !g_blk.init()) return -1;
-    if (!g_blk.ensure((uint64_t)isize, (uint64_t)maxOutputSize)) return -1;
-    if (isize && hipMemcpyAsync(g_blk.dIn, src, (size_t)isize, hipMemcpyHostToDevice, g_blk.st) != hipSuccess) return -1;
+    if (!have_device()) return -1;
+    ScratchLease g_blk;
+    if (!g_blk->init()) return -1;
+    if (!g_blk->ensure((uint64_t)isize, (uint64_t)maxOutputSize)) return -1;
+    if (isize && hipMemcpyAsync(g_blk->dIn, src, (size_t)isize, hipMemcpyHostToDevice, g_blk->st) != hipSuccess) return -1;
     BlockRec rec{0, (uint32_t)isize, 0};
-    if (hipMemcpyAsync(g_blk.dRec, &rec, sizeof(rec), hipMemcpyHostToDevice, g_blk.st) != hipSuccess) return -1;
-    if (launch_decode(g_blk.dIn, g_blk.dRec, 1, (uint32_t)maxOutputSize, g_blk.dOut, (uint64_t)maxOutputSize,
-                      g_blk.dRes, g_blk.st) != hipSuccess)
+    if (hipMemcpyAsync(g_blk->dRec, &rec, sizeof(rec), hipMemcpyHostToDevice, g_blk->st) != hipSuccess) return -1;
+    if (launch_decode(g_blk->dIn, g_blk->dRec, 1, (uint32_t)maxOutputSize, g_blk->dOut, (uint64_t)maxOutputSize,
+                      g_blk->dRes, g_blk->st) != hipSuccess)
         return -1;
     int32_t r = 0;
-    if (hipMemcpyAsync(&r, g_blk.dRes, 4, hipMemcpyDeviceToHost, g_blk.st) != hipSuccess) return -1;
-    if (hipStreamSynchronize(g_blk.st) != hipSuccess) return -1;
+    if (hipMemcpyAsync(&r, g_blk->dRes, 4, hipMemcpyDeviceToHost, g_blk->st) != hipSuccess) return -1;
+    if (hipStreamSynchronize(g_blk->st) != hipSuccess) return -1;
     if (r > 0) {
-        if (hipMemcpyAsync(dst, g_blk.dOut, (size_t)r, hipMemcpyDeviceToHost, g_blk.st) != hipSuccess) return -1;
-        if (hipStreamSynchronize(g_blk.st) != hipSuccess) return -1;
+        if (hipMemcpyAsync(dst, g_blk->dOut, (size_t)r, hipMemcpyDeviceToHost, g_blk->st) != hipSuccess) return -1;
+        if (hipStreamSynchronize(g_blk->st) != hipSuccess) return -1;
     }
     return r == kDecodeOutputTooSmall ? -1 : r;
 }
@@ -261,18 +359,32 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
     uint8_t hdr[kMaxHeader];
     const int hdrLen = build_header(sd, hdr);
     uint64_t* recOff = nullptr;
-    // side stream for the block checksums, except while `st` is being
-    // captured into a graph (no stream creation inside a capture)
-    thread_local AuxStream aux;
+    // side streams (block checksums; the content checksum), except while
+    // `st` is being captured into a graph (no stream creation inside a capture)
+    thread_local AuxStream aux, auxStream;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     const bool capturing = hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone;
+    CompressWs w = carve_compress(ws, (srcSize + bm - 1) / bm, bm);
+    // The content checksum (FLG.2) is one serial XXH32 chain over the input
+    // (SURVEY.md §0.5).  It reads only d_src, so it starts at t = 0 on its
+    // own stream, beside the encode, and the finalize waits for it.
+    const bool sck = sd->flg.streamChecksum != 0;
+    const bool sckSide = sck && !capturing && auxStream.ensure();
+    if (sckSide) {
+        HIPCHK(hipEventRecord(auxStream.evIn, st));
+        HIPCHK(hipStreamWaitEvent(auxStream.st, auxStream.evIn, 0));
+        HIPCHK(launch_xxh32_stream(static_cast<const uint8_t*>(d_src), srcSize, w.ssum, auxStream.st));
+        HIPCHK(hipEventRecord(auxStream.evOut, auxStream.st));
+    }
     const Lz4MtResult r = device_compress_body(static_cast<const uint8_t*>(d_src), srcSize, bm, sd->flg.blockChecksum,
                                                ws, static_cast<uint8_t*>(d_frame), (uint32_t)hdrLen, st, &recOff,
                                                !capturing && aux.ensure() ? &aux : nullptr);
-    if (r != LZ4MT_RESULT_OK) return r;
-    CompressWs w = carve_compress(ws, (srcSize + bm - 1) / bm, bm);
-    if (sd->flg.streamChecksum)
-        HIPCHK(launch_xxh32_stream(static_cast<const uint8_t*>(d_src), srcSize, w.ssum, st));
+    if (r != LZ4MT_RESULT_OK) {
+        if (sckSide) hipStreamWaitEvent(st, auxStream.evOut, 0);   // scratch outlives the side kernel
+        return r;
+    }
+    if (sckSide) HIPCHK(hipStreamWaitEvent(st, auxStream.evOut, 0));
+    else if (sck) HIPCHK(launch_xxh32_stream(static_cast<const uint8_t*>(d_src), srcSize, w.ssum, st));
     g_timing.mark(3, st);
     HIPCHK(launch_frame_finalize(static_cast<uint8_t*>(d_frame), hdr, (uint32_t)hdrLen, recOff,
                                  (uint32_t)((srcSize + bm - 1) / bm), sd->flg.streamChecksum ? w.ssum : nullptr,
@@ -300,8 +412,8 @@ extern "C" Lz4MtResult lz4mtHipCompressFrame(const void* d_src, uint64_t srcSize
                                              uint64_t workspaceSize, void* stream) {
     void* owned = nullptr;
     const hipStream_t st = static_cast<hipStream_t>(stream);
-    uint64_t* dfs = nullptr;
-    if (hipMalloc(reinterpret_cast<void**>(&dfs), 16) != hipSuccess) return LZ4MT_RESULT_ERROR;
+    uint64_t* dfs = reinterpret_cast<uint64_t*>(small_dev());
+    if (!dfs) return LZ4MT_RESULT_ERROR;
     Lz4MtResult r = compress_frame_impl(d_src, srcSize, d_frame, frameCap, dfs, sd, d_workspace, workspaceSize, st, &owned);
     if (r == LZ4MT_RESULT_OK) {
         uint64_t fs = 0;
@@ -313,7 +425,6 @@ extern "C" Lz4MtResult lz4mtHipCompressFrame(const void* d_src, uint64_t srcSize
         hipStreamSynchronize(st);
     }
     if (owned) hipFree(owned);
-    hipFree(dfs);
     return r;
 }
 
@@ -474,6 +585,108 @@ extern "C" Lz4MtResult lz4mtHipFrameInfo(const void* d_frame, uint64_t frameSize
     }
 }
 
+// Header of the frame (or skippable frame) at `pos`: kind 0 = lz4mt frame
+// (sd, hdrLen filled), 1 = skippable (skip = bytes to jump), 2 = end
+// (fewer than 4 bytes, or non-magic data after a frame), or an error code.
+namespace {
+struct HeadInfo {
+    int kind = 0;
+    int hdrLen = 0;
+    uint64_t skip = 0;
+    Lz4MtResult err = LZ4MT_RESULT_OK;
+};
+HeadInfo read_head(const uint8_t* f, uint64_t frameSize, uint64_t pos, bool seen, Lz4MtStreamDescriptor* sd,
+                   hipStream_t st) {
+    HeadInfo hi;
+    uint8_t h[kMaxHeader + 8] = {0};
+    const uint64_t avail = std::min<uint64_t>(sizeof(h), frameSize - pos);
+    if (hipMemcpyAsync(h, f + pos, avail, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+        hi.err = LZ4MT_RESULT_ERROR;
+        return hi;
+    }
+    if (avail < 4) { hi.kind = 2; return hi; }
+    const uint32_t magic = get32(h);
+    if (magic != kMagic) {
+        if (magic >= kSkippableMin && magic <= kSkippableMax) {
+            if (avail < 8) { hi.err = LZ4MT_RESULT_INVALID_HEADER_SKIPPABLE_SIZE_UNREADABLE; return hi; }
+            hi.kind = 1;
+            hi.skip = 8 + (uint64_t)get32(h + 4);
+            return hi;
+        }
+        if (!seen) hi.err = LZ4MT_RESULT_INVALID_MAGIC_NUMBER;
+        hi.kind = 2;
+        return hi;
+    }
+    int hb = 0;
+    hi.err = parse_header(h + 4, avail - 4, sd, &hb);
+    if (hi.err == LZ4MT_RESULT_OK && !sd->flg.blockIndependence) hi.err = LZ4MT_RESULT_BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET;
+    hi.hdrLen = 4 + hb;
+    return hi;
+}
+}  // namespace
+
+extern "C" Lz4MtResult lz4mtHipStreamBound(const void* d_frame, uint64_t frameSize, uint64_t* decodedBound,
+                                           void* stream) {
+    if (!d_frame || !decodedBound) return LZ4MT_RESULT_BAD_ARG;
+    if (!have_device()) return LZ4MT_RESULT_ERROR;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint8_t* f = static_cast<const uint8_t*>(d_frame);
+    DecodeBuffers& B = decode_cache();
+    uint64_t pos = 0, bound = 0;
+    bool seen = false;
+    *decodedBound = 0;
+    while (pos < frameSize) {
+        Lz4MtStreamDescriptor sd = lz4mtInitStreamDescriptor();
+        const HeadInfo hi = read_head(f, frameSize, pos, seen, &sd, st);
+        if (hi.err != LZ4MT_RESULT_OK) return hi.err;
+        if (hi.kind == 2) break;
+        if (hi.kind == 1) { pos = std::min<uint64_t>(frameSize, pos + hi.skip); continue; }
+        seen = true;
+        const uint32_t bm = (uint32_t)block_max_bytes(sd.bd.blockMaximumSize);
+        WalkInfo wi{};
+        const Lz4MtResult wr = walk_frame(f, frameSize, pos + hi.hdrLen, bm, sd.flg.blockChecksum, B, wi, st);
+        if (wr != LZ4MT_RESULT_OK) return wr;
+        bound += (uint64_t)wi.nBlocks * bm;
+        if (wi.result != 0) break;   // a damaged frame: the decoder stops inside it
+        pos = wi.endPos + (sd.flg.streamChecksum ? 4 : 0);
+    }
+    *decodedBound = bound;
+    return LZ4MT_RESULT_OK;
+}
+
+extern "C" Lz4MtResult lz4mtHipFrameRecords(const void* d_frame, uint64_t frameSize, uint64_t* recordStart,
+                                            uint64_t cap, uint64_t* nBlocks, int* hdrLen,
+                                            Lz4MtStreamDescriptor* sd, void* stream) {
+    if (!d_frame || !nBlocks || !sd) return LZ4MT_RESULT_BAD_ARG;
+    if (!have_device()) return LZ4MT_RESULT_ERROR;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint8_t* f = static_cast<const uint8_t*>(d_frame);
+    const HeadInfo hi = read_head(f, frameSize, 0, false, sd, st);
+    if (hi.err != LZ4MT_RESULT_OK) return hi.err;
+    if (hi.kind != 0) return LZ4MT_RESULT_INVALID_MAGIC_NUMBER;
+    const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
+    DecodeBuffers& B = decode_cache();
+    WalkInfo wi{};
+    const Lz4MtResult wr = walk_frame(f, frameSize, (uint64_t)hi.hdrLen, bm, sd->flg.blockChecksum, B, wi, st);
+    if (wr != LZ4MT_RESULT_OK) return wr;
+    if (wi.result != 0) return (Lz4MtResult)wi.result;
+    *nBlocks = wi.nBlocks;
+    if (hdrLen) *hdrLen = hi.hdrLen;
+    if (recordStart && cap >= (uint64_t)wi.nBlocks + 1) {
+        std::vector<BlockRec> r(wi.nBlocks);
+        if (wi.nBlocks) {
+            HIPCHK(hipMemcpyAsync(r.data(), B.recs, wi.nBlocks * sizeof(BlockRec), hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+        }
+        for (uint64_t i = 0; i < wi.nBlocks; ++i) recordStart[i] = r[i].offset - 4;   // the size word
+        recordStart[wi.nBlocks] = wi.endPos - 4;                                      // the EOS word
+    } else if (recordStart) {
+        return LZ4MT_RESULT_BAD_ARG;
+    }
+    return LZ4MT_RESULT_OK;
+}
+
 extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t frameSize, void* d_out, uint64_t outCap,
                                                uint64_t* outSize, Lz4MtStreamDescriptor* sd, void* stream) {
     if (!d_frame || !sd || (!d_out && outCap)) return LZ4MT_RESULT_BAD_ARG;
@@ -486,8 +699,7 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
     Lz4MtResult result = LZ4MT_RESULT_OK;
     DecodeBuffers& B = decode_cache();
     thread_local AuxStream aux;   // block checksums beside the decode
-    uint8_t* tmp = nullptr;   // staging when a frame's output is unaligned or needs compaction
-    uint64_t tmpCap = 0;
+    DevBuf tmp;   // staging when a frame's output is unaligned or needs compaction (freed on every return)
     if (outSize) *outSize = 0;
     while (pos < frameSize) {
         uint8_t h[kMaxHeader + 8] = {0};
@@ -525,12 +737,8 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
         uint8_t* target = out + opos;
         uint64_t targetCap = room;
         if (!aligned) {
-            if (tmpCap < nb * bm) {
-                hipFree(tmp);
-                tmpCap = nb * bm;
-                if (hipMalloc(reinterpret_cast<void**>(&tmp), tmpCap + 64) != hipSuccess) { tmp = nullptr; result = LZ4MT_RESULT_ERROR; break; }
-            }
-            target = tmp;
+            if (!tmp.ensure(nb * bm)) { result = LZ4MT_RESULT_ERROR; break; }
+            target = tmp.p;
             targetCap = std::min<uint64_t>(room, nb * bm);
         }
         // The block checksums run on a side stream beside the decode: the
@@ -573,13 +781,9 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
             // compaction: copy slots through staging in block order
             uint8_t* srcBase = target;
             if (aligned) {  // slots live in the output itself: stage them first
-                if (tmpCap < good * (uint64_t)bm) {
-                    hipFree(tmp);
-                    tmpCap = good * (uint64_t)bm;
-                    if (hipMalloc(reinterpret_cast<void**>(&tmp), tmpCap + 64) != hipSuccess) { tmp = nullptr; result = LZ4MT_RESULT_ERROR; break; }
-                }
-                HIPCHK(hipMemcpyAsync(tmp, target, std::min<uint64_t>(good * (uint64_t)bm, targetCap), hipMemcpyDeviceToDevice, st));
-                srcBase = tmp;
+                if (!tmp.ensure(good * (uint64_t)bm)) { result = LZ4MT_RESULT_ERROR; break; }
+                HIPCHK(hipMemcpyAsync(tmp.p, target, std::min<uint64_t>(good * (uint64_t)bm, targetCap), hipMemcpyDeviceToDevice, st));
+                srcBase = tmp.p;
             }
             uint64_t w = 0;
             for (uint64_t i = 0; i < good; ++i) {
@@ -606,7 +810,6 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
         pos = next;
     }
     hipStreamSynchronize(st);
-    hipFree(tmp);
     if (outSize) *outSize = opos;
     return result;
 }
@@ -623,14 +826,30 @@ extern "C" int lz4mtHipGenSynthetic(void* d_dst, uint64_t n, uint64_t seed, void
 extern "C" uint32_t lz4mtHipXxh32(const void* d_src, uint64_t len, void* stream) {
     if (!have_device()) return 0;
     const hipStream_t st = static_cast<hipStream_t>(stream);
-    uint32_t* d = nullptr;
+    uint32_t* d = reinterpret_cast<uint32_t*>(small_dev());
     uint32_t h = 0;
-    if (hipMalloc(reinterpret_cast<void**>(&d), 16) != hipSuccess) return 0;
+    if (!d) return 0;
     if (launch_xxh32_stream(static_cast<const uint8_t*>(d_src), len, d, st) == hipSuccess &&
         hipMemcpyAsync(&h, d, 4, hipMemcpyDeviceToHost, st) == hipSuccess)
         hipStreamSynchronize(st);
-    hipFree(d);
     return h;
+}
+
+extern "C" int lz4mtHipXxh32Chunks(const void* d_src, uint64_t len, uint32_t chunkBytes, uint32_t* d_digests,
+                                   void* stream) {
+    if (!have_device() || chunkBytes == 0 || (len && (!d_src || !d_digests))) return -1;
+    return launch_xxh32_chunks(static_cast<const uint8_t*>(d_src), len, chunkBytes, d_digests,
+                               static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -1;
+}
+
+namespace lz4mt {
+void release_slot_cache();
+}
+
+extern "C" void lz4mtHipReleaseCaches(void) {
+    release_slot_cache();
+    decode_cache().release();
+    scratch_pool().clear();
 }
 
 extern "C" int lz4mtHipDeviceCount(void) {

@@ -21,7 +21,7 @@
 // src/lz4mt.cpp:971-979); skippable frames are skipped by reading when
 // readSkippable is null (the CLI leaves it null and segfaults,
 // src/main.cpp:767-775); the futures vector race (src/lz4mt.cpp:408,448) has
-// no counterpart; lz4mtResultToString names every code.
+// no counterpart.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -85,8 +85,14 @@ public:
     // readU32: a short read sets ERROR (reference Ctx::readU32)
     bool readU32(uint32_t* v) {
         if (error()) return false;
+        if (!peekU32(v)) { set(LZ4MT_RESULT_ERROR); return false; }
+        return true;
+    }
+    // the same read without touching the result: the DEVICE engine records
+    // the code and applies it after the blocks already batched are written
+    bool peekU32(uint32_t* v) {
         uint8_t b[4];
-        if (read(b, 4) != 4) { set(LZ4MT_RESULT_ERROR); return false; }
+        if (read(b, 4) != 4) return false;
         *v = get32(b);
         return true;
     }
@@ -407,6 +413,9 @@ struct SlotCache {
     ~SlotCache() {
         for (Slot& s : slot) s.release();
     }
+    void release() {
+        for (Slot& s : slot) s.release();
+    }
     // a call that ends early (error) may leave batches in flight: drain them
     void quiesce() {
         for (Slot& s : slot) {
@@ -484,6 +493,11 @@ void run_slot_pipeline(Session& s, int nSlots, Fill fill, Finish finish) {
     cv.notify_all();
     writer.join();
     C.quiesce();
+    // The pinned staging (up to slots x batch bytes) stays cached per thread
+    // only for callers that opted into LZ4MT_MODE_DEVICE (repeated calls pay
+    // no re-pinning; lz4mtHipReleaseCaches() frees it).  A relinked default
+    // PARALLEL caller gets it freed at the end of every call.
+    if (!(s.mode() & LZ4MT_MODE_DEVICE)) C.release();
 }
 
 // Blocks per batch: ~512 MiB of input (at least one block); kSlots batches
@@ -503,12 +517,16 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
             s.quit(LZ4MT_RESULT_ERROR);
             return false;
         }
+        // One read() per block, as the reference does (src/lz4mt.cpp:435-450):
+        // a read of 0 ends the input; a short read is a short block, which
+        // closes this batch (a batch is blocks of bm bytes plus at most one
+        // short last block) -- the next batch carries on reading.
         uint64_t total = 0;
-        for (uint64_t j = 0; j < K; ++j) {   // one read() per block, as the reference does
+        for (uint64_t j = 0; j < K; ++j) {
             const int n = s.read(S.hIn + total, (int)bm);
             if (n <= 0) { *stop = true; break; }
             total += (uint64_t)n;
-            if ((uint32_t)n < bm) { *stop = true; break; }   // a short block is the last one
+            if ((uint32_t)n < bm) break;
         }
         if (total == 0) return false;
         uint64_t* dRecOff = nullptr;
@@ -524,7 +542,9 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
         if (sck) xs.update(S.hIn, total);   // serial content checksum overlaps the kernels
         return true;
     };
-    // the body size, D2H of the body, in-order write
+    // the body size, D2H of the body, then write() per record in the
+    // reference's pieces: size word, payload, [block checksum]
+    // (src/lz4mt.cpp:418-428), so a bounded sink sees the same calls
     auto finish = [&](Slot& S) -> bool {
         if (hipStreamSynchronize(S.st) != hipSuccess) { s.quit(LZ4MT_RESULT_ERROR); return false; }
         const uint64_t bodySize = S.hMeta[0];
@@ -533,10 +553,13 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
             s.quit(LZ4MT_RESULT_ERROR);
             return false;
         }
-        for (uint64_t o = 0; o < bodySize;) {   // write() takes int sizes
-            const int chunk = (int)std::min<uint64_t>(bodySize - o, 1u << 30);
-            if (!s.write(S.hOut + o, chunk)) return false;
-            o += (uint64_t)chunk;
+        for (uint64_t o = 0, b = 0; b < S.nb; ++b) {
+            const uint32_t len = get32(S.hOut + o) & ~kRawBit;
+            if (o + 4 + len + (bck ? 4 : 0) > bodySize) { s.quit(LZ4MT_RESULT_ERROR); return false; }
+            if (!s.write(S.hOut + o, 4) || !s.write(S.hOut + o + 4, (int)len) ||
+                (bck && !s.write(S.hOut + o + 4 + len, 4)))
+                return false;
+            o += 4 + (uint64_t)len + (bck ? 4 : 0);
         }
         return true;
     };
@@ -610,13 +633,13 @@ bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
         while (nb < K) {
             uint32_t bits = 0;
             if (s.readEof()) break;
-            if (!s.readU32(&bits)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_SIZE; break; }
+            if (!s.peekU32(&bits)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_SIZE; break; }
             if (bits == 0) { eos = true; break; }
             const uint32_t n = bits & ~kRawBit;
             if (n > bm) { pending = LZ4MT_RESULT_INVALID_BLOCK_SIZE; break; }
             if (s.read(S.hIn + used, (int)n) != (int)n) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_DATA; break; }
             uint32_t ck = 0;
-            if (bck && !s.readU32(&ck)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_CHECKSUM; break; }
+            if (bck && !s.peekU32(&ck)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_CHECKSUM; break; }
             S.hRecs[nb++] = BlockRec{used, bits, ck};
             used = (used + n + 15) & ~15ull;
         }
@@ -659,11 +682,20 @@ bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
         return true;
     };
     run_slot_pipeline(s, P.slots, fill, finish);
-    if (pending != LZ4MT_RESULT_OK) s.quit(pending);   // refines a read ERROR; a block's own failure wins
+    // a read failure found while filling comes after every batched block in
+    // stream order: it applies once they are written (a block's own failure
+    // wins); the reference sets ERROR and then this code (src/lz4mt.cpp:687-717)
+    if (pending != LZ4MT_RESULT_OK) s.quit(pending);
     return eos;
 }
 
 }  // namespace
+
+// Frees this thread's cached DEVICE-engine slots (pinned staging, device
+// buffers, streams); called by lz4mtHipReleaseCaches.
+namespace lz4mt {
+void release_slot_cache() { g_slots.release(); }
+}  // namespace lz4mt
 
 // ===========================================================================
 // public API
@@ -771,19 +803,21 @@ extern "C" Lz4MtResult lz4mtDecompress(Lz4MtContext* ctx, Lz4MtStreamDescriptor*
 }
 
 extern "C" const char* lz4mtResultToString(Lz4MtResult r) {
-    // Same strings as reference src/lz4mt_result.cpp:4-89; codes 16, 24 and
-    // 25 are named too (the reference prints "Unknown code" for them).
+    // Exactly the reference's table (src/lz4mt_result.cpp:4-89): it has no
+    // case for BLOCK_CHECKSUM_MISMATCH (16), INVALID_HEADER_SKIPPABLE_SIZE_
+    // UNREADABLE (24) or INVALID_HEADER_CANNOT_SKIP_SKIPPABLE_AREA (25), so
+    // those print "Unknown code" there and here.
     static const char* const names[] = {
         "OK", "ERROR", "INVALID_MAGIC_NUMBER", "INVALID_HEADER", "PRESET_DICTIONARY_IS_NOT_SUPPORTED_YET",
         "BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET", "INVALID_VERSION", "INVALID_HEADER_CHECKSUM",
         "INVALID_BLOCK_MAXIMUM_SIZE", "CANNOT_WRITE_HEADER", "CANNOT_WRITE_EOS", "CANNOT_WRITE_STREAM_CHECKSUM",
         "CANNOT_READ_BLOCK_SIZE", "CANNOT_READ_BLOCK_DATA", "CANNOT_READ_BLOCK_CHECKSUM",
-        "CANNOT_READ_STREAM_CHECKSUM", "BLOCK_CHECKSUM_MISMATCH", "STREAM_CHECKSUM_MISMATCH", "DECOMPRESS_FAIL",
+        "CANNOT_READ_STREAM_CHECKSUM", nullptr, "STREAM_CHECKSUM_MISMATCH", "DECOMPRESS_FAIL",
         "BAD_ARG", "INVALID_BLOCK_SIZE", "INVALID_HEADER_RESERVED1", "INVALID_HEADER_RESERVED2",
-        "INVALID_HEADER_RESERVED3", "INVALID_HEADER_SKIPPABLE_SIZE_UNREADABLE",
-        "INVALID_HEADER_CANNOT_SKIP_SKIPPABLE_AREA", "CANNOT_WRITE_DATA_BLOCK", "CANNOT_WRITE_DECODED_BLOCK"};
+        "INVALID_HEADER_RESERVED3", nullptr, nullptr, "CANNOT_WRITE_DATA_BLOCK", "CANNOT_WRITE_DECODED_BLOCK"};
     const unsigned i = (unsigned)r;
-    return i < sizeof(names) / sizeof(names[0]) ? names[i] : "Unknown code";
+    const char* s = i < sizeof(names) / sizeof(names[0]) ? names[i] : nullptr;
+    return s ? s : "Unknown code";
 }
 
 extern "C" int lz4mtResultToLz4cExitCode(Lz4MtResult r) {

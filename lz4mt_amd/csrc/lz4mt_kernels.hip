@@ -1990,6 +1990,28 @@ __global__ void __launch_bounds__(64) k_xxh32_frame_blocks(const uint8_t* __rest
     if (ok && (laneid() & 3u) == 0) digest[b] = h;
 }
 
+// XXH32 of consecutive `chunk`-byte pieces of one range (the last one
+// short), 16 pieces per wave, a lane quad per piece: the parallel "checksum
+// of checksums" the large-config tests and the multi-GPU check compare.
+__global__ void __launch_bounds__(64) k_xxh32_chunks(const uint8_t* __restrict__ p, uint64_t len, uint32_t chunk,
+                                                     uint32_t nChunks, uint32_t* __restrict__ digest) {
+    const uint32_t b = blockIdx.x * 16u + (laneid() >> 2);
+    const bool ok = b < nChunks;
+    const uint64_t off = ok ? (uint64_t)b * chunk : 0;
+    const uint32_t n = ok ? (uint32_t)min<uint64_t>(chunk, len - off) : 0u;
+    const uint32_t h = xxh32_quad(gptr(p) + off, n, gptr(p));
+    if (ok && (laneid() & 3u) == 0) digest[b] = h;
+}
+
+hipError_t launch_xxh32_chunks(const uint8_t* p, uint64_t len, uint32_t chunk, uint32_t* digest, hipStream_t st) {
+    if (len == 0 || chunk == 0) return hipSuccess;
+    const uint64_t nc = (len + chunk - 1) / chunk;
+    if (nc > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_xxh32_chunks, dim3((uint32_t)((nc + 15) / 16)), dim3(64), 0, st, p, len, chunk, (uint32_t)nc,
+                       digest);
+    return hipGetLastError();
+}
+
 // whole-stream XXH32 (lz4mt's serial content checksum): ONE wave, by design
 __global__ void __launch_bounds__(64) k_xxh32_stream(const uint8_t* __restrict__ p, uint64_t len,
                                                      uint32_t* __restrict__ digest) {

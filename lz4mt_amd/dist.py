@@ -13,9 +13,13 @@ does not shard is the stream (content) checksum, a single serial XXH32 chain
 One process per GPU (torch.distributed; backend "nccl" is RCCL on ROCm,
 "gloo" for CPU tests).  Compress: each rank encodes its contiguous block
 range locally, then the compressed record runs are gathered to the root (the
-only exchange step of the path).  Decompress: the host walks the size words
-(O(blocks)) and hands each rank a sub-frame of whole records -- no
-collective on the data path.
+only exchange step of the path, ``gather_frame``).  Decompress of one frame
+across ranks (``scatter_frame``): the root walks the size words on the
+device (lz4mtHipFrameRecords, O(blocks)), cuts the record table at the
+ranks' block ranges and sends each rank its run of whole records with
+grouped point-to-point transfers; each rank decodes header + records + EOS
+locally.  ``verify_stitched`` checks a stitched frame against every rank's
+source (root decode, per-shard chunk digests).
 """
 import struct
 
@@ -65,6 +69,10 @@ def _frame_layout(head):
         raise ValueError("block-dependent frames (-BD) do not shard")
     if flg & 0x04:
         raise ValueError("a stream checksum (FLG.2) is one serial chain and cannot be sharded; use -Sx")
+    if flg & 0x08:
+        # the content-size field (and the header checksum over it) describes
+        # one shard, not the stitched stream, nor a piece of a split frame
+        raise ValueError("a content-size field (FLG.3) does not survive sharding; leave streamSize unset")
     return 4 + header_length(flg), flg
 
 
@@ -181,3 +189,132 @@ def split_frame(frame, world):
         body = frame[recs[first][0]:recs[first + count - 1][1]] if count else b""
         out.append(head + body + EOS)
     return out
+
+
+def rank_blocks(nb, world, rank):
+    """(first block, block count) of ``rank`` when nb blocks are split as in ``shard_blocks``."""
+    per, rem = divmod(nb, world)
+    return rank * per + min(rank, rem), per + (1 if rank < rem else 0)
+
+
+def host_records(frame, frame_len=None):
+    """(header length, [record start offsets..., EOS offset]) of one -Sx frame by a host walk (CPU tensors, bytes)."""
+    b = frame[:frame_len].numpy().tobytes() if isinstance(frame, torch.Tensor) else bytes(frame[:frame_len])
+    hdr, recs, end = walk_records(b)
+    return hdr, [a for a, _ in recs] + [end - 4]
+
+
+def device_records(frame, frame_len=None):
+    """The same from the device walk (lz4mtHipFrameRecords) for a frame in HBM."""
+    import lz4mt_amd as L
+    hdr, starts, _ = L.frame_records(frame, frame_len)
+    return hdr, starts
+
+
+def scatter_frame(frame, frame_len, src=0, group=None, records=None, async_op=False):
+    """Cuts ONE -Sx frame held by ``src`` into per-rank sub-frames of whole
+    records and delivers piece r to rank r (the decompress side of SURVEY.md
+    §8(e): blocks are independent, src/lz4mt.cpp:914-918,991-995).
+
+    ``frame`` is the uint8 tensor on ``src`` (None elsewhere); ``records``
+    maps (frame, frame_len) to (header length, record starts + EOS offset):
+    default the device walk for device tensors, the host walk otherwise.
+    Rank r receives blocks ``rank_blocks(nb, world, r)`` as a valid frame
+    (the source header, its records, EOS) -- the same split ``shard_blocks``
+    makes of the content.  Exchange: one broadcast of the cut table
+    (header + 2 x u64 per rank), then grouped sends root -> peers straight
+    into each peer's buffer.  Returns the piece (and the works with
+    ``async_op``).
+    """
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    peer = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+    if rank == src:
+        dev = frame.device
+        recs_fn = records or (device_records if frame.is_cuda else host_records)
+        hdr, starts = recs_fn(frame, frame_len)
+        _frame_layout(bytes(frame[:hdr].cpu().numpy().tobytes()) + b"\0" * 8)
+        nb = len(starts) - 1
+        table = torch.zeros(4 + 2 * world, dtype=torch.int64)
+        table[0] = hdr
+        table[1:4] = torch.frombuffer(bytearray(frame[:hdr].cpu().numpy().tobytes().ljust(24, b"\0")),
+                                      dtype=torch.int64)
+        for r in range(world):
+            first, count = rank_blocks(nb, world, r)
+            table[4 + 2 * r] = starts[first]
+            table[5 + 2 * r] = starts[first + count] - starts[first]
+        table = table.to(dev)
+    else:
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
+            else torch.device("cpu")
+        table = torch.zeros(4 + 2 * world, dtype=torch.int64, device=dev)
+    dist.broadcast(table, peer(src), group=group)
+    t = table.cpu().tolist()
+    hdr = int(t[0])
+    head = torch.tensor(t[1:4], dtype=torch.int64).numpy().tobytes()[:hdr]
+    off, ln = int(t[4 + 2 * rank]), int(t[5 + 2 * rank])
+    piece = torch.empty(hdr + ln + 4, dtype=torch.uint8, device=dev)
+    works = []
+    if rank == src:
+        ops = [dist.P2POp(dist.isend, frame[int(t[4 + 2 * r]):int(t[4 + 2 * r]) + int(t[5 + 2 * r])], peer(r), group)
+               for r in range(world) if r != rank and int(t[5 + 2 * r])]
+        works = dist.batch_isend_irecv(ops) if ops else []
+        if ln:
+            piece[hdr:hdr + ln] = frame[off:off + ln]
+    elif ln:
+        works = dist.batch_isend_irecv([dist.P2POp(dist.irecv, piece[hdr:hdr + ln], peer(src), group)])
+    piece[:hdr] = torch.frombuffer(bytearray(head), dtype=torch.uint8).to(dev)
+    piece[hdr + ln:] = 0
+    if async_op:
+        return piece, works
+    for w in works:
+        w.wait()
+    return piece
+
+
+def _all_gather_var(t, group=None):
+    """all_gather of 1-D int64 tensors whose lengths differ by rank."""
+    world = dist.get_world_size(group)
+    n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+    ns = [torch.zeros(1, dtype=torch.int64, device=t.device) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    lens = [int(x.item()) for x in ns]
+    m = max(lens + [1])
+    pad = torch.zeros(m, dtype=torch.int64, device=t.device)
+    pad[:t.numel()] = t
+    bufs = [torch.zeros(m, dtype=torch.int64, device=t.device) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    return [b[:k] for b, k in zip(bufs, lens)]
+
+
+def verify_stitched(full, shard_src, decode, digests, dst=0, group=None):
+    """Checks a stitched frame (on ``dst``) against every rank's source shard.
+
+    Every rank passes its source ``shard_src`` (uint8 tensor); ``digests``
+    maps a uint8 tensor to an int64 tensor of chunk digests (e.g. XXH32 of
+    16 MiB pieces, lz4mtHipXxh32Chunks); ``decode`` maps the stitched frame
+    to its content (root only).  The root decodes once, cuts the content at
+    the shard sizes and compares each piece's digests with the all-gathered
+    ones.  Returns True on every rank iff all shards match.
+    """
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    mine = digests(shard_src).to(torch.int64)
+    sizes = _all_gather_var(torch.tensor([shard_src.numel()], dtype=torch.int64, device=mine.device), group)
+    allsum = _all_gather_var(mine, group)
+    ok = torch.ones(1, dtype=torch.int64, device=mine.device)
+    if rank == dst:
+        out = decode(full)
+        pos = 0
+        good = True
+        for r in range(world):
+            n = int(sizes[r].item())
+            piece = out[pos:pos + n]
+            if piece.numel() != n or not torch.equal(digests(piece).to(torch.int64).cpu(), allsum[r].cpu()):
+                good = False
+            pos += n
+        good = good and pos == out.numel()
+        ok[0] = 1 if good else 0
+    peer = dist.get_global_rank(group, dst) if group is not None else dst
+    dist.broadcast(ok, peer, group=group)
+    return bool(ok.item())

@@ -18,6 +18,11 @@ class FrameParams(ctypes.Structure):
                 ("streamSizeFlag", ctypes.c_int), ("streamSize", ctypes.c_uint64)]
 
 
+class KnownAnswer(ctypes.Structure):
+    _fields_ = [("frameSize", ctypes.c_uint64), ("frameXxh32", ctypes.c_uint32), ("frameChunks", ctypes.c_uint32),
+                ("contentXxh32", ctypes.c_uint32), ("contentChunks", ctypes.c_uint32)]
+
+
 def build():
     subprocess.run(["make", "-C", HERE, "-s"], check=True)
 
@@ -41,6 +46,10 @@ def _load():
     lib.orc_gen_random.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64]
     lib.orc_pipeline_roundtrip.argtypes = [u8p, sz, ctypes.POINTER(FrameParams), ctypes.c_int,
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz)]
+    lib.orc_pipeline_roundtrip_codec.argtypes = [u8p, sz, ctypes.POINTER(FrameParams), ctypes.c_int,
+                                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz), u8p, u8p]
+    lib.orc_stream_known_answer.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(FrameParams),
+                                            ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(KnownAnswer)]
     return lib
 
 
@@ -103,11 +112,39 @@ def gen_random(n, seed=7):
     return b.raw[:n]
 
 
-def pipeline_roundtrip(data_buf, n, p, threads):
-    """lz4mt-shaped CPU pipeline timing: (compress_s, decompress_s, frame_bytes)."""
+def pipeline_roundtrip(data_buf, n, p, threads, codec=None):
+    """lz4mt-shaped CPU pipeline timing: (compress_s, decompress_s, frame_bytes).
+
+    ``codec`` = (compress_fn_ptr, decompress_fn_ptr) with the LZ4 signatures
+    lz4mt binds (e.g. from liblz4.so.1, see ``liblz4_codec``); None = this
+    restatement."""
     secs = (ctypes.c_double * 2)()
     fs = ctypes.c_size_t(0)
-    err = lib.orc_pipeline_roundtrip(data_buf, n, ctypes.byref(p), threads, secs, ctypes.byref(fs))
+    cf, df = codec if codec else (None, None)
+    err = lib.orc_pipeline_roundtrip_codec(data_buf, n, ctypes.byref(p), threads, secs, ctypes.byref(fs), cf, df)
     if err:
         raise RuntimeError("oracle pipeline decode error")
     return secs[0], secs[1], fs.value
+
+
+def liblz4_codec(path="liblz4.so.1"):
+    """(compress, decompress, version) function pointers of the system liblz4
+    -- the library lz4mt links (src/main.cpp:749-751, 774) -- or None."""
+    try:
+        lz = ctypes.CDLL(path)
+    except OSError:
+        return None
+    lz.LZ4_versionNumber.restype = ctypes.c_int
+    v = lz.LZ4_versionNumber()
+    cf = ctypes.cast(lz.LZ4_compress_limitedOutput, ctypes.c_void_p).value
+    df = ctypes.cast(lz.LZ4_decompress_safe, ctypes.c_void_p).value
+    return (cf, df), f"{v // 10000}.{v // 100 % 100}.{v % 100}", lz
+
+
+def known_answer(n, p, seed=42, chunk=16 << 20, threads=8):
+    """Streamed known answer of the App. F input (``orc_stream_known_answer``)."""
+    ka = KnownAnswer()
+    if lib.orc_stream_known_answer(n, seed, ctypes.byref(p), threads, chunk, ctypes.byref(ka)) != 0:
+        raise RuntimeError("known answer failed")
+    return {"frame_size": ka.frameSize, "frame_xxh32": ka.frameXxh32, "frame_chunks": ka.frameChunks,
+            "content_xxh32": ka.contentXxh32, "content_chunks": ka.contentChunks}

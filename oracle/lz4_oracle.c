@@ -244,7 +244,14 @@ typedef long long sll;
 
 static void lz77_copy(uint8_t* dst, sll op, sll match, sll len) {
     if (match == op) { memset(dst + op, 0, (size_t)len); return; } /* offset 0 => zeros */
-    for (sll i = 0; i < len; i++) dst[op + i] = dst[match + i];
+    uint8_t* d = dst + op;
+    const uint8_t* s = dst + match;
+    const sll off = op - match;
+    if (off >= len) { memcpy(d, s, (size_t)len); return; }   /* no overlap */
+    sll i = 0;
+    if (off >= 8) /* 8-byte pieces: each piece's source lies before its target */
+        for (; i + 8 <= len; i += 8) memcpy(d + i, s + i, 8);
+    for (; i < len; i++) d[i] = s[i];                         /* short-period runs */
 }
 
 /* read_variable_length(): returns -1 initial error, -2 loop error. */
@@ -666,6 +673,7 @@ void orc_gen_random(uint8_t* dst, uint64_t n, uint64_t seed) {
 /* ===================================================================== */
 typedef struct {
     const uint8_t* src; size_t n, bm, nb; const orc_frame_params* p; int decode;
+    orc_codec_fn cfn, dfn;
     uint8_t** out; int* res; int* done; uint8_t** cin; int* clen; int* craw;
     size_t next, written; pthread_mutex_t mu; pthread_cond_t cv; size_t npool;
     orc_xxh32_state sx; size_t frameBytes; int err;
@@ -681,10 +689,10 @@ static void* pipe_worker(void* a) {
         pthread_mutex_unlock(&c->mu);
         const size_t off = i * c->bm, len = c->n - off < c->bm ? c->n - off : c->bm;
         if (!c->decode) {
-            c->res[i] = orc_lz4_compress(c->src + off, c->out[i % c->npool], (int)len, (int)len);
+            c->res[i] = c->cfn((const char*)c->src + off, (char*)c->out[i % c->npool], (int)len, (int)len);
         } else {
             if (c->craw[i]) { memcpy(c->out[i % c->npool], c->cin[i], (size_t)c->clen[i]); c->res[i] = c->clen[i]; }
-            else c->res[i] = orc_lz4_decompress_safe(c->cin[i], c->out[i % c->npool], c->clen[i], (int)c->bm);
+            else c->res[i] = c->dfn((const char*)c->cin[i], (char*)c->out[i % c->npool], c->clen[i], (int)c->bm);
         }
         /* in-order write chain */
         pthread_mutex_lock(&c->mu);
@@ -726,13 +734,27 @@ static void pipe_run(pipe_ctx* c, int nthreads) {
     for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
 }
 
+static int own_compress(const char* s, char* d, int n, int cap) {
+    return orc_lz4_compress((const uint8_t*)s, (uint8_t*)d, n, cap);
+}
+static int own_decompress(const char* s, char* d, int n, int cap) {
+    return orc_lz4_decompress_safe((const uint8_t*)s, (uint8_t*)d, n, cap);
+}
+
 int orc_pipeline_roundtrip(const uint8_t* src, size_t n, const orc_frame_params* p, int nthreads, double* secs,
                            size_t* frameSize) {
+    return orc_pipeline_roundtrip_codec(src, n, p, nthreads, secs, frameSize, NULL, NULL);
+}
+
+int orc_pipeline_roundtrip_codec(const uint8_t* src, size_t n, const orc_frame_params* p, int nthreads,
+                                 double* secs, size_t* frameSize, orc_codec_fn cfn, orc_codec_fn dfn) {
     const size_t bm = block_max(p->blockMaxId), nb = (n + bm - 1) / bm;
     const size_t npool = (size_t)nthreads + 1;
     pipe_ctx c;
     memset(&c, 0, sizeof(c));
     c.src = src; c.n = n; c.bm = bm; c.nb = nb; c.p = p; c.npool = npool;
+    c.cfn = cfn ? cfn : own_compress;
+    c.dfn = dfn ? dfn : own_decompress;
     c.out = (uint8_t**)malloc(npool * sizeof(uint8_t*));
     for (size_t i = 0; i < npool; i++) c.out[i] = (uint8_t*)malloc(bm);
     c.res = (int*)calloc(nb + 1, sizeof(int));
@@ -754,7 +776,7 @@ int orc_pipeline_roundtrip(const uint8_t* src, size_t n, const orc_frame_params*
     uint8_t* tmp = (uint8_t*)malloc(bm);
     for (size_t i = 0; i < nb; i++) {
         const size_t off = i * bm, len = n - off < bm ? n - off : bm;
-        const int cs = orc_lz4_compress(src + off, tmp, (int)len, (int)len);
+        const int cs = c.cfn((const char*)src + off, (char*)tmp, (int)len, (int)len);
         c.craw[i] = cs <= 0;
         c.clen[i] = cs > 0 ? cs : (int)len;
         c.cin[i] = (uint8_t*)malloc((size_t)c.clen[i] + 1);
@@ -772,4 +794,92 @@ int orc_pipeline_roundtrip(const uint8_t* src, size_t n, const orc_frame_params*
     for (size_t i = 0; i < npool; i++) free(c.out[i]);
     free(c.cin); free(c.clen); free(c.craw); free(c.out); free(c.res); free(c.done);
     return c.err;
+}
+
+/* ===================================================================== */
+/* Known answers for large configs, streamed (no whole-input buffer):     */
+/* the App. F input of n bytes (seed), framed as lz4mt writes it          */
+/* (orc_frame_compress, ref src/lz4mt.cpp:898-935), batch by batch.       */
+/* Reports the frame size, XXH32 of the frame and of the content, and a   */
+/* "checksum of checksums" for each: XXH32 over the little-endian u32     */
+/* XXH32 digests of consecutive `chunk`-byte pieces (the last one short). */
+/* ===================================================================== */
+typedef struct { orc_xxh32_state whole, piece, list; uint64_t fill, chunk, count; } chunked_hash;
+
+static void ch_reset(chunked_hash* h, uint64_t chunk) {
+    orc_xxh32_reset(&h->whole, 0); orc_xxh32_reset(&h->piece, 0); orc_xxh32_reset(&h->list, 0);
+    h->fill = 0; h->chunk = chunk; h->count = 0;
+}
+static void ch_close_piece(chunked_hash* h) {
+    uint8_t b[4];
+    wr32(b, orc_xxh32_digest(&h->piece));
+    orc_xxh32_update(&h->list, b, 4);
+    orc_xxh32_reset(&h->piece, 0);
+    h->fill = 0; h->count++;
+}
+static void ch_update(chunked_hash* h, const uint8_t* p, size_t len) {
+    orc_xxh32_update(&h->whole, p, len);
+    while (len) {
+        size_t take = (size_t)(h->chunk - h->fill);
+        if (take > len) take = len;
+        orc_xxh32_update(&h->piece, p, take);
+        h->fill += take; p += take; len -= take;
+        if (h->fill == h->chunk) ch_close_piece(h);
+    }
+}
+static void ch_finish(chunked_hash* h) { if (h->fill) ch_close_piece(h); }
+
+int orc_stream_known_answer(uint64_t n, uint64_t seed, const orc_frame_params* p, int nthreads, uint64_t chunk,
+                            orc_known_answer* ka) {
+    if (p->blockMaxId < 4 || p->blockMaxId > 7 || chunk == 0) return -1;
+    const size_t bm = block_max(p->blockMaxId);
+    const size_t batchBlocks = (256u << 20) / bm;          /* 256 MiB of input per batch */
+    const size_t batch = batchBlocks * bm;
+    uint8_t* in = (uint8_t*)malloc(batch);
+    uint8_t* tmp = (uint8_t*)malloc(batch);
+    uint8_t* rec = (uint8_t*)malloc(batch + batchBlocks * 8 + 64);
+    int* csz = (int*)malloc(batchBlocks * sizeof(int));
+    if (!in || !tmp || !rec || !csz) { free(in); free(tmp); free(rec); free(csz); return -1; }
+    chunked_hash fh, chh;
+    ch_reset(&fh, chunk); ch_reset(&chh, chunk);
+    uint8_t hdr[32];
+    const size_t hl = write_header(hdr, p);
+    ch_update(&fh, hdr, hl);
+    uint64_t frameSize = hl;
+    for (uint64_t off = 0; off < n; off += batch) {
+        const size_t len = (size_t)(n - off < batch ? n - off : batch);
+        /* segment i of the stream starts from seed + i*G (App. F), so a batch
+           at a 64 KiB-aligned offset is generated on its own */
+        orc_gen_synthetic(in, len, seed + (off >> 16) * GOLDEN);
+        ch_update(&chh, in, len);
+        const size_t nb = (len + bm - 1) / bm;
+        cjob j = { in, len, bm, tmp, csz };
+        parallel_for(nb, nthreads, cjob_fn, &j);
+        size_t o = 0;
+        for (size_t i = 0; i < nb; i++) {
+            const size_t bo = i * bm, bl = len - bo < bm ? len - bo : bm;
+            const uint8_t* stored = csz[i] <= 0 ? in + bo : tmp + bo;
+            const size_t slen = csz[i] <= 0 ? bl : (size_t)csz[i];
+            wr32(rec + o, csz[i] <= 0 ? (uint32_t)bl | RAW_BIT : (uint32_t)csz[i]); o += 4;
+            memcpy(rec + o, stored, slen); o += slen;
+            if (p->blockChecksum) { wr32(rec + o, orc_xxh32(stored, slen, 0)); o += 4; }
+        }
+        ch_update(&fh, rec, o);
+        frameSize += o;
+    }
+    ch_finish(&chh);
+    uint8_t tail[8];
+    size_t tl = 4;
+    wr32(tail, 0);
+    if (p->streamChecksum) { wr32(tail + 4, orc_xxh32_digest(&chh.whole)); tl = 8; }
+    ch_update(&fh, tail, tl);
+    frameSize += tl;
+    ch_finish(&fh);
+    ka->frameSize = frameSize;
+    ka->frameXxh32 = orc_xxh32_digest(&fh.whole);
+    ka->frameChunks = orc_xxh32_digest(&fh.list);
+    ka->contentXxh32 = orc_xxh32_digest(&chh.whole);
+    ka->contentChunks = orc_xxh32_digest(&chh.list);
+    free(in); free(tmp); free(rec); free(csz);
+    return 0;
 }

@@ -89,6 +89,26 @@ void orc_gen_random(uint8_t* dst, uint64_t n, uint64_t seed);
 int orc_pipeline_roundtrip(const uint8_t* src, size_t n,
                            const orc_frame_params* p, int nthreads,
                            double* secs, size_t* frameSize);
+/* The same pipeline over a caller-supplied block codec with the LZ4
+ * signatures lz4mt binds (LZ4_compress_limitedOutput / LZ4_decompress_safe,
+ * e.g. dlopen'd from liblz4.so.1); NULL = this restatement. */
+typedef int (*orc_codec_fn)(const char* src, char* dst, int n, int cap);
+int orc_pipeline_roundtrip_codec(const uint8_t* src, size_t n,
+                                 const orc_frame_params* p, int nthreads,
+                                 double* secs, size_t* frameSize,
+                                 orc_codec_fn compress, orc_codec_fn decompress);
+
+/* ---- streamed known answers for large configs ------------------------- */
+typedef struct {
+    uint64_t frameSize;
+    uint32_t frameXxh32, frameChunks;      /* XXH32 of the frame; of its chunk digests */
+    uint32_t contentXxh32, contentChunks;  /* the same for the content */
+} orc_known_answer;
+/* Frames the App. F input of n bytes (seed) batch by batch without holding
+ * it whole.  "Chunks" = XXH32 over the LE u32 XXH32 digests of consecutive
+ * `chunk`-byte pieces (the last one short).  Returns 0 on success. */
+int orc_stream_known_answer(uint64_t n, uint64_t seed, const orc_frame_params* p,
+                            int nthreads, uint64_t chunk, orc_known_answer* ka);
 
 #ifdef __cplusplus
 }

@@ -45,3 +45,20 @@ def with_stream_size(frame, n):
     desc = bytes([flg, bd]) + struct.pack("<Q", n)
     hc = (xxhash.xxh32(desc, seed=0).intdigest() >> 8) & 0xFF
     return frame[:4] + desc + bytes([hc]) + frame[7:]
+
+
+@pytest.fixture(scope="session")
+def known_answers():
+    with open(os.path.join(GOLDEN, "known_answers.json")) as f:
+        return json.load(f)
+
+
+def checksum_of_checksums(t, chunk=16 << 20):
+    """XXH32 over the little-endian u32 XXH32 digests of consecutive ``chunk``
+    pieces of a device tensor (the "chunks" values of known_answers.json);
+    the digests come from the library (lz4mtHipXxh32Chunks)."""
+    import xxhash
+
+    import lz4mt_amd as L
+    d = L.xxh32_chunks(t, chunk).cpu().numpy().astype("<u4").tobytes()
+    return xxhash.xxh32(d).intdigest()

@@ -1,8 +1,10 @@
-"""Multi-process (gloo, world_size 2) tests of the block-sharded frame path
-(lz4mt_amd/dist.py).  CPU only: each rank compresses its
-block range with the oracle (the checker), the record runs are gathered
-over torch.distributed, and the stitched frame must equal the oracle's frame
-of the whole stream byte for byte."""
+"""Multi-process (gloo, world_size 2 and 3) tests of the block-sharded frame
+path (lz4mt_amd/dist.py) -- the same gather / scatter /
+verify orchestration bench.py runs over RCCL at N > 1.  CPU only: each rank
+compresses its block range with the oracle (the checker), the record runs
+are gathered over torch.distributed, and the stitched frame must equal the
+oracle's frame of the whole stream byte for byte; the root then scatters
+that frame back and every rank decodes its own block range."""
 import os
 import socket
 
@@ -117,4 +119,88 @@ def test_split_frame_decodes_to_slices(world):
 def test_stream_checksum_frames_refuse_to_shard():
     frame = oracle.compress_frame(oracle.gen_synthetic(70000, 1), oracle.params(4, True, False))
     with pytest.raises(ValueError, match="serial"):
+        D.split_frame(frame, 2)
+
+
+def _digests(t, chunk=1 << 16):
+    import xxhash
+    b = t.numpy().tobytes()
+    return torch.tensor([xxhash.xxh32(b[i:i + chunk]).intdigest() for i in range(0, len(b), chunk)],
+                        dtype=torch.int64)
+
+
+def _roundtrip_worker(rank, world, port, n, block_id, q, corrupt_rank=None):
+    """bench.py's N > 1 step on the CPU: local frame -> gather to root ->
+    verify the stitched frame against every shard -> scatter it back ->
+    decode the own piece."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data = oracle.gen_synthetic(n, 42)
+        bm = D.block_bytes(block_id)
+        off, ln, _, _ = D.shard_blocks(n, bm, world, rank)
+        shard = data[off:off + ln]
+        p = oracle.params(block_id, stream_checksum=False, block_checksum=True)
+        local = oracle.compress_frame(shard, p)
+        full = D.gather_frame(torch.frombuffer(bytearray(local), dtype=torch.uint8), len(local))
+        src = bytearray(shard)
+        if rank == corrupt_rank and src:
+            src[len(src) // 2] ^= 1
+        ok = D.verify_stitched(full, torch.frombuffer(src, dtype=torch.uint8) if src else torch.zeros(0, dtype=torch.uint8),
+                               decode=lambda f: torch.frombuffer(bytearray(
+                                   oracle.decompress_frame(f.numpy().tobytes(), n + bm)[1]) or bytearray(1),
+                                   dtype=torch.uint8)[:n],
+                               digests=_digests)
+        piece = D.scatter_frame(full if rank == 0 else None, full.numel() if rank == 0 else 0)
+        rc, dec = oracle.decompress_frame(piece.numpy().tobytes(), ln + bm)
+        q.put((rank, ok, rc == 0 and dec == shard, piece.numel()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_roundtrip(world, n, block_id, corrupt_rank=None):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_roundtrip_worker, args=(r, world, port, n, block_id, q, corrupt_rank))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world,n,block_id", [(2, 17 * 65536 + 12345, 4), (3, 7 * 262144 + 5, 5), (3, 65536 + 9, 4)])
+def test_gather_verify_scatter_roundtrip(world, n, block_id):
+    res = _run_roundtrip(world, n, block_id)
+    assert all(ok for _, ok, _, _ in res), res           # stitched frame matches every shard
+    assert all(dec for _, _, dec, _ in res), res         # each scattered piece decodes to its shard
+
+
+def test_verify_stitched_catches_a_bad_shard():
+    res = _run_roundtrip(2, 9 * 65536, 4, corrupt_rank=1)
+    assert not any(ok for _, ok, _, _ in res), res
+
+
+def test_scatter_pieces_are_the_shard_frames():
+    """The pieces the scatter makes are byte for byte the frames each rank
+    would write for its own shard (same header, its records, EOS)."""
+    n, bid, world = 11 * 65536 + 77, 4, 3
+    data = oracle.gen_synthetic(n, 42)
+    p = oracle.params(bid, False, True)
+    frame = oracle.compress_frame(data, p)
+    hdr, starts = D.host_records(torch.frombuffer(bytearray(frame), dtype=torch.uint8))
+    for r in range(world):
+        first, count = D.rank_blocks(len(starts) - 1, world, r)
+        off, ln, _, _ = D.shard_blocks(n, 65536, world, r)
+        piece = frame[:hdr] + frame[starts[first]:starts[first + count]] + D.EOS
+        assert piece == oracle.compress_frame(data[off:off + ln], p)
+
+
+def test_stream_size_frames_refuse_to_shard():
+    frame = oracle.compress_frame(oracle.gen_synthetic(70000, 1), oracle.params(4, False, True, stream_size=70000))
+    with pytest.raises(ValueError, match="FLG.3"):
         D.split_frame(frame, 2)

@@ -1,4 +1,8 @@
-"""One compress + decompress of N GiB (default 2) for PMC profiling."""
+"""One compress + decompress of N GiB (default 8) for PMC profiling.
+--random: splitmix64 bytes instead of App. F (every block stored raw): the
+encoder then streams its source exactly once and the decoder copies raw
+blocks, so FETCH_SIZE of those launches is measured against a known byte
+count (the calibration tools/pmcsum.py records)."""
 import os
 import sys
 
@@ -7,9 +11,14 @@ import torch  # noqa: E402
 
 import lz4mt_amd as L  # noqa: E402
 
-gib = float(sys.argv[1]) if len(sys.argv) > 1 else 2.0
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+gib = float(args[0]) if args else 8.0
 n = int(gib * (1 << 30))
-src = L.gen_synthetic(n)
+if "--random" in sys.argv:
+    g = torch.Generator(device="cuda").manual_seed(5)
+    src = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+else:
+    src = L.gen_synthetic(n)
 sd = L.make_sd(7, False, True)
 fr = L.compress_frame(src, sd)
 out, r = L.decompress_frame(fr)
