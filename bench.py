@@ -157,10 +157,15 @@ def pmc_traffic(kernel, n, bm, flg):
     k = prof.get("kernels", {}).get(kernel)
     if not k:
         return None, f"{kernel} not in the profile"
-    cal = prof.get("calibration", {}).get(kernel) or prof.get("calibration", {}).get("default")
-    f = cal["fetch_factor"] if cal else 0.5
-    return {"bytes": k["fetch_bytes"] / f + k["write_bytes"], "fetch_raw": k["fetch_bytes"],
-            "write": k["write_bytes"], "fetch_factor": f, "calibration": cal.get("how") if cal else "guide x2",
+    cal = prof.get("calibration", {}).get(kernel) or {}
+    fr = k["fetch_bytes"]
+    if "stream_factor" in cal:   # a streamed part of known size + the rest at its own factor
+        sb = cal["stream_bytes"]
+        fetch = sb + max(0.0, fr - cal["stream_factor"] * sb) / cal["other_factor"]
+    else:
+        fetch = fr / cal.get("fetch_factor", 0.5)
+    return {"bytes": fetch + k["write_bytes"], "fetch_raw": fr, "fetch_calibrated": round(fetch),
+            "write": k["write_bytes"], "calibration": cal.get("how", "guide x2 (uncalibrated)"),
             "source": "profiles/pmc_current.json (" + prof.get("tag", "?") + ")"}, None
 
 
