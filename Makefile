@@ -6,7 +6,8 @@ HIPFLAGS ?= $(EXTRA) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unus
 BUILD  := build
 CSRC   := lz4mt_amd/csrc
 LIB    := lz4mt_amd/liblz4mt_amd.so
-OBJS   := $(BUILD)/lz4mt_kernels_enc.o $(BUILD)/lz4mt_kernels_dec.o $(BUILD)/lz4mt_engine.o $(BUILD)/lz4mt_frame.o $(BUILD)/lz4mt_io.o
+OBJS   := $(BUILD)/lz4mt_kernels_enc.o $(BUILD)/lz4mt_kernels_dec.o $(BUILD)/lz4mt_hc.o $(BUILD)/lz4mt_engine.o \
+          $(BUILD)/lz4mt_frame.o $(BUILD)/lz4mt_io.o
 HDRS   := $(CSRC)/lz4mt_device.h $(CSRC)/lz4mt_host.h include/lz4mt.h include/lz4mt_hip.h include/lz4mt_io.h
 
 all: $(LIB) oracle

@@ -35,8 +35,10 @@ extern "C" {
 /* ---- 1. block operators (reference plugin signatures) ------------------ */
 /* LZ4_compress_limitedOutput semantics (lz4 1.9.3, acceleration 1):
  * returns the compressed size, or 0 when it does not fit maxOutputSize.
- * compressionLevel >= 3 (HC) is not provided on the GPU: returns 0, so the
- * block is stored raw (a valid frame, but not LZ4-HC bytes). */
+ * compressionLevel 3..9: LZ4_compressHC2_limitedOutput (LZ4-HC 1.9.3 hash
+ * chain), the codec the reference wires for those levels
+ * (src/main.cpp:778-785).  Levels 10..12 (lz4's optimal parser) are not
+ * provided: 0, so the block is stored raw. */
 int lz4mtHipCompressBlock(const char* src, char* dst, int isize, int maxOutputSize, int compressionLevel);
 /* LZ4_compressBound. */
 int lz4mtHipCompressBound(int isize);
@@ -51,8 +53,10 @@ uint64_t lz4mtHipCompressWorkspaceSize(uint64_t srcSize, const Lz4MtStreamDescri
 /* Compresses d_src[0..srcSize) into one frame at d_frame (device memory).
  * d_workspace may be NULL (the library then allocates and frees scratch).
  * *frameSize (host) receives the frame length; the call synchronises the
- * stream once at the end to read it.  Block independence is required
- * (blockIndependence = 0 returns BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET). */
+ * stream once at the end to read it.  blockIndependence = 0 writes a
+ * block-dependent (-BD) frame: one wavefront encodes the blocks in order,
+ * each against the 64 KiB before it (lz4's streaming compressor, as the
+ * reference's compressBlockDependency calls it). */
 Lz4MtResult lz4mtHipCompressFrame(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
                                   uint64_t* frameSize, const Lz4MtStreamDescriptor* sd,
                                   void* d_workspace, uint64_t workspaceSize, void* stream);
@@ -61,6 +65,18 @@ Lz4MtResult lz4mtHipCompressFrame(const void* d_src, uint64_t srcSize, void* d_f
 Lz4MtResult lz4mtHipCompressFrameAsync(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
                                        uint64_t* d_frameSize, const Lz4MtStreamDescriptor* sd,
                                        void* d_workspace, uint64_t workspaceSize, void* stream);
+
+/* The same with a compression level: 0..2 fast LZ4, 3..9 LZ4-HC (the
+ * workspace then holds 2 more bytes per input byte: use
+ * lz4mtHipCompressWorkspaceSizeEx).  BAD_ARG for levels 10..12 and for HC
+ * on block-dependent frames. */
+uint64_t lz4mtHipCompressWorkspaceSizeEx(uint64_t srcSize, const Lz4MtStreamDescriptor* sd, int level);
+Lz4MtResult lz4mtHipCompressFrameEx(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
+                                    uint64_t* frameSize, const Lz4MtStreamDescriptor* sd, int level,
+                                    void* d_workspace, uint64_t workspaceSize, void* stream);
+Lz4MtResult lz4mtHipCompressFrameAsyncEx(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
+                                         uint64_t* d_frameSize, const Lz4MtStreamDescriptor* sd, int level,
+                                         void* d_workspace, uint64_t workspaceSize, void* stream);
 
 /* Parses the frame header at d_frame (one small device->host copy) and
  * reports its descriptor, header length and an upper bound of the decoded

@@ -55,10 +55,11 @@ def result_to_exit_code(code):
     return lib.lz4mtResultToLz4cExitCode(int(code))
 
 
-def make_sd(block_max_id=7, stream_checksum=True, block_checksum=False, stream_size=None):
-    """Stream descriptor with the CLI's flag mapping (-B#, -BX, -Sx)."""
+def make_sd(block_max_id=7, stream_checksum=True, block_checksum=False, stream_size=None, block_dependence=False):
+    """Stream descriptor with the CLI's flag mapping (-B#, -BX, -BD, -Sx)."""
     sd = init_stream_descriptor()
     sd.bd.blockMaximumSize = block_max_id
+    sd.flg.blockIndependence = 0 if block_dependence else 1
     sd.flg.streamChecksum = 1 if stream_checksum else 0
     sd.flg.blockChecksum = 1 if block_checksum else 0
     if stream_size is not None:
@@ -158,14 +159,15 @@ def frame_bound(n, sd=None):
     return int(lib.lz4mtHipFrameBound(int(n), ctypes.byref(sd)))
 
 
-def compress_workspace(n, sd=None, device=None):
+def compress_workspace(n, sd=None, device=None, level=0):
     sd = sd if sd is not None else init_stream_descriptor()
-    nbytes = int(lib.lz4mtHipCompressWorkspaceSize(int(n), ctypes.byref(sd)))
+    nbytes = int(lib.lz4mtHipCompressWorkspaceSizeEx(int(n), ctypes.byref(sd), int(level)))
     return torch.empty(nbytes, dtype=torch.uint8, device=device or "cuda")
 
 
-def compress_frame(src, sd=None, out=None, workspace=None, stream=None):
-    """Compresses a device tensor into one lz4mt frame; returns the frame tensor (a view of ``out``)."""
+def compress_frame(src, sd=None, out=None, workspace=None, stream=None, level=0):
+    """Compresses a device tensor into one lz4mt frame; returns the frame tensor (a view of ``out``).
+    ``level`` 3..9 selects LZ4-HC (the reference's codec for those levels)."""
     _check_dev(src, "src")
     sd = sd if sd is not None else init_stream_descriptor()
     n = src.numel()
@@ -174,9 +176,9 @@ def compress_frame(src, sd=None, out=None, workspace=None, stream=None):
         out = torch.empty(cap, dtype=torch.uint8, device=src.device)
     fs = ctypes.c_uint64(0)
     ws_ptr, ws_size = (workspace.data_ptr(), workspace.numel()) if workspace is not None else (None, 0)
-    r = lib.lz4mtHipCompressFrame(ctypes.c_void_p(src.data_ptr() if n else out.data_ptr()), n,
-                                  ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.byref(fs),
-                                  ctypes.byref(sd), ctypes.c_void_p(ws_ptr), ws_size, _stream(stream))
+    r = lib.lz4mtHipCompressFrameEx(ctypes.c_void_p(src.data_ptr() if n else out.data_ptr()), n,
+                                    ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.byref(fs),
+                                    ctypes.byref(sd), int(level), ctypes.c_void_p(ws_ptr), ws_size, _stream(stream))
     if r != Result.OK:
         raise Lz4MtError(r, "lz4mtHipCompressFrame")
     return out[:fs.value]

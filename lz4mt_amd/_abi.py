@@ -95,6 +95,11 @@ PROTOTYPES = {
                                       c_void_p, c_uint64, c_void_p]),
     "lz4mtHipCompressFrameAsync": (c_int, [c_void_p, c_uint64, c_void_p, c_uint64, c_void_p, SD_P, c_void_p,
                                            c_uint64, c_void_p]),
+    "lz4mtHipCompressWorkspaceSizeEx": (c_uint64, [c_uint64, SD_P, c_int]),
+    "lz4mtHipCompressFrameEx": (c_int, [c_void_p, c_uint64, c_void_p, c_uint64, ctypes.POINTER(c_uint64), SD_P,
+                                        c_int, c_void_p, c_uint64, c_void_p]),
+    "lz4mtHipCompressFrameAsyncEx": (c_int, [c_void_p, c_uint64, c_void_p, c_uint64, c_void_p, SD_P, c_int,
+                                             c_void_p, c_uint64, c_void_p]),
     "lz4mtHipFrameInfo": (c_int, [c_void_p, c_uint64, SD_P, ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64),
                                   c_void_p]),
     "lz4mtHipDecompressFrame": (c_int, [c_void_p, c_uint64, c_void_p, c_uint64, ctypes.POINTER(c_uint64), SD_P,

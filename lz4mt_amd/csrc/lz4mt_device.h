@@ -25,6 +25,21 @@ struct BlockRec {
     uint32_t checksum;   // block XXH32 read from the frame (if FLG.4)
 };
 
+// Per-block lz4 stream state of a block-dependent (-BD) frame's encode
+// (see k_encode_linked): catch-up lower bounds for candidates in the block /
+// in the history and the dictSmall limit, in coordinates where the block
+// starts at 65536 and its 64 KiB history is [0, 65536).
+struct LinkPlan {
+    uint32_t lowIn, lowDict, candLow, pad;
+};
+
+// Device state of a block-dependent encode: per-block plans, the carried table.
+struct LinkState {
+    LinkPlan* plan;
+    uint32_t* table;
+    bool fresh;
+};
+
 // Frame-walk summary written by the walk kernel.
 struct WalkInfo {
     uint64_t endPos;     // position just after the EOS word
@@ -97,5 +112,17 @@ hipError_t launch_encode_stats(const uint8_t* src, uint64_t srcSize, uint32_t bl
 hipError_t launch_decode_stats(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax,
                                uint8_t* out, uint64_t outCap, int32_t* dsize, uint64_t* stats, hipStream_t st);
 hipError_t launch_gen_synthetic(uint8_t* dst, uint64_t n, uint64_t seed, hipStream_t st);
+// LZ4-HC (lz4mt_hc.hip): level 1..9 (lz4 1.9.3 hash chain); `delta` is
+// scratch of 2 bytes per input byte.  hipErrorInvalidValue for levels > 9.
+hipError_t launch_encode_hc(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                            uint8_t* slots, uint64_t slotStride, uint32_t capOverride, int level, uint16_t* delta,
+                            int32_t* csize, hipStream_t st);
+uint32_t hc_attempts(int level);   // 0 for levels the library does not run (10..12)
+hipError_t launch_encode_linked(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                                uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh, int32_t* csize,
+                                hipStream_t st);
+hipError_t launch_decode_linked(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax,
+                                uint8_t* out, uint64_t outCap, uint8_t* slot, uint8_t* hist, const uint32_t* digest,
+                                int blockChecksum, int32_t* dsize, int32_t* status, hipStream_t st);
 
 }  // namespace lz4mt

@@ -56,6 +56,7 @@ thread_local Timing g_timing;
 // ---- workspace layout for one compressed frame ----------------------------
 struct CompressWs {
     uint8_t* slots;
+    uint16_t* delta;   // LZ4-HC hash chain (level >= 3 only)
     int32_t* csize;
     uint32_t* bsum;
     uint64_t* recOff;
@@ -64,11 +65,12 @@ struct CompressWs {
     uint64_t bytes;
 };
 
-CompressWs carve_compress(uint8_t* base, uint64_t nb, uint64_t bm) {
+CompressWs carve_compress(uint8_t* base, uint64_t nb, uint64_t bm, int level = 0) {
     CompressWs w{};
     uint64_t o = 0;
     auto take = [&](uint64_t n) { uint8_t* p = base ? base + o : nullptr; o = align_up(o + n, 256); return p; };
     w.slots = take(nb * bm + 64);
+    w.delta = level >= 3 ? reinterpret_cast<uint16_t*>(take(nb * bm * 2 + 64)) : nullptr;
     w.csize = reinterpret_cast<int32_t*>(take((nb + 1) * 4));
     w.bsum = reinterpret_cast<uint32_t*>(take((nb + 1) * 4));
     w.recOff = reinterpret_cast<uint64_t*>(take((nb + 1) * 8));
@@ -91,10 +93,19 @@ struct BlockScratch {
     uint64_t capIn = 0, capOut = 0;
     int32_t* dRes = nullptr;
     BlockRec* dRec = nullptr;
+    uint16_t* dDelta = nullptr;   // LZ4-HC hash chain
+    uint64_t capDelta = 0;
     int dev = -1;
+    bool ensure_delta(uint64_t n) {
+        if (dDelta && n <= capDelta) return true;
+        hipFree(dDelta);
+        capDelta = std::max<uint64_t>(align_up(n + 64, 1 << 20), 1 << 20);
+        if (hipMalloc(&dDelta, capDelta * 2) != hipSuccess) { dDelta = nullptr; capDelta = 0; return false; }
+        return true;
+    }
     void release() {
         if (st) hipStreamSynchronize(st);
-        hipFree(dIn); hipFree(dOut); hipFree(dRes); hipFree(dRec);
+        hipFree(dIn); hipFree(dOut); hipFree(dRes); hipFree(dRec); hipFree(dDelta);
         if (st) hipStreamDestroy(st);
         *this = BlockScratch();
     }
@@ -175,12 +186,16 @@ struct ScratchLease {
 struct DevBuf {
     uint8_t* p = nullptr;
     uint64_t cap = 0;
+    int dev = -1;
     ~DevBuf() { hipFree(p); }
     bool ensure(uint64_t n) {
-        if (p && n <= cap) return true;
+        int d = -1;
+        if (hipGetDevice(&d) != hipSuccess) return false;
+        if (p && n <= cap && d == dev) return true;
         hipFree(p);
         p = nullptr;
         cap = 0;
+        dev = d;
         if (hipMalloc(reinterpret_cast<void**>(&p), n + 64) != hipSuccess) { p = nullptr; return false; }
         cap = n;
         return true;
@@ -218,11 +233,17 @@ namespace lz4mt {
 // written once both are done.
 Lz4MtResult device_compress_body(const uint8_t* src, uint64_t n, uint32_t bm, int blockChecksum, uint8_t* ws,
                                  uint8_t* body, uint32_t hdrLen, hipStream_t st, uint64_t** d_recOffOut,
-                                 const AuxStream* aux) {
+                                 const AuxStream* aux, const LinkState* link, int level) {
     const uint64_t nb = (n + bm - 1) / bm;
-    CompressWs w = carve_compress(ws, nb, bm);
+    CompressWs w = carve_compress(ws, nb, bm, level);
     g_timing.mark(0, st);
-    HIPCHK(launch_encode(src, n, bm, (uint32_t)nb, w.slots, bm, 0xFFFFFFFFu, w.csize, st));
+    if (link)   // block-dependent frame: one wave, blocks in order (k_encode_linked)
+        HIPCHK(launch_encode_linked(src, n, bm, (uint32_t)nb, w.slots, link->plan, link->table, link->fresh, w.csize,
+                                    st));
+    else if (level >= 3)   // LZ4-HC, a wave per block (lz4mt_hc.hip)
+        HIPCHK(launch_encode_hc(src, n, bm, (uint32_t)nb, w.slots, bm, 0xFFFFFFFFu, level, w.delta, w.csize, st));
+    else
+        HIPCHK(launch_encode(src, n, bm, (uint32_t)nb, w.slots, bm, 0xFFFFFFFFu, w.csize, st));
     g_timing.mark(1, st);
     const bool side = blockChecksum && aux && aux->st;
     if (side) {
@@ -267,7 +288,9 @@ void AuxStream::release() {
     st = nullptr; evIn = nullptr; evOut = nullptr; dev = -1;
 }
 
-uint64_t compress_ws_bytes(uint64_t n, uint32_t bm) { return carve_compress(nullptr, (n + bm - 1) / bm, bm).bytes; }
+uint64_t compress_ws_bytes(uint64_t n, uint32_t bm, int level) {
+    return carve_compress(nullptr, (n + bm - 1) / bm, bm, level).bytes;
+}
 
 }  // namespace lz4mt
 
@@ -279,7 +302,10 @@ extern "C" int lz4mtHipCompressBound(int isize) {
 }
 
 extern "C" int lz4mtHipCompressBlock(const char* src, char* dst, int isize, int maxOutputSize, int compressionLevel) {
-    if (compressionLevel >= 3) return 0;   // no GPU LZ4-HC: caller stores the block raw
+    // levels >= 3: LZ4-HC (LZ4_compressHC2_limitedOutput); 10..12, lz4's
+    // optimal parser, is not provided: 0 = the caller stores the block raw
+    const bool hc = compressionLevel >= 3;
+    if (hc && hc_attempts(compressionLevel) == 0) return 0;
     if (isize < 0 || (unsigned)isize > 0x7E000000u) return 0;
     if (maxOutputSize < 0) maxOutputSize = 0;
     if (!have_device()) return -1;
@@ -288,10 +314,14 @@ extern "C" int lz4mtHipCompressBlock(const char* src, char* dst, int isize, int 
     const int bound = lz4mtHipCompressBound(isize);
     const uint64_t outMax = (uint64_t)std::min(maxOutputSize, bound) + 16;
     if (!g_blk->ensure((uint64_t)isize, outMax)) return -1;
+    if (hc && !g_blk->ensure_delta((uint64_t)isize)) return -1;
     if (isize && hipMemcpyAsync(g_blk->dIn, src, (size_t)isize, hipMemcpyHostToDevice, g_blk->st) != hipSuccess) return -1;
-    if (launch_encode(g_blk->dIn, (uint64_t)isize, (uint32_t)std::max(isize, 1), 1, g_blk->dOut, 0,
-                      (uint32_t)maxOutputSize, g_blk->dRes, g_blk->st) != hipSuccess)
-        return -1;
+    const hipError_t le = hc ? launch_encode_hc(g_blk->dIn, (uint64_t)isize, (uint32_t)std::max(isize, 1), 1, g_blk->dOut,
+                                                0, (uint32_t)maxOutputSize, compressionLevel, g_blk->dDelta,
+                                                g_blk->dRes, g_blk->st)
+                             : launch_encode(g_blk->dIn, (uint64_t)isize, (uint32_t)std::max(isize, 1), 1, g_blk->dOut,
+                                             0, (uint32_t)maxOutputSize, g_blk->dRes, g_blk->st);
+    if (le != hipSuccess) return -1;
     int32_t r = 0;
     if (hipMemcpyAsync(&r, g_blk->dRes, 4, hipMemcpyDeviceToHost, g_blk->st) != hipSuccess) return -1;
     if (hipStreamSynchronize(g_blk->st) != hipSuccess) return -1;
@@ -334,23 +364,31 @@ extern "C" uint64_t lz4mtHipFrameBound(uint64_t srcSize, const Lz4MtStreamDescri
     return (uint64_t)kMaxHeader + srcSize + nb * 8 + 8;
 }
 
-extern "C" uint64_t lz4mtHipCompressWorkspaceSize(uint64_t srcSize, const Lz4MtStreamDescriptor* sd) {
+extern "C" uint64_t lz4mtHipCompressWorkspaceSizeEx(uint64_t srcSize, const Lz4MtStreamDescriptor* sd, int level) {
     const int id = sd ? sd->bd.blockMaximumSize : 7;
     const uint32_t bm = (id >= 4 && id <= 7) ? (uint32_t)block_max_bytes(id) : (4u << 20);
-    return compress_ws_bytes(srcSize, bm);
+    return compress_ws_bytes(srcSize, bm, level);
+}
+
+extern "C" uint64_t lz4mtHipCompressWorkspaceSize(uint64_t srcSize, const Lz4MtStreamDescriptor* sd) {
+    return lz4mtHipCompressWorkspaceSizeEx(srcSize, sd, 0);
 }
 
 static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
-                                       uint64_t* d_frameSize, const Lz4MtStreamDescriptor* sd, void* d_ws,
+                                       uint64_t* d_frameSize, const Lz4MtStreamDescriptor* sd, int level, void* d_ws,
                                        uint64_t wsSize, hipStream_t st, void** ownedWs) {
     if (!sd || !d_frame || (!d_src && srcSize)) return LZ4MT_RESULT_BAD_ARG;
     const Lz4MtResult v = validate_sd(sd);
     if (v != LZ4MT_RESULT_OK) return v;
-    if (!sd->flg.blockIndependence) return LZ4MT_RESULT_BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET;
     if (!have_device()) return LZ4MT_RESULT_ERROR;
     if (frameCap < lz4mtHipFrameBound(srcSize, sd)) return LZ4MT_RESULT_BAD_ARG;
+    // LZ4-HC runs for levels 3..9 on independent blocks; the block-dependent
+    // HC stream (LZ4_compressHC_limitedOutput_continue) and levels 10..12
+    // (the optimal parser) are not provided
+    if (level >= 3 && (!sd->flg.blockIndependence || hc_attempts(level) == 0)) return LZ4MT_RESULT_BAD_ARG;
+    if (level < 3) level = 0;
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
-    const uint64_t need = compress_ws_bytes(srcSize, bm);
+    const uint64_t need = compress_ws_bytes(srcSize, bm, level);
     uint8_t* ws = static_cast<uint8_t*>(d_ws);
     if (!ws || wsSize < need) {
         if (hipMalloc(reinterpret_cast<void**>(&ws), need) != hipSuccess) return LZ4MT_RESULT_ERROR;
@@ -364,7 +402,7 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
     thread_local AuxStream aux, auxStream;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     const bool capturing = hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone;
-    CompressWs w = carve_compress(ws, (srcSize + bm - 1) / bm, bm);
+    CompressWs w = carve_compress(ws, (srcSize + bm - 1) / bm, bm, level);
     // The content checksum (FLG.2) is one serial XXH32 chain over the input
     // (SURVEY.md §0.5).  It reads only d_src, so it starts at t = 0 on its
     // own stream, beside the encode, and the finalize waits for it.
@@ -376,9 +414,27 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
         HIPCHK(launch_xxh32_stream(static_cast<const uint8_t*>(d_src), srcSize, w.ssum, auxStream.st));
         HIPCHK(hipEventRecord(auxStream.evOut, auxStream.st));
     }
+    // block-dependent frames: the per-block lz4 stream plan (BdSim) and the
+    // table buffer, kept per thread (the kernels of an async call use them)
+    LinkState ls{};
+    const LinkState* lsp = nullptr;
+    if (!sd->flg.blockIndependence) {
+        thread_local DevBuf planBuf, tableBuf;
+        thread_local std::vector<LinkPlan> hplan;
+        const uint64_t nb = (srcSize + bm - 1) / bm;
+        hplan.assign(std::max<uint64_t>(nb, 1), LinkPlan{});
+        BdSim sim(sd->bd.blockMaximumSize);
+        for (uint64_t b = 0; b < nb; ++b)
+            sim.next((uint32_t)std::min<uint64_t>(bm, srcSize - b * bm), &hplan[b].lowIn, &hplan[b].lowDict,
+                     &hplan[b].candLow);
+        if (!planBuf.ensure(hplan.size() * sizeof(LinkPlan)) || !tableBuf.ensure(4096 * 4)) return LZ4MT_RESULT_ERROR;
+        HIPCHK(hipMemcpyAsync(planBuf.p, hplan.data(), hplan.size() * sizeof(LinkPlan), hipMemcpyHostToDevice, st));
+        ls = LinkState{reinterpret_cast<LinkPlan*>(planBuf.p), reinterpret_cast<uint32_t*>(tableBuf.p), true};
+        lsp = &ls;
+    }
     const Lz4MtResult r = device_compress_body(static_cast<const uint8_t*>(d_src), srcSize, bm, sd->flg.blockChecksum,
                                                ws, static_cast<uint8_t*>(d_frame), (uint32_t)hdrLen, st, &recOff,
-                                               !capturing && aux.ensure() ? &aux : nullptr);
+                                               !capturing && aux.ensure() ? &aux : nullptr, lsp, level);
     if (r != LZ4MT_RESULT_OK) {
         if (sckSide) hipStreamWaitEvent(st, auxStream.evOut, 0);   // scratch outlives the side kernel
         return r;
@@ -393,13 +449,14 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
     return LZ4MT_RESULT_OK;
 }
 
-extern "C" Lz4MtResult lz4mtHipCompressFrameAsync(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
-                                                  uint64_t* d_frameSize, const Lz4MtStreamDescriptor* sd,
-                                                  void* d_workspace, uint64_t workspaceSize, void* stream) {
+extern "C" Lz4MtResult lz4mtHipCompressFrameAsyncEx(const void* d_src, uint64_t srcSize, void* d_frame,
+                                                    uint64_t frameCap, uint64_t* d_frameSize,
+                                                    const Lz4MtStreamDescriptor* sd, int level, void* d_workspace,
+                                                    uint64_t workspaceSize, void* stream) {
     void* owned = nullptr;
     const hipStream_t st = static_cast<hipStream_t>(stream);
-    const Lz4MtResult r =
-        compress_frame_impl(d_src, srcSize, d_frame, frameCap, d_frameSize, sd, d_workspace, workspaceSize, st, &owned);
+    const Lz4MtResult r = compress_frame_impl(d_src, srcSize, d_frame, frameCap, d_frameSize, sd, level, d_workspace,
+                                              workspaceSize, st, &owned);
     if (owned) {  // library-owned scratch: must outlive the kernels
         hipStreamSynchronize(st);
         hipFree(owned);
@@ -407,14 +464,29 @@ extern "C" Lz4MtResult lz4mtHipCompressFrameAsync(const void* d_src, uint64_t sr
     return r;
 }
 
-extern "C" Lz4MtResult lz4mtHipCompressFrame(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
-                                             uint64_t* frameSize, const Lz4MtStreamDescriptor* sd, void* d_workspace,
-                                             uint64_t workspaceSize, void* stream) {
+extern "C" Lz4MtResult lz4mtHipCompressFrameAsync(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
+                                                  uint64_t* d_frameSize, const Lz4MtStreamDescriptor* sd,
+                                                  void* d_workspace, uint64_t workspaceSize, void* stream) {
+    void* owned = nullptr;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    const Lz4MtResult r =
+        compress_frame_impl(d_src, srcSize, d_frame, frameCap, d_frameSize, sd, 0, d_workspace, workspaceSize, st, &owned);
+    if (owned) {  // library-owned scratch: must outlive the kernels
+        hipStreamSynchronize(st);
+        hipFree(owned);
+    }
+    return r;
+}
+
+extern "C" Lz4MtResult lz4mtHipCompressFrameEx(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
+                                               uint64_t* frameSize, const Lz4MtStreamDescriptor* sd, int level,
+                                               void* d_workspace, uint64_t workspaceSize, void* stream) {
     void* owned = nullptr;
     const hipStream_t st = static_cast<hipStream_t>(stream);
     uint64_t* dfs = reinterpret_cast<uint64_t*>(small_dev());
     if (!dfs) return LZ4MT_RESULT_ERROR;
-    Lz4MtResult r = compress_frame_impl(d_src, srcSize, d_frame, frameCap, dfs, sd, d_workspace, workspaceSize, st, &owned);
+    Lz4MtResult r =
+        compress_frame_impl(d_src, srcSize, d_frame, frameCap, dfs, sd, level, d_workspace, workspaceSize, st, &owned);
     if (r == LZ4MT_RESULT_OK) {
         uint64_t fs = 0;
         if (hipMemcpyAsync(&fs, dfs, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -426,6 +498,13 @@ extern "C" Lz4MtResult lz4mtHipCompressFrame(const void* d_src, uint64_t srcSize
     }
     if (owned) hipFree(owned);
     return r;
+}
+
+extern "C" Lz4MtResult lz4mtHipCompressFrame(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
+                                             uint64_t* frameSize, const Lz4MtStreamDescriptor* sd, void* d_workspace,
+                                             uint64_t workspaceSize, void* stream) {
+    return lz4mtHipCompressFrameEx(d_src, srcSize, d_frame, frameCap, frameSize, sd, 0, d_workspace, workspaceSize,
+                                   stream);
 }
 
 // ---------------------------------------------------------------------------
@@ -573,7 +652,6 @@ extern "C" Lz4MtResult lz4mtHipFrameInfo(const void* d_frame, uint64_t frameSize
         int hb = 0;
         const Lz4MtResult r = parse_header(h + 4, avail - 4, sd, &hb);
         if (r != LZ4MT_RESULT_OK) return r;
-        if (!sd->flg.blockIndependence) return LZ4MT_RESULT_BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET;
         const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
         DecodeBuffers B;
         WalkInfo wi{};
@@ -620,7 +698,6 @@ HeadInfo read_head(const uint8_t* f, uint64_t frameSize, uint64_t pos, bool seen
     }
     int hb = 0;
     hi.err = parse_header(h + 4, avail - 4, sd, &hb);
-    if (hi.err == LZ4MT_RESULT_OK && !sd->flg.blockIndependence) hi.err = LZ4MT_RESULT_BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET;
     hi.hdrLen = 4 + hb;
     return hi;
 }
@@ -723,7 +800,6 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
         int hb = 0;
         result = parse_header(h + 4, avail - 4, sd, &hb);
         if (result != LZ4MT_RESULT_OK) break;
-        if (!sd->flg.blockIndependence) { result = LZ4MT_RESULT_BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET; break; }
         const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
         const int bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
         WalkInfo wi{};
@@ -731,6 +807,29 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
         result = walk_frame(f, frameSize, pos + 4 + hb, bm, bck, B, wi, st);
         if (result != LZ4MT_RESULT_OK) break;
         const uint64_t nb = wi.nBlocks;
+        uint64_t produced = 0;
+        if (!sd->flg.blockIndependence) {
+            // block-dependent frame (decompressBlockDependency, src/lz4mt.cpp:
+            // 737-845): one wave decodes the blocks in order, each against the
+            // 64 KiB before it (zeros before the frame's first byte)
+            thread_local DevBuf slotBuf, histBuf;
+            if (!slotBuf.ensure(65536 + (uint64_t)bm + 64) || !histBuf.ensure(65536)) { result = LZ4MT_RESULT_ERROR; break; }
+            HIPCHK(hipMemsetAsync(histBuf.p, 0, 65536, st));
+            if (bck && nb) HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, st));
+            const uint64_t room = outCap > opos ? outCap - opos : 0;
+            HIPCHK(launch_decode_linked(f, B.recs, (uint32_t)nb, bm, out + opos, room, slotBuf.p, histBuf.p, B.digest,
+                                        bck, B.dsize, B.status, st));
+            int32_t stat[2] = {0, 0};
+            std::vector<int32_t> ds(nb);
+            HIPCHK(hipMemcpyAsync(stat, B.status, 8, hipMemcpyDeviceToHost, st));
+            if (nb) HIPCHK(hipMemcpyAsync(ds.data(), B.dsize, nb * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            for (int32_t i = 0; i < stat[0] && (uint64_t)i < nb; ++i) produced += (uint64_t)ds[i];
+            if (stat[1] == 16) result = LZ4MT_RESULT_BLOCK_CHECKSUM_MISMATCH;   // checked before writing
+            else if (stat[1] == 18) result = LZ4MT_RESULT_DECOMPRESS_FAIL;
+            else if (stat[1] != 0) result = LZ4MT_RESULT_ERROR;
+            else if (wi.result != 0) result = (Lz4MtResult)wi.result;
+        } else {
         // decode target: in place when 16-B aligned, else a staging buffer
         const bool aligned = ((reinterpret_cast<uintptr_t>(out) + opos) & 15) == 0;
         const uint64_t room = outCap > opos ? outCap - opos : 0;
@@ -770,7 +869,6 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
             if (stv[i] != 0) { good = i; result = (Lz4MtResult)stv[i]; break; }
         if (good == nb && wi.result != 0) result = (Lz4MtResult)wi.result;
         // gather decoded bytes of blocks [0, good) contiguously at out + opos
-        uint64_t produced = 0;
         bool contiguous = aligned;
         for (uint64_t i = 0; i < good; ++i) {
             if (i + 1 < good && (uint64_t)ds[i] != bm) contiguous = false;
@@ -792,6 +890,7 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
                 w += (uint64_t)ds[i];
             }
         }
+        }   // independent blocks
         if (result != LZ4MT_RESULT_OK) { opos += produced; break; }
         uint64_t next = wi.endPos;
         if (sck) {

@@ -43,8 +43,8 @@
 namespace lz4mt {
 Lz4MtResult device_compress_body(const uint8_t* src, uint64_t n, uint32_t bm, int blockChecksum, uint8_t* ws,
                                  uint8_t* body, uint32_t hdrLen, hipStream_t st, uint64_t** d_recOffOut,
-                                 const AuxStream* aux);
-uint64_t compress_ws_bytes(uint64_t n, uint32_t bm);
+                                 const AuxStream* aux, const LinkState* link, int level);
+uint64_t compress_ws_bytes(uint64_t n, uint32_t bm, int level);
 }  // namespace lz4mt
 
 using namespace lz4mt;
@@ -392,7 +392,7 @@ struct Slot {
             hipFree(dRecs); hipFree(dDs); hipFree(dSt); hipFree(dDig);
             hMeta = nullptr; hRecs = nullptr; hDs = nullptr; hSt = nullptr;
             dRecs = nullptr; dDs = nullptr; dSt = nullptr; dDig = nullptr; metaCap = 0;
-            const uint64_t k = std::max<uint64_t>(blocks, 1);
+            const uint64_t k = std::max<uint64_t>(blocks, 2);   // >= 2: the linked decoder's status pair
             if (hipHostMalloc(reinterpret_cast<void**>(&hMeta), 64, 0) != hipSuccess ||
                 hipHostMalloc(reinterpret_cast<void**>(&hRecs), k * sizeof(BlockRec), 0) != hipSuccess ||
                 hipHostMalloc(reinterpret_cast<void**>(&hDs), k * 4, 0) != hipSuccess ||
@@ -504,26 +504,49 @@ void run_slot_pipeline(Session& s, int nSlots, Fill fill, Finish finish) {
 // in flight keep up to 3 GiB of blocks on the GPU at once.
 
 
+// device buffer owned by one call (freed on return; hipFree waits for the device)
+struct CallBuf {
+    void* p = nullptr;
+    ~CallBuf() { if (p) hipFree(p); }
+    bool alloc(size_t n) { return hipMalloc(&p, n) == hipSuccess; }
+};
+
 void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
-    if (s.level() >= 3) { s.quit(LZ4MT_RESULT_BAD_ARG); return; }   // no GPU LZ4-HC
     if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return; }
+    // LZ4-HC (levels 3..9) on independent blocks; the block-dependent HC
+    // stream and lz4's optimal parser (10..12) are not provided
+    const int level = s.level() >= 3 ? s.level() : 0;
+    if (level && (!sd->flg.blockIndependence || hc_attempts(level) == 0)) { s.quit(LZ4MT_RESULT_BAD_ARG); return; }
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
-    const PipeShape P = pipe_shape(true);
-    uint64_t batch = 0;
+    // Block-dependent frames (compressBlockDependency, src/lz4mt.cpp:460-538)
+    // are one serial stream: one slot (batches in order on one stream), each
+    // batch's input preceded by the 64 KiB before it (`hist`), the lz4
+    // stream table carried in `table`, the per-block lz4 modes from BdSim.
+    const bool linked = !sd->flg.blockIndependence;
+    const uint64_t pre = linked ? 65536 : 0;
+    PipeShape P = pipe_shape(true);
+    if (linked) P.slots = 1;
+    BdSim sim(sd->bd.blockMaximumSize);
+    std::vector<uint8_t> hist(linked ? 65536 : 0, 0);
+    std::vector<LinkPlan> plan;
+    CallBuf table, dplan;
+    if (linked && !table.alloc(4096 * 4)) { s.quit(LZ4MT_RESULT_ERROR); return; }
+    uint64_t batch = 0, planCap = 0;
     auto fill = [&](Slot& S, bool* stop) -> bool {
         const uint64_t K = batch_blocks(P, bm, batch++), inCap = K * bm;
-        if (!S.ensure(inCap, inCap + K * 8 + 64, compress_ws_bytes(inCap, bm), 0)) {
+        if (!S.ensure(pre + inCap, inCap + K * 8 + 64, compress_ws_bytes(inCap, bm, level), 0)) {
             s.quit(LZ4MT_RESULT_ERROR);
             return false;
         }
+        uint8_t* in = S.hIn + pre;
         // One read() per block, as the reference does (src/lz4mt.cpp:435-450):
         // a read of 0 ends the input; a short read is a short block, which
         // closes this batch (a batch is blocks of bm bytes plus at most one
         // short last block) -- the next batch carries on reading.
         uint64_t total = 0;
         for (uint64_t j = 0; j < K; ++j) {
-            const int n = s.read(S.hIn + total, (int)bm);
+            const int n = s.read(in + total, (int)bm);
             if (n <= 0) { *stop = true; break; }
             total += (uint64_t)n;
             if ((uint32_t)n < bm) break;
@@ -531,15 +554,41 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
         if (total == 0) return false;
         uint64_t* dRecOff = nullptr;
         const uint64_t nb = (total + bm - 1) / bm;
-        if (hipMemcpyAsync(S.dIn, S.hIn, total, hipMemcpyHostToDevice, S.st) != hipSuccess ||
-            device_compress_body(S.dIn, total, bm, bck, S.dWs, S.dOut, 0, S.st, &dRecOff, nullptr) != LZ4MT_RESULT_OK ||
+        LinkState ls{};
+        if (linked) {
+            memcpy(S.hIn, hist.data(), 65536);
+            plan.resize(nb);
+            for (uint64_t b = 0; b < nb; ++b)
+                sim.next((uint32_t)std::min<uint64_t>(bm, total - b * bm), &plan[b].lowIn, &plan[b].lowDict,
+                         &plan[b].candLow);
+            if (nb > planCap) {
+                if (dplan.p) { hipStreamSynchronize(S.st); hipFree(dplan.p); dplan.p = nullptr; }
+                if (!dplan.alloc(nb * sizeof(LinkPlan))) { s.quit(LZ4MT_RESULT_ERROR); return false; }
+                planCap = nb;
+            }
+            // the plan buffer is reused by the next batch: same stream, in order
+            if (hipMemcpyAsync(dplan.p, plan.data(), nb * sizeof(LinkPlan), hipMemcpyHostToDevice, S.st) != hipSuccess) {
+                s.quit(LZ4MT_RESULT_ERROR);
+                return false;
+            }
+            ls = LinkState{static_cast<LinkPlan*>(dplan.p), static_cast<uint32_t*>(table.p), batch == 1};
+            // the history of the next batch: the last 64 KiB of (hist ++ this input)
+            if (total >= 65536) memcpy(hist.data(), in + total - 65536, 65536);
+            else {
+                memmove(hist.data(), hist.data() + total, 65536 - total);
+                memcpy(hist.data() + 65536 - total, in, total);
+            }
+        }
+        if (hipMemcpyAsync(S.dIn, S.hIn, pre + total, hipMemcpyHostToDevice, S.st) != hipSuccess ||
+            device_compress_body(S.dIn + pre, total, bm, bck, S.dWs, S.dOut, 0, S.st, &dRecOff, nullptr,
+                                 linked ? &ls : nullptr, level) != LZ4MT_RESULT_OK ||
             hipMemcpyAsync(S.hMeta, dRecOff + nb, 8, hipMemcpyDeviceToHost, S.st) != hipSuccess) {
             s.quit(LZ4MT_RESULT_ERROR);
             return false;
         }
         S.total = total;
         S.nb = nb;
-        if (sck) xs.update(S.hIn, total);   // serial content checksum overlaps the kernels
+        if (sck) xs.update(in, total);   // serial content checksum overlaps the kernels
         return true;
     };
     // the body size, D2H of the body, then write() per record in the
@@ -621,7 +670,18 @@ bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
     if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return false; }
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
-    const PipeShape P = pipe_shape(false);
+    // Block-dependent frames (decompressBlockDependency, src/lz4mt.cpp:
+    // 737-845): one slot, one wave decoding the blocks in order, the 64 KiB
+    // history carried from batch to batch in `hist` (zeros at the start).
+    const bool linked = !sd->flg.blockIndependence;
+    PipeShape P = pipe_shape(false);
+    if (linked) P.slots = 1;
+    CallBuf hist, slotScratch;
+    if (linked && (!hist.alloc(65536) || !slotScratch.alloc(65536 + (size_t)bm + 64) ||
+                   hipMemset(hist.p, 0, 65536) != hipSuccess)) {
+        s.quit(LZ4MT_RESULT_ERROR);
+        return false;
+    }
     uint64_t batch = 0;
     bool eos = false;
     Lz4MtResult pending = LZ4MT_RESULT_OK;   // a read error found while filling a batch
@@ -645,6 +705,22 @@ bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
         }
         *stop = eos || pending != LZ4MT_RESULT_OK;
         if (nb == 0) return false;
+        if (linked) {
+            if (hipMemcpyAsync(S.dIn, S.hIn, used, hipMemcpyHostToDevice, S.st) != hipSuccess ||
+                hipMemcpyAsync(S.dRecs, S.hRecs, nb * sizeof(BlockRec), hipMemcpyHostToDevice, S.st) != hipSuccess ||
+                (bck && launch_xxh32_frame_blocks(S.dIn, S.dRecs, (uint32_t)nb, S.dDig, S.st) != hipSuccess) ||
+                launch_decode_linked(S.dIn, S.dRecs, (uint32_t)nb, bm, S.dOut, nb * bm,
+                                     static_cast<uint8_t*>(slotScratch.p), static_cast<uint8_t*>(hist.p), S.dDig, bck,
+                                     S.dDs, S.dSt, S.st) != hipSuccess ||
+                hipMemcpyAsync(S.hDs, S.dDs, nb * 4, hipMemcpyDeviceToHost, S.st) != hipSuccess ||
+                hipMemcpyAsync(S.hSt, S.dSt, 8, hipMemcpyDeviceToHost, S.st) != hipSuccess ||
+                hipMemcpyAsync(S.hOut, S.dOut, nb * bm, hipMemcpyDeviceToHost, S.st) != hipSuccess) {
+                s.quit(LZ4MT_RESULT_ERROR);
+                return false;
+            }
+            S.nb = nb;
+            return true;
+        }
         if (hipMemcpyAsync(S.dIn, S.hIn, used, hipMemcpyHostToDevice, S.st) != hipSuccess ||
             hipMemcpyAsync(S.dRecs, S.hRecs, nb * sizeof(BlockRec), hipMemcpyHostToDevice, S.st) != hipSuccess ||
             launch_decode(S.dIn, S.dRecs, (uint32_t)nb, bm, S.dOut, nb * bm, S.dDs, S.st) != hipSuccess ||
@@ -663,6 +739,22 @@ bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
     // frame (reference precedence: a decode failure before writing)
     auto finish = [&](Slot& S) -> bool {
         if (hipStreamSynchronize(S.st) != hipSuccess) { s.quit(LZ4MT_RESULT_ERROR); return false; }
+        if (linked) {   // blocks [0, done) are decoded back to back; a failing block is not written
+            const int32_t done = S.hSt[0], code = S.hSt[1];
+            const uint8_t* p = S.hOut;
+            for (int32_t i = 0; i < done; ++i) {
+                const int n = S.hDs[i];
+                if (sck) xs.update(p, (size_t)n);
+                if (!s.write(p, n)) { s.quit(LZ4MT_RESULT_CANNOT_WRITE_DATA_BLOCK); return false; }
+                p += n;
+            }
+            if (code) {
+                s.quit(code == 16 ? LZ4MT_RESULT_BLOCK_CHECKSUM_MISMATCH
+                                  : code == 18 ? LZ4MT_RESULT_DECOMPRESS_FAIL : LZ4MT_RESULT_ERROR);
+                return false;
+            }
+            return true;
+        }
         for (uint64_t i = 0; i < S.nb; ++i) {
             const bool raw = (S.hRecs[i].bits & kRawBit) != 0;
             const int32_t st = S.hSt[i];
@@ -723,12 +815,11 @@ extern "C" Lz4MtStreamDescriptor lz4mtInitStreamDescriptor(void) {
 // reference's default PARALLEL mode when the codec callback of that
 // direction is null -- i.e. when every block would go to this library's GPU
 // block operator one launch at a time (a relinked lz4mt caller).  Same
-// frames, same callback protocol; HC levels keep the per-block path (the
-// operator stores those blocks raw).
+// frames, same callback protocol (LZ4-HC included: levels 3..9).
 bool use_device_engine(const Lz4MtContext* ctx, bool compress) {
     if (ctx->mode & LZ4MT_MODE_DEVICE) return true;
     if (ctx->mode != LZ4MT_MODE_PARALLEL) return false;
-    return compress ? (!ctx->compress && ctx->compressionLevel < 3) : !ctx->decompress;
+    return compress ? !ctx->compress : !ctx->decompress;
 }
 
 extern "C" Lz4MtResult lz4mtCompress(Lz4MtContext* ctx, const Lz4MtStreamDescriptor* sd) {
@@ -740,9 +831,10 @@ extern "C" Lz4MtResult lz4mtCompress(Lz4MtContext* ctx, const Lz4MtStreamDescrip
     uint8_t hdr[kMaxHeader];
     const int hl = build_header(sd, hdr);
     if (!ctx->write || ctx->write(ctx, hdr, hl) != hl) return s.quit(LZ4MT_RESULT_CANNOT_WRITE_HEADER);
-    if (!sd->flg.blockIndependence) return s.quit(LZ4MT_RESULT_BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET);
     HostXxh32 xs(0);
-    if (use_device_engine(ctx, true)) compress_device(s, sd, xs);
+    // block-dependent frames: the reference calls lz4's streaming API
+    // directly, not ctx->compress (src/lz4mt.cpp:295-332): the device engine
+    if (!sd->flg.blockIndependence || use_device_engine(ctx, true)) compress_device(s, sd, xs);
     else compress_host(s, sd, xs);
     if (s.result() != LZ4MT_RESULT_OK) return s.result();
     if (!s.writeU32(0)) return s.quit(LZ4MT_RESULT_CANNOT_WRITE_EOS);
@@ -788,9 +880,11 @@ extern "C" Lz4MtResult lz4mtDecompress(Lz4MtContext* ctx, Lz4MtStreamDescriptor*
         const Lz4MtResult hr = parse_header(h, (size_t)(2 + nex), &tmp, &hb);
         *sd = tmp;
         if (hr != LZ4MT_RESULT_OK) { s.quit(hr); break; }
-        if (!sd->flg.blockIndependence) { s.quit(LZ4MT_RESULT_BLOCK_DEPENDENCE_IS_NOT_SUPPORTED_YET); break; }
         HostXxh32 xs(0);
-        const bool eos = use_device_engine(ctx, false) ? decompress_device(s, sd, xs) : decompress_host(s, sd, xs);
+        // block-dependent frames: LZ4_decompress_safe_withPrefix64k, not
+        // ctx->decompress, in the reference (src/lz4mt.cpp:813-818)
+        const bool eos = (!sd->flg.blockIndependence || use_device_engine(ctx, false)) ? decompress_device(s, sd, xs)
+                                                                                       : decompress_host(s, sd, xs);
         if (s.error() || s.quitting()) break;
         if (!eos) { s.quit(LZ4MT_RESULT_CANNOT_READ_BLOCK_SIZE); break; }
         if (sd->flg.streamChecksum) {

@@ -1,0 +1,437 @@
+// lz4mt_hc.hip — LZ4-HC (compression levels 3..9) for gfx950: the codec
+// lz4mt selects for level >= 3, LZ4_compressHC2_limitedOutput(src, dst, n,
+// cap = n, level) (reference src/main.cpp:778-785, src/lz4mt.cpp:391), i.e.
+// lz4 1.9.3's LZ4_compress_HC -> LZ4HC_compress_hashChain.  Bit-exact with
+// oracle/lz4hc_oracle.c (pinned against liblz4 1.9.3).
+//
+// Two kernels, one wavefront per block each:
+//   k_hc_prev    the hash chain of the block: for every position p the
+//                distance to the previous position with the same 4-byte hash
+//                (u16; 0 = none within 64 KiB).  LZ4HC_Insert inserts every
+//                position in order before each search, so the chain lz4hc
+//                walks at a search is exactly this "previous same hash" list
+//                (its chainTable delta, capped at 65535, and its hashTable
+//                head).  The "last position per hash" table (32768 x u32)
+//                sits in LDS; 64 positions per step, equal hashes inside a
+//                step resolved by ballot.
+//   k_encode_hc  the hashChain parse (InsertAndFindBestMatch, the Search2 /
+//                Search3 lazy evaluation, pattern analysis at level 9) with
+//                the parse state wave-uniform; the lanes run the data-parallel
+//                parts: forward match count (64 x 4 bytes per round), the
+//                backward count, byte-run lengths and the literal copies.
+//                The chain walk is serial (one dependent delta load per
+//                candidate, with the candidate's bytes in the same round).
+#include "lz4mt_device.h"
+
+namespace lz4mt {
+
+#define WAVE_SYNC() __builtin_amdgcn_wave_barrier()
+
+typedef const __attribute__((address_space(1))) uint8_t g_cu8;
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+typedef const __attribute__((address_space(1))) uint16_t g_cu16;
+typedef __attribute__((address_space(1))) uint16_t g_u16;
+typedef __attribute__((address_space(3))) uint8_t l_u8;
+typedef __attribute__((address_space(3))) uint32_t l_u32;
+
+namespace {
+
+__device__ __forceinline__ uint32_t laneid() { return __lane_id(); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ uint32_t ffs64(uint64_t m) { return m ? (uint32_t)__builtin_ctzll(m) : 64u; }
+
+constexpr uint32_t kHashLog = 15;
+constexpr uint32_t kHcDist = 65535;
+constexpr int kOptimalML = 18;   // (ML_MASK - 1) + MINMATCH
+
+__device__ __forceinline__ uint32_t rd32(g_cu8* p) {   // little-endian, any alignment (bytes inside the block)
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+__device__ __forceinline__ uint32_t rd16(g_cu8* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+__device__ __forceinline__ uint32_t hc_hash(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// k_hc_prev: delta[p] = p - (previous position with the same hash), 0 if
+// none within 65535, for p in [0, n - 4] (positions lz4hc may insert)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_hc_prev(const uint8_t* __restrict__ src, uint64_t srcSize, uint32_t blockSize,
+                                                uint16_t* __restrict__ delta) {
+    __shared__ uint32_t last[1u << kHashLog];   // position + 1 of the latest occurrence (0 = none)
+    __shared__ uint8_t dd[1024];                // duplicate-hash detection inside a step
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
+    g_cu8* s = (g_cu8*)src + off;
+    g_u16* dl = (g_u16*)delta + off;
+    const uint32_t L = laneid();
+    for (uint32_t i = L; i < (1u << kHashLog); i += 64) last[i] = 0;
+    WAVE_SYNC();
+    if (n < 4) return;
+    const uint32_t np = n - 3;   // positions with 4 readable bytes
+    for (uint32_t base = 0; base < np; base += 64) {
+        const uint32_t p = base + L;
+        const bool live = p < np;
+        const uint32_t h = live ? hc_hash(rd32(s + p)) : 0u;
+        // lanes sharing a hash: the group's earlier member is the predecessor
+        if (live) ((l_u8*)dd)[h & 1023] = (uint8_t)L;
+        WAVE_SYNC();
+        const uint32_t sv = live ? ((l_u8*)dd)[h & 1023] : L;
+        uint64_t pending = ballot(live && sv != L);
+        int pred = -1;
+        uint64_t gm = 1ull << L;
+        while (pending) {
+            const uint32_t leader = ffs64(pending);
+            const uint32_t key = rdlane(h, (int)leader);
+            const uint64_t m = ballot(live && h == key);
+            if ((m >> L) & 1) {
+                gm = m;
+                const uint64_t below = m & ((1ull << L) - 1ull);
+                pred = below ? 63 - __clzll((long long)below) : -1;
+            }
+            pending &= ~m;
+        }
+        if (live) {
+            uint32_t q1 = pred >= 0 ? base + (uint32_t)pred + 1 : ((l_u32*)last)[h];   // position + 1 of the previous
+            const uint32_t d = (q1 && p + 1 - q1 <= kHcDist) ? p + 1 - q1 : 0u;
+            dl[p] = (uint16_t)d;
+        }
+        WAVE_SYNC();
+        // the group's last member records its position
+        if (live && !(gm & ~((2ull << L) - 1ull))) ((l_u32*)last)[h] = p + 1;
+        WAVE_SYNC();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_encode_hc
+// ---------------------------------------------------------------------------
+namespace {
+
+struct HcBlock {
+    g_cu8* s;             // block source
+    uint32_t n;
+    g_cu16* dl;           // k_hc_prev output
+    uint32_t maxAttempts;
+    bool pattern;         // pattern analysis (level 9)
+
+    // chain delta as lz4hc's chainTable holds it (capped 65535 = "none")
+    __device__ __forceinline__ uint32_t chain(uint32_t m) const {
+        const uint32_t d = dl[m];
+        return d ? d : kHcDist;
+    }
+    // LZ4_count(a, b, limit): equal bytes of [a, limit) and [b, ...), 256 per round
+    __device__ uint32_t count_fwd(uint32_t a, uint32_t b, uint32_t limit) const {
+        const uint32_t L = laneid();
+        uint32_t c = 0;
+        for (;;) {
+            const uint32_t x = a + c + 4 * L;
+            uint32_t eq = 0;
+            if (x < limit) {
+                const uint32_t av = rd32(s + x), bv = rd32(s + b + c + 4 * L);
+                const uint32_t diff = av ^ bv;
+                eq = diff ? ((uint32_t)__builtin_ctz(diff) >> 3) : 4u;
+                eq = min(eq, limit - x);
+            }
+            const uint64_t nf = ballot(eq < 4);
+            if (nf) {
+                const uint32_t f = ffs64(nf);
+                return c + 4 * f + rdlane(eq, (int)f);
+            }
+            c += 256;
+        }
+    }
+    // LZ4HC_countBack: <= 0, bounded by max(iMin - ip, mMin - match)
+    __device__ int count_back(uint32_t ip, uint32_t match, uint32_t iMin, uint32_t mMin) const {
+        const uint32_t L = laneid();
+        const uint32_t lim = min(ip - iMin, match - mMin);   // steps allowed
+        uint32_t k = 0;
+        for (;;) {
+            const uint32_t j = k + L + 1;
+            const bool same = j <= lim && s[ip - j] == s[match - j];
+            const uint64_t stop = ballot(!same);
+            if (stop != 0) return -(int)(k + ffs64(stop));
+            k += 64;
+        }
+    }
+    // length of the run of byte v starting at p, up to end
+    __device__ uint32_t run_fwd(uint32_t p, uint32_t end, uint32_t v) const {
+        const uint32_t L = laneid();
+        for (uint32_t c = 0;; c += 64) {
+            const uint32_t x = p + c + L;
+            const uint64_t stop = ballot(!(x < end && s[x] == v));
+            if (stop) return c + ffs64(stop);
+        }
+    }
+    // length of the run of byte v ending just before p, down to low
+    __device__ uint32_t run_back(uint32_t p, uint32_t low, uint32_t v) const {
+        const uint32_t L = laneid();
+        for (uint32_t c = 0;; c += 64) {
+            const uint32_t j = c + L + 1;
+            const uint64_t stop = ballot(!(j <= p - low && s[p - j] == v));
+            if (stop) return c + ffs64(stop);
+        }
+    }
+
+    // LZ4HC_InsertAndGetWiderMatch (single segment, chainSwap = 0); positions
+    // are block offsets.  Returns longest; *mpos / *spos as lz4hc's
+    // matchpos / startpos.
+    __device__ int wider(uint32_t ip, uint32_t iLow, uint32_t iHigh, int longest, uint32_t* mpos,
+                         uint32_t* spos) const {
+        const uint32_t lowest = ip > kHcDist ? ip - kHcDist : 0u;
+        const uint32_t lookBack = ip - iLow;
+        int nbAttempts = (int)maxAttempts;
+        const uint32_t pat = rd32(s + ip);
+        int repeat = 0;   // 0 untested, 1 confirmed, 2 not
+        uint32_t srcPatLen = 0;
+        const uint32_t d0 = uni(dl[ip]);
+        if (d0 == 0) return longest;   // no earlier position with this hash in the window
+        uint32_t m = ip - d0;
+        while (m >= lowest && nbAttempts > 0) {
+            --nbAttempts;
+            // the candidate's filter bytes and its chain link, one round
+            const uint32_t f16 = uni(rd16(s + m - lookBack + (uint32_t)longest - 1));
+            const uint32_t m32 = uni(rd32(s + m));
+            const uint32_t dnext = uni(dl[m]);
+            if (uni(rd16(s + iLow + (uint32_t)longest - 1)) == f16 && m32 == pat) {
+                const int back = lookBack ? count_back(ip, m, iLow, 0) : 0;
+                int ml = 4 + (int)count_fwd(ip + 4, m + 4, iHigh);
+                ml -= back;
+                if (ml > longest) {
+                    longest = ml;
+                    *mpos = m + (uint32_t)back;
+                    *spos = ip + (uint32_t)back;
+                }
+            }
+            const uint32_t distNext = dnext ? dnext : kHcDist;
+            if (pattern && distNext == 1) {
+                const uint32_t cand = m - 1;
+                if (repeat == 0) {
+                    if (((pat & 0xFFFF) == (pat >> 16)) & ((pat & 0xFF) == (pat >> 24))) {
+                        repeat = 1;
+                        srcPatLen = run_fwd(ip + 4, iHigh, pat & 255u) + 4;
+                    } else {
+                        repeat = 2;
+                    }
+                }
+                if (repeat == 1 && cand >= lowest && uni(rd32(s + cand)) == pat) {   // good candidate
+                    const uint32_t fwdLen = run_fwd(cand + 4, iHigh, pat & 255u) + 4;
+                    uint32_t backLen = run_back(cand, 0, pat & 255u);
+                    {
+                        const uint32_t lo = cand - backLen;
+                        backLen = cand - (lo > lowest ? lo : lowest);
+                    }
+                    const uint32_t segLen = backLen + fwdLen;
+                    if (segLen >= srcPatLen && fwdLen <= srcPatLen) {
+                        m = cand + fwdLen - srcPatLen;
+                    } else {
+                        m = cand - backLen;
+                        if (lookBack == 0) {
+                            const uint32_t maxML = segLen < srcPatLen ? segLen : srcPatLen;
+                            if ((uint32_t)longest < maxML) {
+                                if (ip - m > kHcDist) break;
+                                longest = (int)maxML;
+                                *mpos = m;
+                                *spos = ip;
+                            }
+                            const uint32_t dn = chain(m);
+                            if (dn > m + 65536u) break;   // lz4hc: distToNextPattern > matchIndex (index = offset + 64 KiB)
+                            m -= dn;
+                            if ((int32_t)m < 0) break;     // below the block: under `lowest`
+                        }
+                    }
+                    continue;
+                }
+            }
+            if (m < distNext) break;   // would go below the block: under `lowest`
+            m -= distNext;
+        }
+        return longest;
+    }
+};
+
+// LZ4HC_encodeSequence into d; returns false on overflow (limitedOutput)
+__device__ bool hc_encode(g_cu8* s, g_u8* d, uint32_t& ip, uint32_t& op, uint32_t& anchor, int ml, uint32_t ref,
+                          bool limit, uint32_t cap) {
+    const uint32_t L = laneid();
+    const uint32_t token = op;
+    uint32_t o = op + 1;
+    const uint32_t lit = ip - anchor;
+    if (limit && (uint64_t)o + lit / 255 + lit + (2 + 1 + 5) > cap) return false;
+    uint32_t tk;
+    if (lit >= 15) {
+        tk = 15u << 4;
+        const uint32_t ext = (lit - 15) / 255 + 1, rem = (lit - 15) % 255;
+        for (uint32_t c = 0; c < ext; c += 64)
+            if (c + L < ext) d[o + c + L] = (uint8_t)(c + L + 1 < ext ? 255u : rem);
+        o += ext;
+    } else {
+        tk = lit << 4;
+    }
+    for (uint32_t c = 0; c < lit; c += 64)
+        if (c + L < lit) d[o + c + L] = s[anchor + c + L];
+    o += lit;
+    const uint32_t off = ip - ref;
+    if (L == 0) { d[o] = (uint8_t)off; d[o + 1] = (uint8_t)(off >> 8); }
+    o += 2;
+    uint32_t len = (uint32_t)ml - 4;
+    if (limit && (uint64_t)o + len / 255 + (1 + 5) > cap) return false;
+    if (len >= 15) {
+        tk += 15;
+        len -= 15;
+        // 255 pairs, then one 255 when >= 255 remains, then the remainder:
+        // the same bytes as (len / 255) 255s and len % 255
+        const uint32_t ext = len / 255 + 1, rem = len % 255;
+        for (uint32_t c = 0; c < ext; c += 64)
+            if (c + L < ext) d[o + c + L] = (uint8_t)(c + L + 1 < ext ? 255u : rem);
+        o += ext;
+    } else {
+        tk += len;
+    }
+    if (L == 0) d[token] = (uint8_t)tk;
+    WAVE_SYNC();
+    op = o;
+    ip += (uint32_t)ml;
+    anchor = ip;
+    return true;
+}
+
+// LZ4HC_compress_hashChain; 0 = does not fit cap (store raw)
+__device__ int32_t encode_block_hc(const HcBlock& B, g_u8* d, uint32_t cap) {
+    const uint32_t L = laneid();
+    const uint32_t n = B.n;
+    g_cu8* s = B.s;
+    const bool limit = (uint64_t)cap < (uint64_t)n + n / 255 + 16;
+    uint32_t ip = 0, anchor = 0, op = 0;
+    const uint32_t mflimit = n >= 12 ? n - 12 : 0, matchlimit = n >= 5 ? n - 5 : 0;
+    int ml0, ml, ml2, ml3;
+    uint32_t start0 = 0, ref0 = 0, ref = 0, start2 = 0, ref2 = 0, start3 = 0, ref3 = 0;
+    if (n < 13) goto last_literals;
+    while (ip <= mflimit) {
+        {
+            uint32_t useless = ip;
+            ml = B.wider(ip, ip, matchlimit, 3, &ref, &useless);
+        }
+        if (ml < 4) { ++ip; continue; }
+        start0 = ip; ref0 = ref; ml0 = ml;
+    search2:
+        if (ip + (uint32_t)ml <= mflimit) ml2 = B.wider(ip + (uint32_t)ml - 2, ip, matchlimit, ml, &ref2, &start2);
+        else ml2 = ml;
+        if (ml2 == ml) {
+            if (!hc_encode(s, d, ip, op, anchor, ml, ref, limit, cap)) return 0;
+            continue;
+        }
+        if (start0 < ip && start2 < ip + (uint32_t)ml0) { ip = start0; ref = ref0; ml = ml0; }
+        if (start2 - ip < 3) {
+            ml = ml2; ip = start2; ref = ref2;
+            goto search2;
+        }
+    search3:
+        if (start2 - ip < (uint32_t)kOptimalML) {
+            int nml = ml;
+            if (nml > kOptimalML) nml = kOptimalML;
+            if (ip + (uint32_t)nml > start2 + (uint32_t)ml2 - 4) nml = (int)(start2 - ip) + ml2 - 4;
+            const int corr = nml - (int)(start2 - ip);
+            if (corr > 0) { start2 += (uint32_t)corr; ref2 += (uint32_t)corr; ml2 -= corr; }
+        }
+        if (start2 + (uint32_t)ml2 <= mflimit) ml3 = B.wider(start2 + (uint32_t)ml2 - 3, start2, matchlimit, ml2, &ref3, &start3);
+        else ml3 = ml2;
+        if (ml3 == ml2) {
+            if (start2 < ip + (uint32_t)ml) ml = (int)(start2 - ip);
+            if (!hc_encode(s, d, ip, op, anchor, ml, ref, limit, cap)) return 0;
+            ip = start2;
+            if (!hc_encode(s, d, ip, op, anchor, ml2, ref2, limit, cap)) return 0;
+            continue;
+        }
+        if (start3 < ip + (uint32_t)ml + 3) {
+            if (start3 >= ip + (uint32_t)ml) {
+                if (start2 < ip + (uint32_t)ml) {
+                    const int corr = (int)(ip + (uint32_t)ml - start2);
+                    start2 += (uint32_t)corr; ref2 += (uint32_t)corr; ml2 -= corr;
+                    if (ml2 < 4) { start2 = start3; ref2 = ref3; ml2 = ml3; }
+                }
+                if (!hc_encode(s, d, ip, op, anchor, ml, ref, limit, cap)) return 0;
+                ip = start3; ref = ref3; ml = ml3;
+                start0 = start2; ref0 = ref2; ml0 = ml2;
+                goto search2;
+            }
+            start2 = start3; ref2 = ref3; ml2 = ml3;
+            goto search3;
+        }
+        if (start2 < ip + (uint32_t)ml) {
+            if (start2 - ip < (uint32_t)kOptimalML) {
+                if (ml > kOptimalML) ml = kOptimalML;
+                if (ip + (uint32_t)ml > start2 + (uint32_t)ml2 - 4) ml = (int)(start2 - ip) + ml2 - 4;
+                const int corr = ml - (int)(start2 - ip);
+                if (corr > 0) { start2 += (uint32_t)corr; ref2 += (uint32_t)corr; ml2 -= corr; }
+            } else {
+                ml = (int)(start2 - ip);
+            }
+        }
+        if (!hc_encode(s, d, ip, op, anchor, ml, ref, limit, cap)) return 0;
+        ip = start2; ref = ref2; ml = ml2;
+        start2 = start3; ref2 = ref3; ml2 = ml3;
+        goto search3;
+    }
+last_literals : {
+    const uint32_t run = n - anchor;
+    const uint32_t llAdd = (run + 255 - 15) / 255;
+    if (limit && (uint64_t)op + 1 + llAdd + run > cap) return 0;
+    uint32_t o = op;
+    if (run >= 15) {
+        if (L == 0) d[o] = (uint8_t)(15u << 4);
+        ++o;
+        const uint32_t ext = (run - 15) / 255 + 1, rem = (run - 15) % 255;
+        for (uint32_t c = 0; c < ext; c += 64)
+            if (c + L < ext) d[o + c + L] = (uint8_t)(c + L + 1 < ext ? 255u : rem);
+        o += ext;
+    } else {
+        if (L == 0) d[o] = (uint8_t)(run << 4);
+        ++o;
+    }
+    for (uint32_t c = 0; c < run; c += 64)
+        if (c + L < run) d[o + c + L] = s[anchor + c + L];
+    op = o + run;
+}
+    return (int32_t)op;
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(64) k_encode_hc(const uint8_t* __restrict__ src, uint64_t srcSize,
+                                                  uint32_t blockSize, uint8_t* __restrict__ slots,
+                                                  uint64_t slotStride, uint32_t capOverride,
+                                                  const uint16_t* __restrict__ delta, uint32_t maxAttempts,
+                                                  int32_t* __restrict__ csize) {
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
+    const uint32_t cap = capOverride == 0xFFFFFFFFu ? n : capOverride;   // lz4mt: cap = n
+    HcBlock B{(g_cu8*)src + off, n, (g_cu16*)delta + off, maxAttempts, maxAttempts > 128};
+    const int32_t r = encode_block_hc(B, (g_u8*)slots + (uint64_t)b * slotStride, cap);
+    if (laneid() == 0) csize[b] = r;
+}
+
+// level -> maxNbAttempts (lz4 1.9.3 clTable, levels 1..9; < 1 = default 9)
+uint32_t hc_attempts(int level) {
+    static const uint32_t kA[10] = {2, 2, 2, 4, 8, 16, 32, 64, 128, 256};
+    if (level < 1) level = 9;
+    return level > 9 ? 0u : kA[level];
+}
+
+hipError_t launch_encode_hc(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                            uint8_t* slots, uint64_t slotStride, uint32_t capOverride, int level, uint16_t* delta,
+                            int32_t* csize, hipStream_t st) {
+    const uint32_t att = hc_attempts(level);
+    if (att == 0) return hipErrorInvalidValue;
+    if (nBlocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hc_prev, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, delta);
+    hipLaunchKernelGGL(k_encode_hc, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, slotStride,
+                       capOverride, delta, att, csize);
+    return hipGetLastError();
+}
+
+}  // namespace lz4mt

@@ -167,4 +167,57 @@ inline Lz4MtResult parse_header(const uint8_t* p, size_t avail, Lz4MtStreamDescr
     return LZ4MT_RESULT_OK;
 }
 
+// Replays, block by block, the state that decides how the reference's
+// block-dependent compressor (compressBlockDependency, src/lz4mt.cpp:460-538)
+// calls LZ4 1.9.3's LZ4_compress_limitedOutput_continue: its input buffer of
+// max(blockMax + 64 KiB, 1088 KiB) bytes, LZ4_slideInputBuffer when the next
+// block would not fit (it returns the stream's dictionary pointer in 1.9.3),
+// and the stream's dictionary bookkeeping in LZ4_compress_fast_continue
+// (renormalisation, tiny-dictionary reset, overlap trimming, prefix vs
+// external-dictionary mode, dictSmall).  For 1 and 4 MiB blocks the
+// reference reads each block over its own dictionary (its frames then need
+// not decode back); those sizes follow one contiguous buffer instead -- the
+// same stream without that defect.
+// next() returns the block's catch-up bounds and dictSmall limit in the
+// coordinates of k_encode_linked (block at 65536, history below).
+struct BdSim {
+    uint64_t bm = 0, bufSize = 0;   // bufSize 0: one contiguous buffer
+    uint64_t inStart = 0, dict = 0, dictSize = 0, cur = 0;
+    bool dictNull = true;
+    explicit BdSim(int blockMaxId) {
+        bm = (uint64_t)1 << (8 + 2 * blockMaxId);
+        const uint64_t b = bm + 65536, m = (1024 + 64) * 1024;
+        bufSize = blockMaxId <= 5 ? (b > m ? b : m) : 0;
+    }
+    void next(uint32_t n, uint32_t* lowIn, uint32_t* lowDict, uint32_t* candLow) {
+        if (bufSize && inStart + bm > bufSize) inStart = dict;   // translate()
+        uint64_t dictEnd = dict + dictSize;
+        if (cur + n > 0x80000000ull) {                           // LZ4_renormDictT
+            cur = 65536;
+            if (dictSize > 65536) dictSize = 65536;
+            dict = dictEnd - dictSize;
+        }
+        if ((uint32_t)(dictSize - 1) < 3u && (dictNull || dictEnd != inStart)) {   // invalidate tiny dictionaries
+            dictSize = 0; dict = inStart; dictNull = false; dictEnd = inStart;
+        }
+        const uint64_t srcEnd = inStart + n;
+        if (!dictNull && srcEnd > dict && srcEnd < dictEnd) {   // overlapping input / dictionary
+            dictSize = dictEnd - srcEnd;
+            if (dictSize > 65536) dictSize = 65536;
+            if (dictSize < 4) dictSize = 0;
+            dict = dictEnd - dictSize;
+        }
+        const bool prefix = !dictNull && dictEnd == inStart;
+        const bool small = dictSize < 65536 && dictSize < cur;
+        const uint32_t ds = (uint32_t)(dictSize < 65536 ? dictSize : 65536);
+        *lowDict = 65536 - ds;
+        *lowIn = prefix ? 65536 - ds : 65536;
+        *candLow = small ? 65536 - ds : 0;
+        cur += n;
+        if (prefix) dictSize += n;
+        else { dict = inStart; dictSize = n; dictNull = false; }
+        inStart += n;
+    }
+};
+
 }  // namespace lz4mt

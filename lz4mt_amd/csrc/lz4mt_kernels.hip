@@ -170,14 +170,14 @@ struct SrcView {
         ring[w & kRingMaskW] = a;
         ring[(w + 1) & kRingMaskW] = b;
     }
-    __device__ __forceinline__ void init() {
-        B = 0;
-        for (uint32_t c = 0; c < kRingE; c += 512) {
+    __device__ __forceinline__ void init(uint32_t b0 = 0) {   // b0: a multiple of 512
+        B = b0;
+        for (uint32_t c = b0; c < b0 + kRingE; c += 512) {
             uint32_t a, b;
             fetch(c, a, b);
             store(c, a, b);
         }
-        pfPos = kRingE;
+        pfPos = b0 + kRingE;
         fetch(pfPos, pa, pb);
         WAVE_SYNC();
     }
@@ -296,38 +296,56 @@ __device__ __forceinline__ void put_head(OutView& O, uint32_t op, uint32_t lit, 
     put_ext(O, op + 1, ext_len(lit), lit >= 15 ? (lit - 15) % 255 : 0);
 }
 
-template <bool U16, bool TAG, bool ST>
+// Block-dependent (-BD) parameters of encode_block<..., LINK = true>: the
+// block is compressed as one step of LZ4 1.9.3's LZ4_compress_fast_continue
+// (byU32 table carried over from the previous blocks, history before the
+// block).  Positions are "s'-coordinates": s points 64 KiB before the block,
+// so the block is [kLinkO0, kLinkO0 + len) and its history [0, kLinkO0).
+//   lowIn / lowDict  catch-up lower bound (lz4's lowLimit) for candidates in
+//                    the block / in the history: the source start in
+//                    usingExtDict mode, the prefix start in withPrefix64k mode
+//   candLow          dictSmall: candidates below it are out of the valid area
+//   fresh            a new stream: the table starts at the block's position 0
+constexpr uint32_t kLinkO0 = 65536;
+struct LinkArgs {
+    uint32_t lowIn, lowDict, candLow;
+    bool fresh;
+};
+
+template <bool U16, bool TAG, bool ST, bool LINK = false>
 __device__ int32_t encode_block(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
                                 l_u32* __restrict__ Traw, l_u8* __restrict__ S, l_u32* __restrict__ ringE,
-                                l_u8* __restrict__ outRing, uint64_t* acc) {
+                                l_u8* __restrict__ outRing, uint64_t* acc, LinkArgs lk = LinkArgs{0, 0, 0, true}) {
     const uint32_t L = laneid();
     uint64_t ts = STAMP_T();
-    const uint32_t bound = n + n / 255 + 16;
+    const uint32_t o0 = LINK ? kLinkO0 : 0u;   // position of the block's first byte
+    const uint32_t blen = n - o0;
+    const uint32_t bound = blen + blen / 255 + 16;
     const bool limited = cap < bound;
-    if (n == 0) {
+    if (blen == 0) {
         if (limited && cap == 0) return 0;
         if (L == 0) d[0] = 0;
         return 1;
     }
     l_u16* T16 = (l_u16*)Traw;
-    {
+    if (!LINK || lk.fresh) {
         // a fresh entry is position 0 -- a real candidate in LZ4 1.9.3 --
         // so tagged tables start with the tag of the bytes at 0
-        const uint32_t t0 = TAG ? (cand_tag(ld32u(s)) << kPosBits) : 0u;
+        const uint32_t t0 = TAG ? (cand_tag(ld32u(s)) << kPosBits) : o0;
         l_u4* T4 = (l_u4*)Traw;
         for (uint32_t i = L; i < 1024; i += 64) T4[i] = (v4u){t0, t0, t0, t0};
     }
     SrcView V{s, n, ringE, 0, 0, 0, 0};
-    V.init();
+    V.init(o0);
     OutView O{d, outRing, 0};
 
     const uint32_t mflimitP1 = n - kMfLimit + 1;
     const uint32_t matchlimit = n - kLastLiterals;
-    uint32_t anchor = 0, op = 0;
+    uint32_t anchor = o0, op = 0;
 
-    if (n < (uint32_t)kMinLength) goto last_literals;
+    if (blen < (uint32_t)kMinLength) goto last_literals;
     {
-        Win W{1, 0, 0, 0, 1, 0};  // T[h(0)] = 0; search from ip = 1
+        Win W{1, 0, o0, 0, o0 + 1, 0};  // T[h(0)] = 0; search from ip = 1
         for (;;) {
             // ---------------- one probe window ----------------
             if (ST) acc[10] += 1;
@@ -378,7 +396,7 @@ __device__ int32_t encode_block(g_cu8* __restrict__ s, uint32_t n, g_u8* __restr
             // candidate outside the ring, confirmed in the count round trip
             bool ok = false, maybe = false;
             if (live && !isIns && !term) {
-                const bool distok = U16 || (cand + kDistMax >= p);
+                const bool distok = (U16 || (cand + kDistMax >= p)) && (!LINK || cand >= lk.candLow);
                 if (distok) {
                     if (TAG && pred < 0 && !V.in_ring(cand, 4)) maybe = (told >> kPosBits) == mytag;
                     else ok = (V.rd4(cand) == w0);
@@ -402,7 +420,10 @@ __device__ int32_t encode_block(g_cu8* __restrict__ s, uint32_t n, g_u8* __restr
                 // Catch-up and forward count in one round: with back = catch-up
                 // length, LZ4_count from the caught-up position equals
                 // back + count from ip+4 (the skipped bytes are known equal).
-                maxb = wasTest ? 0u : min(ip - anchor, cd);
+                {
+                    const uint32_t lowL = !LINK ? 0u : (cd >= o0 ? lk.lowIn : lk.lowDict);
+                    maxb = wasTest ? 0u : min(ip - anchor, cd > lowL ? cd - lowL : 0u);
+                }
                 lim = matchlimit - (ip + kMinMatch);
                 V.cover(min(ip + kMinMatch + 256, n));
                 // round-0 operands (the cd side is the global round trip)
@@ -1069,6 +1090,59 @@ __global__ void __launch_bounds__(64) k_encode16(const uint8_t* __restrict__ src
     if (laneid() == 0) csize[b] = r;
 }
 
+// Block-dependent frames (-BD, reference compressBlockDependency,
+// src/lz4mt.cpp:460-538): ONE wave encodes the blocks in order, as lz4's
+// LZ4_compress_limitedOutput_continue does (cap = inSize - 1): the byU32
+// table stays in LDS from block to block (rebased to the next block's
+// coordinates, entries older than 64 KiB dropped) and each block sees the 64
+// KiB of input before it (src[-65536, 0) must be readable from block 1 on:
+// the previous batch's tail when called per batch).  `table` (16 KiB) passes
+// the table between calls: read unless `fresh`, written at the end.  The
+// per-block lz4 mode (prefix / external dictionary, dictionary size) comes
+// from the host's replay of the reference's buffer handling (LinkPlan).
+__global__ void __launch_bounds__(64) k_encode_linked(const uint8_t* __restrict__ src, uint64_t srcSize,
+                                                      uint32_t blockSize, uint32_t nBlocks,
+                                                      uint8_t* __restrict__ slots, const LinkPlan* __restrict__ plan,
+                                                      uint32_t* __restrict__ table, int fresh,
+                                                      int32_t* __restrict__ csize) {
+    ENCODE_LDS
+    l_u32* Tl = (l_u32*)T;
+    l_u8* Sl = (l_u8*)S;
+    l_u8* Xl = (l_u8*)X;
+    const uint32_t L = laneid();
+    if (!fresh) {
+        for (uint32_t i = L; i < 4096; i += 64) Tl[i] = table[i];
+        WAVE_SYNC();
+    }
+    for (uint32_t b = 0; b < nBlocks; ++b) {
+        const uint64_t off = (uint64_t)b * blockSize;
+        const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
+        const LinkPlan pl = plan[b];
+        const LinkArgs lk{pl.lowIn, pl.lowDict, pl.candLow, fresh && b == 0};
+        const int32_t r = encode_block<false, false, false, true>(gptr(src) + off - kLinkO0, kLinkO0 + n,
+                                                                  gptr(slots) + off, n - 1, Tl, Sl, (l_u32*)Xl,
+                                                                  Xl + kRingE, nullptr, lk);
+        if (L == 0) csize[b] = r;
+        WAVE_SYNC();
+        // the next block's coordinates: x -> x - n; older than the window -> 0
+        for (uint32_t i = L; i < 4096; i += 64) {
+            const uint32_t e = Tl[i];
+            Tl[i] = e > n ? e - n : 0u;
+        }
+        WAVE_SYNC();
+    }
+    for (uint32_t i = L; i < 4096; i += 64) table[i] = Tl[i];
+}
+
+hipError_t launch_encode_linked(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                                uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh, int32_t* csize,
+                                hipStream_t st) {
+    if (nBlocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_encode_linked, dim3(1), dim3(64), 0, st, src, srcSize, blockSize, nBlocks, slots, plan, table,
+                       fresh ? 1 : 0, csize);
+    return hipGetLastError();
+}
+
 hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks, uint8_t* slots,
                          uint64_t slotStride, uint32_t capOverride, int32_t* csize, hipStream_t st) {
     if (nBlocks == 0) return hipSuccess;
@@ -1132,6 +1206,7 @@ struct Dec {
     uint32_t la;          // lookahead: lane L holds bytes [labase + 4L, labase + 4L + 4)
     int64_t flushed;      // [0, flushed) stored to dst
     int64_t completed;    // [0, completed) known complete in memory
+    int32_t lowP;         // lowest position a match may read: 0, or -65536 with a 64 KiB prefix before dst
 
     __device__ __forceinline__ void refill(int64_t i) {
         const uintptr_t base = (reinterpret_cast<uintptr_t>(src) + (uintptr_t)i) & ~uintptr_t(15);
@@ -1225,7 +1300,7 @@ struct Dec {
                         const uint32_t kq = (L * magic) >> 16;   // L / offset for L < 64
                         sp = o + L - (int64_t)(kq + 1) * offset;
                     }
-                    v = (sp >= o - kRing) ? ring[sp & (kRing - 1)] : dst[sp];
+                    v = (sp >= o - kRing && sp >= 0) ? ring[sp & (kRing - 1)] : dst[sp];
                 }
                 ring[(o + L) & (kRing - 1)] = (uint8_t)v;
             }
@@ -1240,7 +1315,7 @@ struct Dec {
     __device__ __forceinline__ void copy_seq(int64_t ipl, int64_t opl, int64_t lit, uint32_t off, int64_t mlen) {
         const int64_t tot = lit + mlen;
         if (tot <= 64 && (int64_t)off >= tot && (int64_t)off <= kRing - 128 && ipl >= wlo &&
-            ipl + lit <= wlo + kInWin) {
+            ipl + lit <= wlo + kInWin && opl + lit >= (int64_t)off) {
             STAMP_ADD(0, ts);
             if (ST) acc[6] += 1;
             flush_to(opl);
@@ -1365,13 +1440,16 @@ struct Dec {
         const int32_t lp = ipT + (int32_t)e1;                // literal start
         const int32_t om = oj + (int32_t)lit;                // match output start
         const int32_t src = om - (int32_t)off;
-        const int32_t ringLo = op + 4096 - kRing;
+        const int32_t ringLo = max(op + 4096 - kRing, 0);   // prefix bytes (< 0) are never in the ring
         // 4. fast-loop conditions (lz4 1.9.3, see decode_block)
         bool ok = act && off != 0 && !(m15 && b2 == 255) && incl <= 4096;
         ok = ok && (l15 ? (ipT < iend - 15 && ipT + 1 < iend - 15 && oj + (int32_t)lit <= oend - 32 &&
                            lp + (int32_t)lit <= iend - 32)
                         : ipT <= iend - 17);
-        ok = ok && om >= (int32_t)off;
+        ok = ok && om - (int32_t)off >= lowP;
+        // a prefix source running into the block reads bytes not yet flushed
+        // from the ring: the serial path copies those byte by byte
+        ok = ok && !(src < 0 && src + (int32_t)mlen > 0);
         ok = ok && (!m15 || lp + (int32_t)lit + 3 < iend - kLastLiterals + 1);
         ok = ok && om + (int32_t)mlen < oend - 64;
         ok = ok && !(src < ringLo && mlen > 128);   // far loads carry at most 128 bytes
@@ -1410,8 +1488,9 @@ struct Dec {
                 fv[g] = 0; fv2[g] = 0;
                 if ((uint32_t)g < nf8) {
                     const v4u q = fprm[g];   // bytes past the match repeat its last one (never written)
-                    fv[g] = dst[q.x + min(L, q.z - 1)];
-                    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)q.z) > 64) fv2[g] = dst[q.x + min(L + 64, q.z - 1)];
+                    const int64_t fs = (int32_t)q.x;   // a prefix source is negative
+                    fv[g] = dst[fs + min(L, q.z - 1)];
+                    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)q.z) > 64) fv2[g] = dst[fs + min(L + 64, q.z - 1)];
                 }
             }
         }
@@ -1527,8 +1606,9 @@ struct Dec {
                 const int j = __ffsll((long long)farLeft) - 1;
                 const uint32_t js = (uint32_t)rdlane((uint32_t)src, j), jm = rdlane(mlen, j);
                 const uint32_t jo = (uint32_t)rdlane((uint32_t)om, j);
-                const uint32_t a0 = L < jm ? (uint32_t)dst[js + L] : 0u;
-                const uint32_t a1 = L + 64 < jm ? (uint32_t)dst[js + 64 + L] : 0u;
+                const int64_t jsS = (int32_t)js;
+                const uint32_t a0 = L < jm ? (uint32_t)dst[jsS + L] : 0u;
+                const uint32_t a1 = L + 64 < jm ? (uint32_t)dst[jsS + 64 + L] : 0u;
                 if (L < jm) ring[(jo + L) & (kRing - 1)] = (uint8_t)a0;
                 if (L + 64 < jm) ring[(jo + 64 + L) & (kRing - 1)] = (uint8_t)a1;
                 farLeft &= farLeft - 1;
@@ -1627,7 +1707,7 @@ __device__ int32_t decode_block(Dec<ST>& D, int64_t cap) {
         match = op - (int64_t)offset;
         length = token & 15;
         if (length == 15) {
-            if (match < 0) goto output_error;
+            if (match < D.lowP) goto output_error;
             e = D.rvl(ip, iend - kLastLiterals + 1, true, false, ext);
             length += ext;
             if (e != 0) goto output_error;
@@ -1636,14 +1716,14 @@ __device__ int32_t decode_block(Dec<ST>& D, int64_t cap) {
         } else {
             length += kMinMatch;
             if (op + length >= oend - 64) goto safe_match_copy;
-            if (match >= 0 && offset >= 8) {
+            if (match >= D.lowP && offset >= 8) {
                 PHYS_CHECK(op + length);
                 D.copy_seq(plIp, plOp, plLen, offset, length);
                 op += length;
                 continue;
             }
         }
-        if (match < 0) goto output_error;
+        if (match < D.lowP) goto output_error;
         cpy = op + length;
         PHYS_CHECK(cpy);
         D.copy_seq(plIp, plOp, plLen, offset, length);
@@ -1663,7 +1743,7 @@ safe_decode:
             offset = D.in8(ip) | (D.in8(ip + 1) << 8);
             ip += 2;
             match = op - (int64_t)offset;
-            if (length != 15 && offset >= 8 && match >= 0) {
+            if (length != 15 && offset >= 8 && match >= D.lowP) {
                 PHYS_CHECK(op + length + kMinMatch);
                 D.copy_seq(plIp, plOp, plLen, offset, length + kMinMatch);
                 op += length + kMinMatch;
@@ -1702,7 +1782,7 @@ safe_decode:
         }
         length += kMinMatch;
     safe_match_copy:
-        if (match < 0) goto output_error;
+        if (match < D.lowP) goto output_error;
         cpy = op + length;
         if (cpy > oend - kLastLiterals) goto output_error;
         PHYS_CHECK(cpy);
@@ -1762,6 +1842,7 @@ __global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ frame
         D.la = 0;
         D.flushed = 0;
         D.completed = 0;
+        D.lowP = 0;
         res = decode_block(D, (int64_t)blockMax);
     }
     if (laneid() == 0) dsize[b] = res;
@@ -1792,12 +1873,125 @@ __global__ void __launch_bounds__(64) k_decode_stats(const uint8_t* __restrict__
     D.la = 0;
     D.flushed = 0;
     D.completed = 0;
+    D.lowP = 0;
     const int32_t res = decode_block(D, (int64_t)blockMax);
     acc[5] = __builtin_amdgcn_s_memtime() - t0;
     if (laneid() == 0) {
         dsize[b] = res;
         for (int i = 0; i < 16; ++i) stats[b * 16 + i] = acc[i];
     }
+}
+
+// byte copy by one wave; 16-byte pieces when both ends share the alignment
+__device__ void wave_copy(g_u8* __restrict__ dst, g_cu8* __restrict__ src, int64_t n) {
+    const uint32_t L = laneid();
+    int64_t i = 0;
+    if (((reinterpret_cast<uintptr_t>(dst) ^ reinterpret_cast<uintptr_t>(src)) & 15) == 0) {
+        const int64_t head = min<int64_t>(n, (int64_t)((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15));
+        if ((int64_t)L < head) dst[L] = src[L];
+        i = head;
+        for (; i + 1024 <= n; i += 1024) *(g_u4*)(dst + i + 16 * L) = *(g_cu4*)(src + i + 16 * L);
+    }
+    for (; i < n; i += 64)
+        if (i + L < n) dst[i + L] = src[i + L];
+}
+
+// Block-dependent frames (-BD, reference decompressBlockDependency,
+// src/lz4mt.cpp:737-845): ONE wave decodes the blocks in order.  Each block
+// is checked against its checksum BEFORE it is decoded (the reference's
+// order there), then decoded by LZ4_decompress_safe_withPrefix64k rules
+// into `slot` = [64 KiB history | blockMax], the history being the last 64
+// KiB of (hist ++ this call's output so far); the bytes are then appended
+// to out.  `hist` (64 KiB, device) is the history before the call (zeros
+// for a new frame: the reference's zero-filled MemPool buffer) and receives
+// the history after it.  status[0] = blocks completed, status[1] = the
+// Lz4MtResult of the block that stopped the call (0 = none).
+__global__ void __launch_bounds__(64) k_decode_linked(const uint8_t* __restrict__ frame,
+                                                      const BlockRec* __restrict__ recs, uint32_t nBlocks,
+                                                      uint32_t blockMax, uint8_t* __restrict__ out, uint64_t outCap,
+                                                      uint8_t* __restrict__ slot, uint8_t* __restrict__ hist,
+                                                      const uint32_t* __restrict__ digest, int bck,
+                                                      int32_t* __restrict__ dsize, int32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kWinAlloc];
+    const uint32_t L = laneid();
+    g_u8* const sl = gptr(slot);
+    g_u8* const o = gptr(out);
+    int64_t opos = 0;
+    uint32_t b = 0;
+    int32_t code = 0;
+    // history [0, 65536) of the slot: the 64 KiB before output position opos
+    auto load_hist = [&](int64_t at) {
+        for (int64_t i = 16 * L; i < 65536; i += 1024) {
+            const int64_t x = at - 65536 + i;
+            v4u v;
+            if (x >= 0) {
+                g_cu8* p = (g_cu8*)o + x;
+                v = (v4u){ld32u(p), ld32u(p + 4), ld32u(p + 8), ld32u(p + 12)};
+            } else {   // (partly) before this call's output: bytes of hist
+                uint8_t t[16];
+                for (int k = 0; k < 16; ++k) t[k] = x + k < 0 ? gptr(hist)[65536 + x + k] : o[x + k];
+                v = (v4u){(uint32_t)t[0] | t[1] << 8 | t[2] << 16 | (uint32_t)t[3] << 24,
+                          (uint32_t)t[4] | t[5] << 8 | t[6] << 16 | (uint32_t)t[7] << 24,
+                          (uint32_t)t[8] | t[9] << 8 | t[10] << 16 | (uint32_t)t[11] << 24,
+                          (uint32_t)t[12] | t[13] << 8 | t[14] << 16 | (uint32_t)t[15] << 24};
+            }
+            *(g_u4*)(sl + i) = v;
+        }
+        // the slot is reused block after block: wait for these stores and
+        // drop the vector L1's lines of it (the previous block's decode read
+        // them), or this block's far reads could see the old bytes
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        WAVE_SYNC();
+    };
+    for (; b < nBlocks; ++b) {
+        const BlockRec r = recs[b];
+        const int64_t len = r.bits & 0x7FFFFFFFu;
+        if (bck && digest[b] != r.checksum) { code = 16; break; }   // BLOCK_CHECKSUM_MISMATCH, nothing written
+        load_hist(opos);
+        int32_t res;
+        if (r.bits & 0x80000000u) {
+            copy_raw(gptr(frame) + r.offset, sl + 65536, len);
+            res = (int32_t)len;
+        } else {
+            Dec<false> D;
+            D.acc = nullptr;
+            D.ts = 0;
+            D.src = gptr(frame) + r.offset;
+            D.len = len;
+            D.dst = sl + 65536;
+            D.physcap = blockMax;
+            D.ring = (l_u8*)ring;
+            D.win = (l_u8*)win;
+            D.wlo = INT64_MIN / 4;
+            D.labase = INT64_MIN / 4;
+            D.la = 0;
+            D.flushed = 0;
+            D.completed = 0;
+            D.lowP = -65536;
+            res = decode_block(D, (int64_t)blockMax);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        WAVE_SYNC();
+        if (L == 0) dsize[b] = res;
+        if (res < 0) { code = 18; break; }                               // DECOMPRESS_FAIL
+        if ((uint64_t)opos + (uint64_t)res > outCap) { code = 1; break; }   // ERROR: output too small
+        wave_copy(o + opos, sl + 65536, res);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the next history read sees these bytes
+        WAVE_SYNC();
+        opos += res;
+    }
+    load_hist(opos);   // the history after this call -> hist
+    for (int64_t i = 16 * L; i < 65536; i += 1024) *(g_u4*)(gptr(hist) + i) = *(g_cu4*)(sl + i);
+    if (L == 0) { status[0] = (int32_t)b; status[1] = code; }
+}
+
+hipError_t launch_decode_linked(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax,
+                                uint8_t* out, uint64_t outCap, uint8_t* slot, uint8_t* hist, const uint32_t* digest,
+                                int blockChecksum, int32_t* dsize, int32_t* status, hipStream_t st) {
+    hipLaunchKernelGGL(k_decode_linked, dim3(1), dim3(64), 0, st, frame, recs, nBlocks, blockMax, out, outCap, slot,
+                       hist, digest, blockChecksum, dsize, status);
+    return hipGetLastError();
 }
 
 hipError_t launch_decode_stats(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax,

@@ -37,6 +37,8 @@ def _load():
     lib.orc_lz4_compress_bound.restype = ctypes.c_int
     lib.orc_lz4_compress.argtypes = [u8p, u8p, ctypes.c_int, ctypes.c_int]
     lib.orc_lz4_decompress_safe.argtypes = [u8p, u8p, ctypes.c_int, ctypes.c_int]
+    lib.orc_lz4hc_compress.argtypes = [u8p, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.orc_lz4_decompress_safe_prefix64k.argtypes = [u8p, u8p, ctypes.c_int, ctypes.c_int]
     lib.orc_frame_bound.restype = sz
     lib.orc_frame_bound.argtypes = [sz, ctypes.POINTER(FrameParams)]
     lib.orc_frame_compress.restype = sz
@@ -72,11 +74,30 @@ def compress_block(data, cap=None):
     return dst.raw[:n]
 
 
+def compress_block_hc(data, cap=None, level=9):
+    """LZ4_compressHC2_limitedOutput(src, dst, n, cap, level) restated (levels 1..9); b'' when it does not fit."""
+    cap = len(data) if cap is None else cap
+    dst = ctypes.create_string_buffer(max(cap, lib.orc_lz4_compress_bound(len(data))) + 16)
+    n = lib.orc_lz4hc_compress(_buf(data), dst, len(data), cap, level)
+    if n < 0:
+        raise ValueError("HC levels above 9 (the optimal parser) are not restated")
+    return dst.raw[:n]
+
+
 def decompress_block(block, cap):
     """LZ4_decompress_safe restated: (ret, bytes)."""
     dst = ctypes.create_string_buffer(max(cap, 1) + 16)
     n = lib.orc_lz4_decompress_safe(_buf(block), dst, len(block), cap)
     return n, (dst.raw[:n] if n > 0 else b"")
+
+
+def decompress_block_prefix64k(block, cap, prefix=b""):
+    """LZ4_decompress_safe_withPrefix64k restated: (ret, bytes); ``prefix`` =
+    the history before the block (zero-padded to 64 KiB on the left)."""
+    hist = (bytes(65536) + bytes(prefix))[-65536:]
+    buf = ctypes.create_string_buffer(hist + bytes(max(cap, 1) + 16), 65536 + max(cap, 1) + 16)
+    n = lib.orc_lz4_decompress_safe_prefix64k(_buf(block), ctypes.byref(buf, 65536), len(block), cap)
+    return n, (buf.raw[65536:65536 + n] if n > 0 else b"")
 
 
 def params(block_max_id=7, stream_checksum=True, block_checksum=False, stream_size=None):

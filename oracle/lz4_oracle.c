@@ -271,7 +271,12 @@ static int rvl(const uint8_t* src, sll srcSize, sll* ip, sll lencheck, int loopC
 
 static inline unsigned in8(const uint8_t* src, sll n, sll i) { return (i >= 0 && i < n) ? src[i] : 0; }
 
-int orc_lz4_decompress_safe(const uint8_t* src, uint8_t* dst, int srcSize, int outputSize) {
+/* lowP = lowest output position a match may read: 0 for
+ * LZ4_decompress_safe (lowPrefix = dst), -65536 for
+ * LZ4_decompress_safe_withPrefix64k (lowPrefix = dst - 64 KB; then no offset
+ * can point before it, and the fast-copy test `dict == withPrefix64k ||
+ * match >= lowPrefix` is the same comparison). */
+static int decompress_generic(const uint8_t* src, uint8_t* dst, int srcSize, int outputSize, sll lowP) {
     if (src == NULL) return -1;
     const sll N = srcSize;
     sll ip = 0, op = 0, cpy, match;
@@ -309,7 +314,7 @@ int orc_lz4_decompress_safe(const uint8_t* src, uint8_t* dst, int srcSize, int o
         length = token & 15;
         if (length == 15) {
             size_t ext;
-            if (match < 0) goto output_error;
+            if (match < lowP) goto output_error;
             e = rvl(src, N, &ip, iend - LASTLITERALS + 1, 1, 0, &ext);
             length += ext;
             if (e != 0) goto output_error;
@@ -318,13 +323,13 @@ int orc_lz4_decompress_safe(const uint8_t* src, uint8_t* dst, int srcSize, int o
         } else {
             length += MINMATCH;
             if (op + (sll)length >= oend - 64) goto safe_match_copy;
-            if (match >= 0 && offset >= 8) {
+            if (match >= lowP && offset >= 8) {
                 lz77_copy(dst, op, match, (sll)length);
                 op += (sll)length;
                 continue;
             }
         }
-        if (match < 0) goto output_error;
+        if (match < lowP) goto output_error;
         cpy = op + (sll)length;
         lz77_copy(dst, op, match, (sll)length);
         op = cpy;
@@ -341,7 +346,7 @@ safe_decode:
             offset = in8(src, N, ip) | (in8(src, N, ip + 1) << 8);
             ip += 2;
             match = op - (sll)offset;
-            if (length != 15 && offset >= 8 && match >= 0) {
+            if (length != 15 && offset >= 8 && match >= lowP) {
                 lz77_copy(dst, op, match, (sll)length + MINMATCH);
                 op += (sll)length + MINMATCH;
                 continue;
@@ -380,7 +385,7 @@ safe_decode:
         }
         length += MINMATCH;
     safe_match_copy:
-        if (match < 0) goto output_error;
+        if (match < lowP) goto output_error;
         cpy = op + (sll)length;
         if (cpy > oend - 12 && cpy > oend - LASTLITERALS) goto output_error;
         lz77_copy(dst, op, match, (sll)length);
@@ -390,6 +395,16 @@ safe_decode:
 
 output_error:
     return (int)(-ip) - 1;
+}
+
+int orc_lz4_decompress_safe(const uint8_t* src, uint8_t* dst, int srcSize, int outputSize) {
+    return decompress_generic(src, dst, srcSize, outputSize, 0);
+}
+
+/* LZ4_decompress_safe_withPrefix64k (lz4 1.9.3): the 64 KiB before dst are
+ * readable history (ref src/lz4mt.cpp:813-818, block-dependent frames). */
+int orc_lz4_decompress_safe_prefix64k(const uint8_t* src, uint8_t* dst, int srcSize, int outputSize) {
+    return decompress_generic(src, dst, srcSize, outputSize, -65536);
 }
 
 /* ===================================================================== */
@@ -556,7 +571,6 @@ int orc_frame_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t outC
         if ((uint8_t)((orc_xxh32(b, 2 + (hasSize ? 8 : 0), 0) >> 8) & 0xFF) != b[2 + (hasSize ? 8 : 0)]) {
             result = R_HC; break;
         }
-        if (!indep) { result = R_DEP; break; }
         const size_t bm = block_max(bid);
         /* scan blocks */
         size_t cap = 64, nb = 0;
@@ -584,6 +598,45 @@ int orc_frame_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t outC
             j->src = bp; j->len = (int)len; j->out = dst + out; j->raw = (bits & RAW_BIT) != 0;
             j->bck = ck; j->hasBck = bck; j->bm = (int)bm; j->res = R_OK; j->dsz = 0;
             out += j->raw ? len : bm; /* provisional slot; compacted below */
+        }
+        if (!indep) {
+            /* decompressBlockDependency (ref src/lz4mt.cpp:737-845): blocks in
+               order, each checked BEFORE it is decoded or written, decoded
+               with LZ4_decompress_safe_withPrefix64k against a history of 64
+               KiB of zeros (the zero-filled MemPool buffer) followed by all
+               of this frame's output so far */
+            /* the blocks read before a read error are still decoded and
+               written (the reference handles each block as it is read); a
+               block's own failure comes first in stream order */
+            uint8_t* hist = (uint8_t*)calloc(65536 + bm, 1);
+            size_t w = frameOut;
+            int bres = R_OK;
+            for (size_t i = 0; i < nb && bres == R_OK; i++) {
+                djob* j = &jobs[i];
+                if (j->hasBck && orc_xxh32(j->src, (size_t)j->len, 0) != j->bck) { bres = R_BCK; break; }
+                const size_t have = w - frameOut, keep = have < 65536 ? have : 65536;
+                memset(hist, 0, 65536);
+                memcpy(hist + 65536 - keep, dst + w - keep, keep);
+                int d;
+                if (j->raw) { memcpy(hist + 65536, j->src, (size_t)j->len); d = j->len; }
+                else d = orc_lz4_decompress_safe_prefix64k(j->src, hist + 65536, j->len, (int)bm);
+                if (d < 0) { bres = R_DECOMP; break; }
+                if (w + (size_t)d > outCap) { bres = R_ERROR; break; }
+                memcpy(dst + w, hist + 65536, (size_t)d);
+                w += (size_t)d;
+            }
+            if (bres != R_OK && (result == R_OK || result == R_ERROR)) result = bres;
+            free(hist);
+            free(jobs);
+            out = w;
+            if (result != R_OK) break;
+            if (!eos) { result = R_RD_BSIZE; break; }
+            if (sck) {
+                if (ms_read(&s, b, 4) != 4) { result = R_RD_SCK; break; }
+                if (orc_xxh32(dst + frameOut, out - frameOut, 0) != rd32(b)) { result = R_SCK; break; }
+            }
+            if (s.pos == s.n) break;
+            continue;
         }
         /* decode (in parallel), then compact slots in block order */
         parallel_for(nb, nthreads, djob_fn, jobs);

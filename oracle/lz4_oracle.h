@@ -55,7 +55,15 @@ int orc_lz4_compress(const uint8_t* src, uint8_t* dst, int n, int cap);
 int orc_lz4_decompress_safe(const uint8_t* src, uint8_t* dst, int srcSize,
                             int cap);
 
-/* ---- lz4mt frame (independent blocks only) ---------------------------- */
+/* LZ4-HC 1.9.3 LZ4_compress_HC (= LZ4_compressHC2_limitedOutput, lz4mt's
+ * codec for levels >= 3): levels 1..9 (hash chain); -1 for 10..12. */
+int orc_lz4hc_compress(const uint8_t* src, uint8_t* dst, int n, int cap, int level);
+
+/* LZ4_decompress_safe_withPrefix64k 1.9.3: dst[-65536..-1] is history. */
+int orc_lz4_decompress_safe_prefix64k(const uint8_t* src, uint8_t* dst,
+                                      int srcSize, int cap);
+
+/* ---- lz4mt frame ------------------------------------------------------- */
 typedef struct {
     int      streamChecksum;   /* FLG bit 2 */
     int      blockChecksum;    /* FLG bit 4 */
@@ -71,7 +79,7 @@ size_t orc_frame_bound(size_t n, const orc_frame_params* p);
 size_t orc_frame_compress(const uint8_t* src, size_t n, uint8_t* dst,
                           const orc_frame_params* p, int nthreads);
 /* Decodes a byte stream of concatenated frames the way lz4mtDecompress
- * does.  Returns an Lz4MtResult code; *outSize receives decoded bytes.
+ * does, block-dependent (-BD) frames included (decompressBlockDependency).  Returns an Lz4MtResult code; *outSize receives decoded bytes.
  * `outCap` bounds the output; exceeding it returns LZ4MT_RESULT_ERROR. */
 int orc_frame_decompress(const uint8_t* src, size_t n, uint8_t* dst,
                          size_t outCap, size_t* outSize, int nthreads);

@@ -62,3 +62,25 @@ def checksum_of_checksums(t, chunk=16 << 20):
     import lz4mt_amd as L
     d = L.xxh32_chunks(t, chunk).cpu().numpy().astype("<u4").tobytes()
     return xxhash.xxh32(d).intdigest()
+
+
+def bd_input(n, seed):
+    """Block-dependent (-BD) test input with matches across block
+    boundaries: App. F text with pieces re-copied from up to 64 KiB back
+    (deterministic on any host; tests/golden/make_golden.py uses it)."""
+    import random
+
+    from oracle import gen_synthetic
+    rnd = random.Random(seed)
+    base = gen_synthetic(n + 65536, seed)
+    out = bytearray()
+    pos = 0
+    while len(out) < n:
+        if len(out) > 70000 and rnd.random() < 0.5:
+            a = len(out) - rnd.randrange(4, 65535)
+            out += out[a:a + rnd.randrange(4, 300)]
+        else:
+            k = rnd.randrange(1, 200)
+            out += base[pos:pos + k]
+            pos += k
+    return bytes(out[:n])

@@ -26,6 +26,8 @@ import xxhash
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+sys.path.insert(0, os.path.dirname(HERE))
+from conftest import bd_input  # noqa: E402  (the -BD test input, shared with the GPU tests)
 LZ4 = ctypes.CDLL("/lib/x86_64-linux-gnu/liblz4.so.1")
 CLI = "/opt/conda/bin/lz4"
 
@@ -68,6 +70,146 @@ def frame(data, bid=7, sck=True, bck=False):
     if sck:
         out += struct.pack("<I", xxh(data))
     return bytes(out)
+
+
+# ---- block-dependent (-BD) frames ------------------------------------------
+def _bd_records(blocks, bck):
+    out = bytearray()
+    for payload, raw in blocks:
+        out += struct.pack("<I", len(payload) | (0x80000000 if raw else 0)) + payload
+        if bck:
+            out += struct.pack("<I", xxh(payload))
+    return bytes(out)
+
+
+def _bd_header(bid, sck, bck):
+    flg = (1 << 6) | (int(bck) << 4) | (int(sck) << 2)   # FLG.5 (block independence) clear
+    desc = bytes([flg, bid << 4])
+    return struct.pack("<I", 0x184D2204) + desc + bytes([(xxh(desc) >> 8) & 0xFF])
+
+
+def bd_frame_reference(data, bid, sck, bck):
+    """compressBlockDependency (reference src/lz4mt.cpp:460-538) replayed on
+    liblz4 1.9.3 with its exact call sequence: a max(bm + 64 KiB, 1088 KiB)
+    input buffer, LZ4_resetStreamState, LZ4_compress_limitedOutput_continue
+    (cap = inSize - 1), LZ4_slideInputBuffer when the next block would not
+    fit.  In 1.9.3 LZ4_slideInputBuffer returns the dictionary pointer, so
+    for 1 and 4 MiB blocks the next block is read over its own dictionary
+    and the frame does not decode back; 64 and 256 KiB
+    blocks round-trip."""
+    LZ4.LZ4_slideInputBuffer.restype = ctypes.c_void_p
+    bm = 1 << (8 + 2 * bid)
+    size = max(bm + 65536, (1024 + 64) * 1024)
+    buf = ctypes.create_string_buffer(size)
+    base = ctypes.addressof(buf)
+    dst = ctypes.create_string_buffer(bm + 64)
+    st = ctypes.create_string_buffer(LZ4.LZ4_sizeofStreamState())
+    LZ4.LZ4_resetStreamState(st, buf)
+    ins, pos, blocks = base, 0, []
+    while True:
+        if ins + bm > base + size:
+            ins = LZ4.LZ4_slideInputBuffer(st)
+        chunk = data[pos:pos + bm]
+        if not chunk:
+            break
+        ctypes.memmove(ins, chunk, len(chunk))
+        pos += len(chunk)
+        n = LZ4.LZ4_compress_limitedOutput_continue(st, ctypes.c_void_p(ins), dst, len(chunk), len(chunk) - 1)
+        blocks.append((dst.raw[:n], False) if n > 0 else (chunk, True))
+        ins += len(chunk)
+    tail = b"\0\0\0\0" + (struct.pack("<I", xxh(data)) if sck else b"")
+    return _bd_header(bid, sck, bck) + _bd_records(blocks, bck) + tail
+
+
+def bd_frame_contiguous(data, bid, sck, bck):
+    """The same stream compressed from one contiguous buffer (every block in
+    LZ4 prefix mode after the first), cap = inSize - 1: what the reference's
+    loop computes when its dictionary survives (this library's -BD output
+    for 1 and 4 MiB blocks)."""
+    bm = 1 << (8 + 2 * bid)
+    buf = ctypes.create_string_buffer(data, len(data) + 1)
+    base = ctypes.addressof(buf)
+    dst = ctypes.create_string_buffer(bm + 64)
+    st = ctypes.create_string_buffer(LZ4.LZ4_sizeofStreamState())
+    LZ4.LZ4_resetStreamState(st, buf)
+    blocks = []
+    for off in range(0, len(data), bm):
+        chunk = data[off:off + bm]
+        n = LZ4.LZ4_compress_limitedOutput_continue(st, ctypes.c_void_p(base + off), dst, len(chunk), len(chunk) - 1)
+        blocks.append((dst.raw[:n], False) if n > 0 else (chunk, True))
+    tail = b"\0\0\0\0" + (struct.pack("<I", xxh(data)) if sck else b"")
+    return _bd_header(bid, sck, bck) + _bd_records(blocks, bck) + tail
+
+
+def bd_decode_reference(frame):
+    """decompressBlockDependency (src/lz4mt.cpp:737-845) on liblz4 1.9.3:
+    LZ4_decompress_safe_withPrefix64k over a zeroed 64 KiB + block buffer.
+    Returns the content or None (a block fails to decode)."""
+    bid = (frame[5] >> 4) & 7
+    bck = bool(frame[4] & 0x10)
+    bm = 1 << (8 + 2 * bid)
+    d = ctypes.create_string_buffer(65536 + bm)
+    dbase = ctypes.addressof(d)
+    dptr, pos, out = dbase + 65536, 7, []
+    while True:
+        w = struct.unpack_from("<I", frame, pos)[0]
+        pos += 4
+        if w == 0:
+            return b"".join(out)
+        n = w & 0x7FFFFFFF
+        payload = frame[pos:pos + n]
+        pos += n + (4 if bck else 0)
+        if w & 0x80000000:
+            out.append(payload)
+            if n >= 65536:
+                ctypes.memmove(dbase, payload[-65536:], 65536)
+                dptr = dbase + 65536
+                continue
+            ctypes.memmove(dptr, payload, n)
+            k = n
+        else:
+            k = LZ4.LZ4_decompress_safe_withPrefix64k(payload, ctypes.c_void_p(dptr), n, bm)
+            if k < 0:
+                return None
+            out.append(ctypes.string_at(dptr, k))
+        dptr += k
+        if dbase + 65536 + bm - dptr < bm:
+            ctypes.memmove(dbase, dptr - 65536, 65536)
+            dptr = dbase + 65536
+
+
+BD_CASES = [  # (name, bytes, seed, block id, stream checksum, block checksum)
+    ("bd_b4_sX", 1_500_000, 11, 4, False, True), ("bd_b4_SX", 1_500_000, 11, 4, True, True),
+    ("bd_b5_Sx", 1_500_000, 12, 5, True, False),
+]
+BD_KNOWN = [  # larger -BD frames pinned by size + XXH32 only: (name, bytes, seed, id, sck, bck, writer)
+    ("bd_b4_9m", 9_437_184 + 4321, 21, 4, False, True, "reference"),
+    ("bd_b5_9m", 9_437_184 + 4321, 22, 5, True, True, "reference"),
+    ("bd_b6_9m", 9_437_184 + 4321, 23, 6, False, True, "contiguous"),
+    ("bd_b7_9m", 9_437_184 + 4321, 24, 7, True, False, "contiguous"),
+]
+
+
+def bd_main(manifest):
+    manifest["bd_frames"], manifest["bd_known"] = [], []
+    for name, n, seed, bid, sck, bck in BD_CASES:
+        data = bd_input(n, seed)
+        f = bd_frame_reference(data, bid, sck, bck)
+        assert bd_decode_reference(f) == data, name
+        open(os.path.join(HERE, "frames", f"{name}.lz4"), "wb").write(f)
+        manifest["bd_frames"].append({"name": name, "bytes": n, "seed": seed, "bid": bid, "stream_checksum": sck,
+                                      "block_checksum": bck, "file": f"frames/{name}.lz4", "size": len(f),
+                                      "xxh32": xxh(f), "content_xxh32": xxh(data)})
+    for name, n, seed, bid, sck, bck, writer in BD_KNOWN:
+        data = bd_input(n, seed)
+        f = (bd_frame_reference if writer == "reference" else bd_frame_contiguous)(data, bid, sck, bck)
+        ok = bd_decode_reference(f) == data
+        assert ok, name
+        ref = bd_frame_reference(data, bid, sck, bck)
+        manifest["bd_known"].append({"name": name, "bytes": n, "seed": seed, "bid": bid, "stream_checksum": sck,
+                                     "block_checksum": bck, "writer": writer, "size": len(f), "xxh32": xxh(f),
+                                     "content_xxh32": xxh(data), "reference_frame_identical": ref == f,
+                                     "reference_frame_roundtrips": bd_decode_reference(ref) == data})
 
 
 def cli_frame(data, bid, sck, bck):
@@ -190,6 +332,21 @@ def main():
             manifest["crafted"].append({"name": name, "block_hex": blk.hex(), "cap": cap, "ret": r,
                                         "out_hex": out.hex() if r > 0 and len(out) <= 64 else None,
                                         "out_xxh32": xxh(out) if r >= 0 else None})
+    # LZ4-HC block vectors: LZ4_compressHC2_limitedOutput = LZ4_compress_HC
+    # (the reference's codec for levels >= 3, src/main.cpp:778-785)
+    LZ4.LZ4_compress_HC.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    manifest["hc_blocks"] = []
+    hc_inputs = dict(cases)
+    hc_inputs["bdmix300k"] = bd_input(300_000, 31)
+    for name, data in hc_inputs.items():
+        blk = data[:300_000]
+        for level in (3, 4, 6, 8, 9):
+            for cap in sorted({len(blk), max(len(blk) - 1, 0)}):
+                dst = ctypes.create_string_buffer(max(cap, 1) + len(blk) // 255 + 64)
+                r = LZ4.LZ4_compress_HC(blk, dst, len(blk), cap, level)
+                manifest["hc_blocks"].append({"input": name, "n": len(blk), "cap": cap, "level": level, "ret": r,
+                                              "sha1": hashlib.sha1(dst.raw[:r]).hexdigest()})
+    bd_main(manifest)
     json.dump(manifest, open(os.path.join(HERE, "golden.json"), "w"), indent=0)
     print("frames", len(manifest["frames"]), "blocks", len(manifest["blocks"]), "decode", len(manifest["decode"]),
           "crafted", len(manifest["crafted"]), "cli mismatches",

@@ -1,0 +1,125 @@
+"""GPU parity for block-dependent (-BD) frames, SURVEY.md §8(f) #4.
+
+Compress: the reference's compressBlockDependency (src/lz4mt.cpp:460-538)
+replayed on liblz4 1.9.3 with its exact call sequence gives the golden
+frames (tests/golden/make_golden.py: bd_frame_reference for 64 / 256 KiB
+blocks, bd_frame_contiguous for 1 / 4 MiB blocks, where the reference reads
+each block over its own dictionary -- DESIGN.md).  The device encoder must
+write the same bytes, through the device frame engine and through
+lz4mtCompress (one batch and many).
+
+Decompress: decompressBlockDependency (src/lz4mt.cpp:737-845): the golden
+frames decode to their inputs; damaged frames give the oracle's result code
+and bytes (the block checksum is checked before a block is written there).
+"""
+import pytest
+import torch
+import xxhash
+
+import oracle
+from conftest import bd_input, read_golden
+
+pytestmark = pytest.mark.gpu
+
+L = None
+
+
+@pytest.fixture(scope="module", autouse=True)
+def lib():
+    global L
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    import lz4mt_amd
+    L = lz4mt_amd
+    return L
+
+
+def dev(b):
+    t = torch.empty(max(len(b), 1), dtype=torch.uint8, device="cuda")
+    if b:
+        t[:len(b)].copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
+    return t[:len(b)]
+
+
+def host(t):
+    return bytes(t.cpu().numpy().tobytes())
+
+
+def _sd(f):
+    return L.make_sd(f["bid"], f["stream_checksum"], f["block_checksum"], block_dependence=True)
+
+
+def test_bd_golden_frames_device(golden):
+    for f in golden["bd_frames"]:
+        data = bd_input(f["bytes"], f["seed"])
+        frame = read_golden(f["file"])
+        got = host(L.compress_frame(dev(data), _sd(f)))
+        assert got == frame, f["name"]
+        out, r = L.decompress_frame(dev(frame))
+        assert r == 0 and host(out) == data, f["name"]
+
+
+def test_bd_known_answers_device(golden):
+    for f in golden["bd_known"]:
+        data = bd_input(f["bytes"], f["seed"])
+        assert xxhash.xxh32(data).intdigest() == f["content_xxh32"]
+        frame = L.compress_frame(dev(data), _sd(f))
+        assert (frame.numel(), L.xxh32(frame)) == (f["size"], f["xxh32"]), f["name"]
+        out, r = L.decompress_frame(frame)
+        assert r == 0 and L.xxh32(out) == f["content_xxh32"], f["name"]
+
+
+@pytest.mark.parametrize("mode", ["DEVICE", "PARALLEL", "SEQUENTIAL"])
+@pytest.mark.parametrize("batches", ["one", "many"])
+def test_bd_callback_api(golden, monkeypatch, mode, batches):
+    """lz4mtCompress / lz4mtDecompress on -BD frames: the device engine in
+    every mode (the reference bypasses ctx.compress / ctx.decompress for
+    them); with small batches the lz4 table and the 64 KiB history carry
+    across batches."""
+    if batches == "many":
+        monkeypatch.setenv("LZ4MT_AMD_BATCH0_MIB", "1")
+        monkeypatch.setenv("LZ4MT_AMD_BATCH_MIB", "1")
+    m = {"DEVICE": L.MODE_DEVICE, "PARALLEL": L.MODE_PARALLEL, "SEQUENTIAL": L.MODE_SEQUENTIAL}[mode]
+    for f in golden["bd_frames"] + [k for k in golden["bd_known"] if k["bid"] >= 6]:
+        data = bd_input(f["bytes"], f["seed"])
+        r, frame = L.compress(data, _sd(f), mode=m)
+        assert r == 0, (f["name"], L.result_to_string(r))
+        if "file" in f:
+            assert frame == read_golden(f["file"]), (f["name"], mode, batches)
+        else:
+            assert (len(frame), xxhash.xxh32(frame).intdigest()) == (f["size"], f["xxh32"]), (f["name"], mode)
+        r, out, sd = L.decompress(frame, len(data) + 64, mode=m)
+        assert r == 0 and out == data, (f["name"], mode, batches, L.result_to_string(r))
+        assert sd.flg.blockIndependence == 0
+
+
+@pytest.mark.parametrize("api", ["device", "DEVICE", "PARALLEL"])
+def test_bd_damaged_frames_vs_oracle(golden, api):
+    """Flipped bytes, truncations and rewritten size words in -BD frames:
+    the oracle's result code (decompressBlockDependency order: size, data,
+    checksum word, checksum, decode, write) and its bytes."""
+    import random
+    rnd = random.Random({"device": 1, "DEVICE": 2, "PARALLEL": 3}[api])
+    f = golden["bd_frames"][0]   # 64 KiB blocks, block checksums
+    data = bd_input(f["bytes"], f["seed"])
+    frame = read_golden(f["file"])
+    cap = len(data) + (1 << 20)
+    for it in range(40):
+        b = bytearray(frame)
+        kind = it % 3
+        if kind == 0:
+            b[rnd.randrange(7, len(b))] ^= 1 << rnd.randrange(8)
+        elif kind == 1:
+            del b[rnd.randrange(8, len(b)):]
+        else:
+            a = rnd.randrange(7, len(b) - 4)
+            b[a:a + 4] = rnd.randrange(1 << 32).to_bytes(4, "little")
+        rw, ow = oracle.decompress_frame(bytes(b), cap)
+        if api == "device":
+            out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+            o, r = L.decompress_frame(dev(bytes(b)), out=out, check=False)
+            got = host(o)
+        else:
+            r, got, _ = L.decompress(bytes(b), cap, mode=L.MODE_DEVICE if api == "DEVICE" else L.MODE_PARALLEL)
+        assert r == rw, (it, kind, L.result_to_string(r), L.result_to_string(rw))
+        assert got == ow, (it, kind, len(got), len(ow))

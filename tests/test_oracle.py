@@ -146,3 +146,131 @@ def test_differential_vs_liblz4():
             want = L.LZ4_decompress_safe(bytes(m), o, len(m), cap)
             got, out = oracle.decompress_block(bytes(m), cap)
             assert got == want and (got < 0 or out == o.raw[:got])
+
+
+# ---------------------------------------------------------------------------
+# block-dependent (-BD) frames: decompressBlockDependency restated
+# (src/lz4mt.cpp:737-845), LZ4_decompress_safe_withPrefix64k restated
+# ---------------------------------------------------------------------------
+def test_bd_golden_frames_decode(golden):
+    from conftest import bd_input
+    for f in golden["bd_frames"]:
+        data = bd_input(f["bytes"], f["seed"])
+        assert xxhash.xxh32(data).intdigest() == f["content_xxh32"]
+        frame = read_golden(f["file"])
+        assert xxhash.xxh32(frame).intdigest() == f["xxh32"]
+        r, out = oracle.decompress_frame(frame, len(data) + (1 << 20))
+        assert r == 0 and out == data, f["name"]
+        # a flipped payload byte: the block checksum fails before the block is written
+        if f["block_checksum"]:
+            bad = bytearray(frame); bad[300] ^= 1
+            r, out = oracle.decompress_frame(bytes(bad), len(data) + (1 << 20))
+            assert r == 16 and out == b""
+
+
+@pytest.mark.skipif(not os.path.exists(LIBLZ4), reason="liblz4 not present")
+def test_prefix64k_decode_vs_liblz4():
+    """Differential against liblz4's LZ4_decompress_safe_withPrefix64k on
+    linked blocks and their mutations: same return value, same bytes."""
+    from conftest import bd_input
+    lz = ctypes.CDLL(LIBLZ4)
+    data = bd_input(600_000, 5)
+    buf = ctypes.create_string_buffer(data, len(data))
+    base = ctypes.addressof(buf)
+    st = ctypes.create_string_buffer(lz.LZ4_sizeofStreamState())
+    lz.LZ4_resetStreamState(st, buf)
+    dst = ctypes.create_string_buffer(1 << 17)
+    rnd = random.Random(9)
+    bm = 65536
+    for off in range(0, len(data), bm):
+        n = min(bm, len(data) - off)
+        c = lz.LZ4_compress_limitedOutput_continue(st, ctypes.c_void_p(base + off), dst, n, n - 1)
+        if c <= 0:
+            continue
+        blk = dst.raw[:c]
+        prefix = data[max(0, off - 65536):off]
+        variants = [blk]
+        for _ in range(12):
+            m = bytearray(blk)
+            m[rnd.randrange(len(m))] = rnd.randrange(256)
+            variants.append(bytes(m))
+        variants.append(blk[:rnd.randrange(1, len(blk))])
+        for v in variants:
+            for cap in (n, n - 1, bm, n + 100):
+                want_buf = ctypes.create_string_buffer((bytes(65536) + prefix)[-65536:] + bytes(cap + 64))
+                want = lz.LZ4_decompress_safe_withPrefix64k(v, ctypes.byref(want_buf, 65536), len(v), cap)
+                got, out = oracle.decompress_block_prefix64k(v, cap, prefix)
+                assert got == want, (off, cap, got, want)
+                if got >= 0:
+                    assert out == want_buf.raw[65536:65536 + got]
+
+
+@pytest.mark.skipif(not os.path.exists(LIBLZ4), reason="liblz4 not present")
+def test_reference_bd_compress_defect_at_1mib_blocks():
+    """Why this library does not copy the reference's -BD compressor for 1
+    and 4 MiB blocks: replayed on liblz4 1.9.3 with its exact call sequence,
+    LZ4_slideInputBuffer hands back the dictionary pointer and the next block
+    is read over its own dictionary -- on this input the 1 MiB-block frame
+    does not decode back to the input (64 and 256 KiB blocks do)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_golden as G
+    data = oracle.gen_synthetic(12 << 20, 42)
+    assert G.bd_decode_reference(G.bd_frame_reference(data, 6, False, True)) != data
+    assert G.bd_decode_reference(G.bd_frame_reference(data, 4, False, True)) == data
+    # the contiguous stream (this library's 1/4 MiB -BD output) does decode back
+    assert G.bd_decode_reference(G.bd_frame_contiguous(data, 6, False, True)) == data
+
+
+# ---------------------------------------------------------------------------
+# LZ4-HC 1.9.3 (levels 3..9): the reference's codec for compression levels >= 3
+# ---------------------------------------------------------------------------
+def test_hc_blocks_vs_golden(golden, golden_inputs):
+    import hashlib
+    from conftest import bd_input
+    inputs = dict(golden_inputs)
+    inputs["bdmix300k"] = bd_input(300_000, 31)
+    for v in golden["hc_blocks"]:
+        data = inputs[v["input"]][:v["n"]]
+        c = oracle.compress_block_hc(data, v["cap"], v["level"])
+        assert len(c) == v["ret"] and hashlib.sha1(c).hexdigest() == v["sha1"], v
+
+
+def _hc_mixed(n, seed):
+    rnd = random.Random(seed)
+    syn = oracle.gen_synthetic(1 << 20, seed)
+    out = bytearray()
+    while len(out) < n:
+        k = rnd.randrange(7)
+        if k == 0:
+            a = rnd.randrange(len(syn) - 5000)
+            out += syn[a:a + rnd.randrange(50, 5000)]
+        elif k == 1:
+            out += bytes([rnd.randrange(256)]) * rnd.randrange(1, 3000)
+        elif k == 2 and len(out) > 10:
+            a = rnd.randrange(max(0, len(out) - 70000), len(out))
+            out += out[a:a + rnd.randrange(4, 3000)]
+        elif k == 3:
+            out += oracle.gen_random(rnd.randrange(10, 500), rnd.randrange(1 << 30))
+        elif k == 4:
+            p = bytes(rnd.randrange(256) for _ in range(rnd.randrange(2, 9)))
+            out += p * rnd.randrange(2, 300)
+        elif k == 5:
+            out += bytes(rnd.randrange(2) for _ in range(rnd.randrange(10, 2000)))
+        else:
+            out += b"\0" * rnd.randrange(1, 70000)
+    return bytes(out[:n])
+
+
+@pytest.mark.skipif(not os.path.exists(LIBLZ4), reason="liblz4 not present")
+def test_hc_differential_vs_liblz4():
+    lz = ctypes.CDLL(LIBLZ4)
+    lz.LZ4_compress_HC.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    for seed in range(24):
+        rnd = random.Random(seed)
+        d = _hc_mixed(rnd.choice([13, 100, 5000, 65547, 200_000, 1 << 20]), seed)
+        for level in (3, rnd.choice([4, 5, 6, 7, 8]), 9):
+            for cap in (len(d), len(d) - 1, len(d) // 2):
+                dst = ctypes.create_string_buffer(max(cap, 1) + len(d) // 255 + 64)
+                r = lz.LZ4_compress_HC(d, dst, len(d), cap, level)
+                assert oracle.compress_block_hc(d, cap, level) == dst.raw[:r], (seed, len(d), level, cap)
