@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--block-id", type=int, default=7, help="4..7 = 64 KiB..4 MiB")
     p.add_argument("--stream-checksum", action="store_true",
                    help="default lz4mt flags (FLG.2 content checksum, no block checksum) instead of -Sx -BX")
+    p.add_argument("--level", type=int, default=0, help="compression level: 3..9 = LZ4-HC (not the headline)")
+    p.add_argument("--block-dependent", action="store_true", help="-BD frames (serial; not the headline)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-mib", type=int, default=1024, help="CPU baseline sample (MiB, all threads)")
     p.add_argument("--decompress-only", action="store_true",
@@ -188,19 +190,29 @@ def main():
     sck = a.stream_checksum
     if sck and world > 1:
         raise SystemExit("the content checksum (FLG.2) is one serial chain over the whole stream: it does not shard")
-    sd = L.make_sd(a.block_id, stream_checksum=sck, block_checksum=not sck)
-    flg = 0x64 if sck else 0x70
+    sd = L.make_sd(a.block_id, stream_checksum=sck, block_checksum=not sck, block_dependence=a.block_dependent)
+    flg = (0x64 if sck else 0x70) & ~(0x20 if a.block_dependent else 0)
+    if (a.level >= 3 or a.block_dependent) and world > 1:
+        raise SystemExit("--level / --block-dependent are single-GPU measurements")
     cap = L.frame_bound(n, sd)
     frame_buf = torch.empty(cap, dtype=torch.uint8, device=dev)
-    ws = L.compress_workspace(n, sd, device=dev)
+    ws = L.compress_workspace(n, sd, device=dev, level=a.level)
     out = torch.empty(n + (1 << 20), dtype=torch.uint8, device=dev)
     fsz = torch.zeros(2, dtype=torch.int64, device=dev)
 
     def compress():
-        r = L.lib.lz4mtHipCompressFrameAsync(
-            ctypes.c_void_p(src.data_ptr()), n, ctypes.c_void_p(frame_buf.data_ptr()), cap,
-            ctypes.c_void_p(fsz.data_ptr()), ctypes.byref(sd), ctypes.c_void_p(ws.data_ptr()), ws.numel(),
-            ctypes.c_void_p(stream.cuda_stream))
+        if sck:   # the synchronous call: the serial content checksum runs on the host beside the encode
+            hs = ctypes.c_uint64(0)
+            r = L.lib.lz4mtHipCompressFrameEx(
+                ctypes.c_void_p(src.data_ptr()), n, ctypes.c_void_p(frame_buf.data_ptr()), cap, ctypes.byref(hs),
+                ctypes.byref(sd), a.level, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                ctypes.c_void_p(stream.cuda_stream))
+            fsz[0] = hs.value
+        else:
+            r = L.lib.lz4mtHipCompressFrameAsyncEx(
+                ctypes.c_void_p(src.data_ptr()), n, ctypes.c_void_p(frame_buf.data_ptr()), cap,
+                ctypes.c_void_p(fsz.data_ptr()), ctypes.byref(sd), a.level, ctypes.c_void_p(ws.data_ptr()),
+                ws.numel(), ctypes.c_void_p(stream.cuda_stream))
         if r != 0:
             raise L.Lz4MtError(r, "compress")
 
@@ -287,20 +299,24 @@ def main():
     dec_avg = sum(dec_ms) / len(dec_ms) if dec_ms else None
     body = frame_len - 7 - 4 - (4 if sck else 0)
     alg = n + body                           # algorithmic bytes per launch: in + out
+    # the kernels the timing marks bracket in this mode
+    enc_k = ("k_encode_linked_round" if a.block_dependent else "k_encode_hc" if a.level >= 3 else "k_encode")
+    dec_k = "k_decode_linked" if a.block_dependent else "k_decode"
     roof = dec_roof = None
     if enc_avg:
         ach = alg / (enc_avg * 1e-3) / 1e9
-        tr, why = pmc_traffic("k_encode", n, bm, flg)
+        tr, why = pmc_traffic(enc_k, n, bm, flg)
         roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBPS, 5), "traffic": round(tr["bytes"]) if tr else None,
-                "kernel": "k_encode", "kernel_ms": round(enc_avg, 3), "algorithmic_bytes": alg,
+                "kernel": enc_k + (" (+ k_link_settle rounds, serial fallback)" if a.block_dependent else ""),
+                "kernel_ms": round(enc_avg, 3), "algorithmic_bytes": alg,
                 "traffic_detail": tr or why}
     if dec_avg:
         ach = alg / (dec_avg * 1e-3) / 1e9
-        tr, why = pmc_traffic("k_decode", n, bm, flg)
+        tr, why = pmc_traffic(dec_k, n, bm, flg)
         dec_roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBPS, 5), "traffic": round(tr["bytes"]) if tr else None,
-                    "kernel": "k_decode", "kernel_ms": round(dec_avg, 3), "algorithmic_bytes": alg,
+                    "kernel": dec_k, "kernel_ms": round(dec_avg, 3), "algorithmic_bytes": alg,
                     "traffic_detail": tr or why}
     if a.decompress_only and dec_roof:   # the decode kernel is the dominant one here
         roof = dec_roof
@@ -308,7 +324,8 @@ def main():
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(a.cpu_mib, a.block_id, sck)
-        flags = "default flags (FLG.2 content checksum)" if sck else "-Sx -BX"
+        flags = ("default flags (FLG.2 content checksum)" if sck else "-Sx -BX") + \
+            (" -BD" if a.block_dependent else "") + (f" level {a.level} (LZ4-HC)" if a.level >= 3 else "")
         line = {
             "metric": "device-resident LZ4 GiB/s (compress, decompress) on 4 MiB blocks at 1/2/4/8 MI355X",
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": K, "warmup": a.warmup,

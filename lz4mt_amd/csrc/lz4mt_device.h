@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace lz4mt {
 
@@ -38,6 +39,7 @@ struct LinkState {
     LinkPlan* plan;
     uint32_t* table;
     bool fresh;
+    uint32_t* rounds;    // parallel rounds' scratch, link_round_bytes(nBlocks) (null: the serial kernel)
 };
 
 // Frame-walk summary written by the walk kernel.
@@ -121,8 +123,35 @@ uint32_t hc_attempts(int level);   // 0 for levels the library does not run (10.
 hipError_t launch_encode_linked(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                                 uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh, int32_t* csize,
                                 hipStream_t st);
+// The block-dependent encode as parallel fixed-point rounds
+// (k_encode_linked_round / k_link_settle; the serial kernel finishes from
+// the first unsettled block if kLinkRounds rounds do not settle).
+constexpr int kLinkRounds = 32;
+uint64_t link_round_bytes(uint64_t nBlocks);   // scratch: entry + exit tables, round control words
+hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                                    uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh,
+                                    uint32_t* scratch, int32_t* csize, int rounds, hipStream_t st);
 hipError_t launch_decode_linked(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax,
                                 uint8_t* out, uint64_t outCap, uint8_t* slot, uint8_t* hist, const uint32_t* digest,
                                 int blockChecksum, int32_t* dsize, int32_t* status, hipStream_t st);
+// The same contract as launch_decode_linked (status, dsize, out, hist in/out),
+// decoded in parallel fixed-point rounds (k_dlink_*; serial finish if
+// `rounds` do not settle).  scratch: dlink_scratch_bytes(nBlocks, blockMax).
+uint64_t dlink_scratch_bytes(uint64_t nBlocks, uint32_t blockMax);
+// LZ4MT_AMD_BD_ROUNDS=k caps the -BD encode's parallel rounds (tests: the
+// serial finish from the first unsettled block); default kLinkRounds
+inline int env_rounds() {
+    const char* e = getenv("LZ4MT_AMD_BD_ROUNDS");
+    return e ? atoi(e) : kLinkRounds;
+}
+// LZ4MT_AMD_BD_SERIAL=1: the one-wave -BD kernels only (A/B and tests)
+inline bool bd_serial() {
+    const char* e = getenv("LZ4MT_AMD_BD_SERIAL");
+    return e && e[0] == '1';
+}
+hipError_t launch_decode_linked_par(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax,
+                                    uint8_t* out, uint64_t outCap, uint8_t* hist, const uint32_t* digest,
+                                    int blockChecksum, int32_t* dsize, int32_t* status, uint8_t* scratch, int rounds,
+                                    hipStream_t st);
 
 }  // namespace lz4mt

@@ -218,12 +218,82 @@ uint8_t* small_dev() {
     return p;
 }
 
+// The content checksum (FLG.2) is ONE serial XXH32 chain:
+// a GPU runs it on one wavefront at ~0.8 GB/s, a host core at several
+// times that.  The synchronous frame calls therefore hash on the host:
+// the bytes stream device -> pinned host memory in 64 MiB chunks on a copy
+// stream (double-buffered: chunk i+1 in flight while chunk i is hashed),
+// beside whatever the GPU does meanwhile (the encode reads the same input).
+class HostHasher {
+public:
+    static constexpr uint64_t kChunk = 64ull << 20;
+    ~HostHasher() { release(); }
+    // XXH32 of d[0, len) once `ready` (recorded on the producing stream) has completed
+    bool hash(const uint8_t* d, uint64_t len, hipEvent_t ready, uint32_t* out) {
+        if (!ensure()) return false;
+        HostXxh32 x(0);
+        if (ready && hipStreamWaitEvent(cp_, ready, 0) != hipSuccess) return false;
+        const uint64_t nc = (len + kChunk - 1) / kChunk;
+        auto issue = [&](uint64_t i) {
+            const uint64_t o = i * kChunk, k = std::min(kChunk, len - o);
+            return hipMemcpyAsync(pin_[i & 1], d + o, k, hipMemcpyDeviceToHost, cp_) == hipSuccess &&
+                   hipEventRecord(ev_[i & 1], cp_) == hipSuccess;
+        };
+        if (nc && !issue(0)) return false;
+        for (uint64_t i = 0; i < nc; ++i) {
+            if (i + 1 < nc && !issue(i + 1)) return false;   // its buffer held chunk i-1, hashed already
+            if (hipEventSynchronize(ev_[i & 1]) != hipSuccess) return false;
+            const uint64_t o = i * kChunk;
+            x.update(pin_[i & 1], std::min(kChunk, len - o));
+        }
+        *out = x.digest();
+        return true;
+    }
+    hipStream_t stream() const { return cp_; }
+    uint32_t* word() const { return word_; }   // pinned: a digest to copy to the device
+
+private:
+    bool ensure() {
+        int d = -1;
+        if (hipGetDevice(&d) != hipSuccess) return false;
+        if (cp_ && d == dev_) return true;
+        release();
+        dev_ = d;
+        if (hipStreamCreateWithFlags(&cp_, hipStreamNonBlocking) != hipSuccess) { cp_ = nullptr; return false; }
+        for (int i = 0; i < 2; ++i)
+            if (hipHostMalloc(reinterpret_cast<void**>(&pin_[i]), kChunk, 0) != hipSuccess ||
+                hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming) != hipSuccess) {
+                release();
+                return false;
+            }
+        if (hipHostMalloc(reinterpret_cast<void**>(&word_), 64, 0) != hipSuccess) { release(); return false; }
+        return true;
+    }
+    void release() {
+        if (cp_) { hipStreamSynchronize(cp_); hipStreamDestroy(cp_); }
+        for (int i = 0; i < 2; ++i) {
+            if (pin_[i]) hipHostFree(pin_[i]);
+            if (ev_[i]) hipEventDestroy(ev_[i]);
+            pin_[i] = nullptr; ev_[i] = nullptr;
+        }
+        if (word_) hipHostFree(word_);
+        word_ = nullptr; cp_ = nullptr; dev_ = -1;
+    }
+    hipStream_t cp_ = nullptr;
+    uint8_t* pin_[2] = {nullptr, nullptr};
+    hipEvent_t ev_[2] = {nullptr, nullptr};
+    uint32_t* word_ = nullptr;
+    int dev_ = -1;
+};
+thread_local HostHasher g_hasher;
+
 }  // namespace
 
 // ===========================================================================
 // internal C++ API shared with the host frame engine (lz4mt_frame.cpp)
 // ===========================================================================
 namespace lz4mt {
+
 
 // Compresses nb blocks (block b = src[b*bm, ...), last block short) into a
 // frame BODY (records only) at `body`; total body size written to
@@ -237,7 +307,10 @@ Lz4MtResult device_compress_body(const uint8_t* src, uint64_t n, uint32_t bm, in
     const uint64_t nb = (n + bm - 1) / bm;
     CompressWs w = carve_compress(ws, nb, bm, level);
     g_timing.mark(0, st);
-    if (link)   // block-dependent frame: one wave, blocks in order (k_encode_linked)
+    if (link && link->rounds && !bd_serial())   // block-dependent: parallel rounds (exact; serial fallback)
+        HIPCHK(launch_encode_linked_par(src, n, bm, (uint32_t)nb, w.slots, link->plan, link->table, link->fresh,
+                                        link->rounds, w.csize, env_rounds(), st));
+    else if (link)             // block-dependent frame: one wave, blocks in order (k_encode_linked)
         HIPCHK(launch_encode_linked(src, n, bm, (uint32_t)nb, w.slots, link->plan, link->table, link->fresh, w.csize,
                                     st));
     else if (level >= 3)   // LZ4-HC, a wave per block (lz4mt_hc.hip)
@@ -376,7 +449,7 @@ extern "C" uint64_t lz4mtHipCompressWorkspaceSize(uint64_t srcSize, const Lz4MtS
 
 static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
                                        uint64_t* d_frameSize, const Lz4MtStreamDescriptor* sd, int level, void* d_ws,
-                                       uint64_t wsSize, hipStream_t st, void** ownedWs) {
+                                       uint64_t wsSize, hipStream_t st, void** ownedWs, bool hostHash) {
     if (!sd || !d_frame || (!d_src && srcSize)) return LZ4MT_RESULT_BAD_ARG;
     const Lz4MtResult v = validate_sd(sd);
     if (v != LZ4MT_RESULT_OK) return v;
@@ -407,7 +480,14 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
     // (SURVEY.md §0.5).  It reads only d_src, so it starts at t = 0 on its
     // own stream, beside the encode, and the finalize waits for it.
     const bool sck = sd->flg.streamChecksum != 0;
-    const bool sckSide = sck && !capturing && auxStream.ensure();
+    // the synchronous call hashes on the host (HostHasher), beside the
+    // encode; the asynchronous one stays on the device (one wavefront)
+    thread_local hipEvent_t srcReady = nullptr, sumDone = nullptr;
+    const bool sckHost = sck && hostHash && !capturing &&
+                         (srcReady || hipEventCreateWithFlags(&srcReady, hipEventDisableTiming) == hipSuccess) &&
+                         (sumDone || hipEventCreateWithFlags(&sumDone, hipEventDisableTiming) == hipSuccess);
+    if (sckHost) HIPCHK(hipEventRecord(srcReady, st));
+    const bool sckSide = sck && !sckHost && !capturing && auxStream.ensure();
     if (sckSide) {
         HIPCHK(hipEventRecord(auxStream.evIn, st));
         HIPCHK(hipStreamWaitEvent(auxStream.st, auxStream.evIn, 0));
@@ -419,7 +499,7 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
     LinkState ls{};
     const LinkState* lsp = nullptr;
     if (!sd->flg.blockIndependence) {
-        thread_local DevBuf planBuf, tableBuf;
+        thread_local DevBuf planBuf, tableBuf, roundBuf;
         thread_local std::vector<LinkPlan> hplan;
         const uint64_t nb = (srcSize + bm - 1) / bm;
         hplan.assign(std::max<uint64_t>(nb, 1), LinkPlan{});
@@ -427,9 +507,12 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
         for (uint64_t b = 0; b < nb; ++b)
             sim.next((uint32_t)std::min<uint64_t>(bm, srcSize - b * bm), &hplan[b].lowIn, &hplan[b].lowDict,
                      &hplan[b].candLow);
-        if (!planBuf.ensure(hplan.size() * sizeof(LinkPlan)) || !tableBuf.ensure(4096 * 4)) return LZ4MT_RESULT_ERROR;
+        if (!planBuf.ensure(hplan.size() * sizeof(LinkPlan)) || !tableBuf.ensure(4096 * 4) ||
+            !roundBuf.ensure(link_round_bytes(std::max<uint64_t>(nb, 1))))
+            return LZ4MT_RESULT_ERROR;
         HIPCHK(hipMemcpyAsync(planBuf.p, hplan.data(), hplan.size() * sizeof(LinkPlan), hipMemcpyHostToDevice, st));
-        ls = LinkState{reinterpret_cast<LinkPlan*>(planBuf.p), reinterpret_cast<uint32_t*>(tableBuf.p), true};
+        ls = LinkState{reinterpret_cast<LinkPlan*>(planBuf.p), reinterpret_cast<uint32_t*>(tableBuf.p), true,
+                       reinterpret_cast<uint32_t*>(roundBuf.p)};
         lsp = &ls;
     }
     const Lz4MtResult r = device_compress_body(static_cast<const uint8_t*>(d_src), srcSize, bm, sd->flg.blockChecksum,
@@ -439,8 +522,18 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
         if (sckSide) hipStreamWaitEvent(st, auxStream.evOut, 0);   // scratch outlives the side kernel
         return r;
     }
-    if (sckSide) HIPCHK(hipStreamWaitEvent(st, auxStream.evOut, 0));
-    else if (sck) HIPCHK(launch_xxh32_stream(static_cast<const uint8_t*>(d_src), srcSize, w.ssum, st));
+    if (sckHost) {   // the kernels above run while the host hashes
+        uint32_t h = 0;
+        if (!g_hasher.hash(static_cast<const uint8_t*>(d_src), srcSize, srcReady, &h)) return LZ4MT_RESULT_ERROR;
+        *g_hasher.word() = h;
+        HIPCHK(hipMemcpyAsync(w.ssum, g_hasher.word(), 4, hipMemcpyHostToDevice, g_hasher.stream()));
+        HIPCHK(hipEventRecord(sumDone, g_hasher.stream()));
+        HIPCHK(hipStreamWaitEvent(st, sumDone, 0));
+    } else if (sckSide) {
+        HIPCHK(hipStreamWaitEvent(st, auxStream.evOut, 0));
+    } else if (sck) {
+        HIPCHK(launch_xxh32_stream(static_cast<const uint8_t*>(d_src), srcSize, w.ssum, st));
+    }
     g_timing.mark(3, st);
     HIPCHK(launch_frame_finalize(static_cast<uint8_t*>(d_frame), hdr, (uint32_t)hdrLen, recOff,
                                  (uint32_t)((srcSize + bm - 1) / bm), sd->flg.streamChecksum ? w.ssum : nullptr,
@@ -456,7 +549,7 @@ extern "C" Lz4MtResult lz4mtHipCompressFrameAsyncEx(const void* d_src, uint64_t 
     void* owned = nullptr;
     const hipStream_t st = static_cast<hipStream_t>(stream);
     const Lz4MtResult r = compress_frame_impl(d_src, srcSize, d_frame, frameCap, d_frameSize, sd, level, d_workspace,
-                                              workspaceSize, st, &owned);
+                                              workspaceSize, st, &owned, false);
     if (owned) {  // library-owned scratch: must outlive the kernels
         hipStreamSynchronize(st);
         hipFree(owned);
@@ -470,7 +563,8 @@ extern "C" Lz4MtResult lz4mtHipCompressFrameAsync(const void* d_src, uint64_t sr
     void* owned = nullptr;
     const hipStream_t st = static_cast<hipStream_t>(stream);
     const Lz4MtResult r =
-        compress_frame_impl(d_src, srcSize, d_frame, frameCap, d_frameSize, sd, 0, d_workspace, workspaceSize, st, &owned);
+        compress_frame_impl(d_src, srcSize, d_frame, frameCap, d_frameSize, sd, 0, d_workspace, workspaceSize, st, &owned,
+                            false);
     if (owned) {  // library-owned scratch: must outlive the kernels
         hipStreamSynchronize(st);
         hipFree(owned);
@@ -486,7 +580,8 @@ extern "C" Lz4MtResult lz4mtHipCompressFrameEx(const void* d_src, uint64_t srcSi
     uint64_t* dfs = reinterpret_cast<uint64_t*>(small_dev());
     if (!dfs) return LZ4MT_RESULT_ERROR;
     Lz4MtResult r =
-        compress_frame_impl(d_src, srcSize, d_frame, frameCap, dfs, sd, level, d_workspace, workspaceSize, st, &owned);
+        compress_frame_impl(d_src, srcSize, d_frame, frameCap, dfs, sd, level, d_workspace, workspaceSize, st, &owned,
+                            true);
     if (r == LZ4MT_RESULT_OK) {
         uint64_t fs = 0;
         if (hipMemcpyAsync(&fs, dfs, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -812,13 +907,23 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
             // block-dependent frame (decompressBlockDependency, src/lz4mt.cpp:
             // 737-845): one wave decodes the blocks in order, each against the
             // 64 KiB before it (zeros before the frame's first byte)
+            // (parallel rounds, k_dlink_*; LZ4MT_AMD_BD_SERIAL=1: the one-wave kernel)
             thread_local DevBuf slotBuf, histBuf;
-            if (!slotBuf.ensure(65536 + (uint64_t)bm + 64) || !histBuf.ensure(65536)) { result = LZ4MT_RESULT_ERROR; break; }
+            const bool serial = bd_serial();
+            const uint64_t scratch = serial ? 65536 + (uint64_t)bm + 64 : dlink_scratch_bytes(nb, bm);
+            if (!slotBuf.ensure(scratch) || !histBuf.ensure(65536)) { result = LZ4MT_RESULT_ERROR; break; }
             HIPCHK(hipMemsetAsync(histBuf.p, 0, 65536, st));
             if (bck && nb) HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, st));
             const uint64_t room = outCap > opos ? outCap - opos : 0;
-            HIPCHK(launch_decode_linked(f, B.recs, (uint32_t)nb, bm, out + opos, room, slotBuf.p, histBuf.p, B.digest,
-                                        bck, B.dsize, B.status, st));
+            g_timing.mark(1, st);
+            if (serial)
+                HIPCHK(launch_decode_linked(f, B.recs, (uint32_t)nb, bm, out + opos, room, slotBuf.p, histBuf.p,
+                                            B.digest, bck, B.dsize, B.status, st));
+            else
+                HIPCHK(launch_decode_linked_par(f, B.recs, (uint32_t)nb, bm, out + opos, room, histBuf.p, B.digest,
+                                                bck, B.dsize, B.status, slotBuf.p, env_rounds(), st));
+            g_timing.mark(2, st);
+            g_timing.mark(3, st);
             int32_t stat[2] = {0, 0};
             std::vector<int32_t> ds(nb);
             HIPCHK(hipMemcpyAsync(stat, B.status, 8, hipMemcpyDeviceToHost, st));
@@ -897,9 +1002,12 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
             if (next + 4 > frameSize) { opos += produced; result = LZ4MT_RESULT_CANNOT_READ_STREAM_CHECKSUM; break; }
             uint8_t want[4];
             HIPCHK(hipMemcpyAsync(want, f + next, 4, hipMemcpyDeviceToHost, st));
-            HIPCHK(launch_xxh32_stream(out + opos, produced, B.ssum, st));
+            // the serial content checksum on the host (HostHasher)
+            thread_local hipEvent_t outReady = nullptr;
+            if (!outReady) HIPCHK(hipEventCreateWithFlags(&outReady, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(outReady, st));
             uint32_t got = 0;
-            HIPCHK(hipMemcpyAsync(&got, B.ssum, 4, hipMemcpyDeviceToHost, st));
+            if (!g_hasher.hash(out + opos, produced, outReady, &got)) { result = LZ4MT_RESULT_ERROR; break; }
             HIPCHK(hipStreamSynchronize(st));
             next += 4;
             if (got != get32(want)) { opos += produced; result = LZ4MT_RESULT_STREAM_CHECKSUM_MISMATCH; break; }

@@ -530,9 +530,9 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
     BdSim sim(sd->bd.blockMaximumSize);
     std::vector<uint8_t> hist(linked ? 65536 : 0, 0);
     std::vector<LinkPlan> plan;
-    CallBuf table, dplan;
+    CallBuf table, dplan, rounds;
     if (linked && !table.alloc(4096 * 4)) { s.quit(LZ4MT_RESULT_ERROR); return; }
-    uint64_t batch = 0, planCap = 0;
+    uint64_t batch = 0, planCap = 0, roundCap = 0;
     auto fill = [&](Slot& S, bool* stop) -> bool {
         const uint64_t K = batch_blocks(P, bm, batch++), inCap = K * bm;
         if (!S.ensure(pre + inCap, inCap + K * 8 + 64, compress_ws_bytes(inCap, bm, level), 0)) {
@@ -571,7 +571,13 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
                 s.quit(LZ4MT_RESULT_ERROR);
                 return false;
             }
-            ls = LinkState{static_cast<LinkPlan*>(dplan.p), static_cast<uint32_t*>(table.p), batch == 1};
+            if (nb > roundCap) {   // the parallel rounds' entry / exit tables
+                if (rounds.p) { hipStreamSynchronize(S.st); hipFree(rounds.p); rounds.p = nullptr; }
+                if (!rounds.alloc(link_round_bytes(nb))) { s.quit(LZ4MT_RESULT_ERROR); return false; }
+                roundCap = nb;
+            }
+            ls = LinkState{static_cast<LinkPlan*>(dplan.p), static_cast<uint32_t*>(table.p), batch == 1,
+                           static_cast<uint32_t*>(rounds.p)};
             // the history of the next batch: the last 64 KiB of (hist ++ this input)
             if (total >= 65536) memcpy(hist.data(), in + total - 65536, 65536);
             else {
@@ -677,8 +683,9 @@ bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
     PipeShape P = pipe_shape(false);
     if (linked) P.slots = 1;
     CallBuf hist, slotScratch;
-    if (linked && (!hist.alloc(65536) || !slotScratch.alloc(65536 + (size_t)bm + 64) ||
-                   hipMemset(hist.p, 0, 65536) != hipSuccess)) {
+    const bool serialBd = bd_serial();
+    uint64_t scratchCap = 0;   // blocks the linked scratch holds
+    if (linked && (!hist.alloc(65536) || hipMemset(hist.p, 0, 65536) != hipSuccess)) {
         s.quit(LZ4MT_RESULT_ERROR);
         return false;
     }
@@ -706,12 +713,23 @@ bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
         *stop = eos || pending != LZ4MT_RESULT_OK;
         if (nb == 0) return false;
         if (linked) {
+            // scratch: the parallel rounds' slots (one slot for the serial kernel);
+            // one slot pipeline, so the previous batch is done with it
+            const uint64_t need = serialBd ? 65536 + (uint64_t)bm + 64 : dlink_scratch_bytes(nb, bm);
+            if (need > scratchCap) {
+                if (slotScratch.p) { hipStreamSynchronize(S.st); hipFree(slotScratch.p); slotScratch.p = nullptr; }
+                if (!slotScratch.alloc(need)) { s.quit(LZ4MT_RESULT_ERROR); return false; }
+                scratchCap = need;
+            }
+            uint8_t* const scr = static_cast<uint8_t*>(slotScratch.p);
+            uint8_t* const hst = static_cast<uint8_t*>(hist.p);
             if (hipMemcpyAsync(S.dIn, S.hIn, used, hipMemcpyHostToDevice, S.st) != hipSuccess ||
                 hipMemcpyAsync(S.dRecs, S.hRecs, nb * sizeof(BlockRec), hipMemcpyHostToDevice, S.st) != hipSuccess ||
                 (bck && launch_xxh32_frame_blocks(S.dIn, S.dRecs, (uint32_t)nb, S.dDig, S.st) != hipSuccess) ||
-                launch_decode_linked(S.dIn, S.dRecs, (uint32_t)nb, bm, S.dOut, nb * bm,
-                                     static_cast<uint8_t*>(slotScratch.p), static_cast<uint8_t*>(hist.p), S.dDig, bck,
-                                     S.dDs, S.dSt, S.st) != hipSuccess ||
+                (serialBd ? launch_decode_linked(S.dIn, S.dRecs, (uint32_t)nb, bm, S.dOut, nb * bm, scr, hst, S.dDig,
+                                                 bck, S.dDs, S.dSt, S.st)
+                          : launch_decode_linked_par(S.dIn, S.dRecs, (uint32_t)nb, bm, S.dOut, nb * bm, hst, S.dDig,
+                                                     bck, S.dDs, S.dSt, scr, env_rounds(), S.st)) != hipSuccess ||
                 hipMemcpyAsync(S.hDs, S.dDs, nb * 4, hipMemcpyDeviceToHost, S.st) != hipSuccess ||
                 hipMemcpyAsync(S.hSt, S.dSt, 8, hipMemcpyDeviceToHost, S.st) != hipSuccess ||
                 hipMemcpyAsync(S.hOut, S.dOut, nb * bm, hipMemcpyDeviceToHost, S.st) != hipSuccess) {

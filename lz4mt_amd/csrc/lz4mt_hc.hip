@@ -25,7 +25,18 @@
 
 namespace lz4mt {
 
-#define WAVE_SYNC() __builtin_amdgcn_wave_barrier()
+// Lanes of one wavefront hand data to each other through LDS.  LDS
+// operations of a wave execute in order, so no wait is needed, but the
+// COMPILER must neither move LDS accesses across this point nor forward a
+// lane's own store to its later load (another lane may have overwritten the
+// word): wave_barrier alone has no memory effect in LLVM, so the
+// wavefront-scope fences (no instructions on gfx950) carry the ordering.
+#define WAVE_SYNC()                                              \
+    do {                                                         \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   \
+        __builtin_amdgcn_wave_barrier();                         \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
+    } while (0)
 
 typedef const __attribute__((address_space(1))) uint8_t g_cu8;
 typedef __attribute__((address_space(1))) uint8_t g_u8;

@@ -31,10 +31,39 @@
 
 namespace lz4mt {
 
+// LZ4MT_AMD_BD_STATS=1: print the -BD rounds' work (blocks redone per
+// round, first unsettled block) to stderr -- synchronises the stream
+static void link_stats(const char* what, const uint32_t* changed, const uint32_t* firstU, int rounds,
+                       uint32_t nBlocks, hipStream_t st) {
+    const char* e = getenv("LZ4MT_AMD_BD_STATS");
+    if (!e || e[0] != '1') return;
+    uint32_t c[kLinkRounds + 1], f[kLinkRounds + 1];
+    if (hipMemcpyAsync(c, changed, sizeof(c), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(f, firstU, sizeof(f), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return;
+    fprintf(stderr, "[lz4mt -BD %s] %u blocks, queued per round:", what, nBlocks);
+    int last = 0;
+    for (int r = 1; r <= rounds; ++r) if (c[r]) last = r;
+    for (int r = 1; r <= last; ++r) fprintf(stderr, " %u", c[r]);
+    fprintf(stderr, "%s\n", c[rounds] ? " (serial finish)" : "");
+}
+
 // ---------------------------------------------------------------------------
 // small helpers
 // ---------------------------------------------------------------------------
-#define WAVE_SYNC() __builtin_amdgcn_wave_barrier()
+// Lanes of one wavefront hand data to each other through LDS.  LDS
+// operations of a wave execute in order, so no wait is needed, but the
+// COMPILER must neither move LDS accesses across this point nor forward a
+// lane's own store to its later load (another lane may have overwritten the
+// word): wave_barrier alone has no memory effect in LLVM, so the
+// wavefront-scope fences (no instructions on gfx950) carry the ordering.
+#define WAVE_SYNC()                                              \
+    do {                                                         \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   \
+        __builtin_amdgcn_wave_barrier();                         \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
+    } while (0)
 
 // Address-space-typed pointers.  Every global (1) and LDS (3) access goes
 // through these so the compiler emits global_* / ds_* instructions: a
@@ -313,7 +342,7 @@ struct LinkArgs {
 };
 
 template <bool U16, bool TAG, bool ST, bool LINK = false>
-__device__ int32_t encode_block(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
+__device__ __forceinline__ int32_t encode_block(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
                                 l_u32* __restrict__ Traw, l_u8* __restrict__ S, l_u32* __restrict__ ringE,
                                 l_u8* __restrict__ outRing, uint64_t* acc, LinkArgs lk = LinkArgs{0, 0, 0, true}) {
     const uint32_t L = laneid();
@@ -1104,17 +1133,25 @@ __global__ void __launch_bounds__(64) k_encode_linked(const uint8_t* __restrict_
                                                       uint32_t blockSize, uint32_t nBlocks,
                                                       uint8_t* __restrict__ slots, const LinkPlan* __restrict__ plan,
                                                       uint32_t* __restrict__ table, int fresh,
-                                                      int32_t* __restrict__ csize) {
+                                                      int32_t* __restrict__ csize, const uint32_t* __restrict__ gate,
+                                                      const uint32_t* __restrict__ startp,
+                                                      const uint32_t* __restrict__ entry) {
+    if (gate && *gate == 0) return;   // the parallel rounds settled: nothing to redo
     ENCODE_LDS
     l_u32* Tl = (l_u32*)T;
     l_u8* Sl = (l_u8*)S;
     l_u8* Xl = (l_u8*)X;
     const uint32_t L = laneid();
-    if (!fresh) {
-        for (uint32_t i = L; i < 4096; i += 64) Tl[i] = table[i];
+    // after parallel rounds: resume at the first unsettled block, whose
+    // entry table is exact (its predecessors are)
+    const uint32_t b0 = startp ? *startp : 0u;
+    if (b0 >= nBlocks) return;
+    if (b0 > 0 || !fresh) {
+        const uint32_t* in = b0 > 0 ? entry + (uint64_t)b0 * 4096 : table;
+        for (uint32_t i = L; i < 4096; i += 64) Tl[i] = in[i];
         WAVE_SYNC();
     }
-    for (uint32_t b = 0; b < nBlocks; ++b) {
+    for (uint32_t b = b0; b < nBlocks; ++b) {
         const uint64_t off = (uint64_t)b * blockSize;
         const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
         const LinkPlan pl = plan[b];
@@ -1139,7 +1176,149 @@ hipError_t launch_encode_linked(const uint8_t* src, uint64_t srcSize, uint32_t b
                                 hipStream_t st) {
     if (nBlocks == 0) return hipSuccess;
     hipLaunchKernelGGL(k_encode_linked, dim3(1), dim3(64), 0, st, src, srcSize, blockSize, nBlocks, slots, plan, table,
-                       fresh ? 1 : 0, csize);
+                       fresh ? 1 : 0, csize, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                       (const uint32_t*)nullptr);
+    return hipGetLastError();
+}
+
+// Block-dependent encode in parallel: the only state one block hands the
+// next is the lz4 table (its entries within 64 KiB of the next block; the
+// history bytes are input).  Round 0 encodes every block at once, block b
+// from a guessed entry table (all stale; block 0 from the call's first
+// table, exact), and writes its exit table rebased to block b+1 (stale
+// entries -> 0, which behave exactly like any other stale entry).  After
+// round r, k_link_settle compares exit[b-1] with entry[b] for every block
+// whose predecessor was re-encoded in round r; a differing entry is
+// replaced and its block queued for round r+1 (flag[b] = r+1).  Once no
+// entry changes, every block started from its predecessor's true exit
+// table: by induction from block 0 the output is exactly the serial
+// stream's.  A parse forgets a wrong start within a few KiB, so chains of
+// wrong tables die out geometrically and rounds after the first re-encode
+// few blocks.  If kLinkRounds rounds do not settle, the serial kernel
+// finishes from the first unsettled block (its entry is exact).
+//   ctl words: changed[kLinkRounds + 1] | first[kLinkRounds + 1] |
+//              flag[nBlocks] | enc[nBlocks]
+__global__ void __launch_bounds__(64) k_encode_linked_round(const uint8_t* __restrict__ src, uint64_t srcSize,
+                                                            uint32_t blockSize, uint8_t* __restrict__ slots,
+                                                            const LinkPlan* __restrict__ plan,
+                                                            const uint32_t* __restrict__ first, int fresh,
+                                                            const uint32_t* __restrict__ entry,
+                                                            uint32_t* __restrict__ exitT, int32_t* __restrict__ csize,
+                                                            const uint32_t* __restrict__ gate,
+                                                            const uint32_t* __restrict__ flag,
+                                                            uint32_t* __restrict__ enc, uint32_t round) {
+    const uint32_t b = blockIdx.x;
+    if (*gate == 0 || flag[b] != round) return;   // settled / this block's entry did not change
+    ENCODE_LDS
+    l_u32* Tl = (l_u32*)T;
+    const uint32_t L = laneid();
+    const uint32_t* in = b == 0 ? first : entry + (uint64_t)b * 4096;
+    const bool fr = b == 0 && fresh;
+    if (!fr) {
+        for (uint32_t i = L; i < 4096; i += 64) Tl[i] = in[i];
+        WAVE_SYNC();
+    }
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
+    const LinkPlan pl = plan[b];
+    const LinkArgs lk{pl.lowIn, pl.lowDict, pl.candLow, fr};
+    const int32_t r = encode_block<false, false, false, true>(gptr(src) + off - kLinkO0, kLinkO0 + n,
+                                                              gptr(slots) + off, n - 1, Tl, (l_u8*)S, (l_u32*)X,
+                                                              (l_u8*)X + kRingE, nullptr, lk);
+    if (L == 0) {
+        csize[b] = r;
+        enc[b] = round;
+    }
+    WAVE_SYNC();
+    uint32_t* o = exitT + (uint64_t)b * 4096;
+    for (uint32_t i = L; i < 4096; i += 64) {
+        const uint32_t e = Tl[i];
+        o[i] = e > n ? e - n : 0u;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_link_settle(const uint32_t* __restrict__ exitT, uint32_t* __restrict__ entry,
+                                                     uint32_t nBlocks, const uint32_t* __restrict__ gate,
+                                                     const uint32_t* __restrict__ enc, uint32_t* __restrict__ flag,
+                                                     uint32_t* __restrict__ changedNext,
+                                                     uint32_t* __restrict__ firstNext, uint32_t round) {
+    const uint32_t b = blockIdx.x + 1;   // entry[b] <- exit[b-1]
+    if (b >= nBlocks || *gate == 0 || enc[b - 1] != round) return;   // exit[b-1] unchanged
+    const uint32_t* x = exitT + (uint64_t)(b - 1) * 4096;
+    uint32_t* e = entry + (uint64_t)b * 4096;
+    __shared__ uint32_t diff;
+    if (threadIdx.x == 0) diff = 0;
+    __syncthreads();
+    uint32_t d = 0;
+    for (uint32_t i = threadIdx.x; i < 4096; i += 256) {
+        const uint32_t v = x[i];
+        d |= (e[i] != v) ? 1u : 0u;
+        e[i] = v;
+    }
+    if (d) atomicOr(&diff, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0 && diff) {
+        flag[b] = round + 1;
+        atomicAdd(changedNext, 1u);
+        atomicMin(firstNext, b);
+    }
+}
+
+__global__ void k_link_final(const uint32_t* __restrict__ exitT, uint32_t nBlocks, const uint32_t* __restrict__ gate,
+                             uint32_t* __restrict__ table) {
+    if (*gate != 0) return;   // not settled: the serial kernel writes the table
+    const uint32_t* x = exitT + (uint64_t)(nBlocks - 1) * 4096;
+    for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) table[i] = x[i];
+}
+
+__global__ void k_link_init(uint32_t* __restrict__ ctl, uint32_t nBlocks) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t R = kLinkRounds + 1;
+    if (i < R) ctl[i] = i == 0 ? 1u : 0u;                  // changed: round 0 open
+    else if (i < 2 * R) ctl[i] = 0xFFFFFFFFu;             // first unsettled block
+    else if (i < 2 * R + nBlocks) ctl[i] = 0u;            // flag: every block in round 0
+}
+
+uint64_t link_round_bytes(uint64_t nBlocks) {
+    return nBlocks * 4096 * 4 * 2 + (2 * (uint64_t)(kLinkRounds + 1) + 2 * nBlocks) * 4;
+}
+
+// The whole block-dependent encode of one call, asynchronously: up to
+// kLinkRounds parallel rounds, each skipped on the device once one settled,
+// then the serial kernel from the first unsettled block, which runs only if
+// none settled (exact either way).  scratch: link_round_bytes(nBlocks).
+hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                                    uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh,
+                                    uint32_t* scratch, int32_t* csize, int rounds, hipStream_t st) {
+    if (nBlocks == 0) return hipSuccess;
+    if (rounds < 1 || rounds > kLinkRounds) rounds = kLinkRounds;
+    uint32_t* entry = scratch;
+    uint32_t* exitT = entry + (uint64_t)nBlocks * 4096;
+    uint32_t* ctl = exitT + (uint64_t)nBlocks * 4096;
+    uint32_t* changed = ctl;
+    uint32_t* firstU = ctl + kLinkRounds + 1;
+    uint32_t* flag = firstU + kLinkRounds + 1;
+    uint32_t* enc = flag + nBlocks;
+    // first guess: blocks 1.. start from an all-stale table
+    if (hipMemsetAsync(entry, 0, (uint64_t)nBlocks * 4096 * 4, st) != hipSuccess) return hipErrorUnknown;
+    const uint32_t nInit = 2 * (kLinkRounds + 1) + nBlocks;
+    hipLaunchKernelGGL(k_link_init, dim3((nInit + 255) / 256), dim3(256), 0, st, ctl, nBlocks);
+    for (int r = 0; r < rounds; ++r) {
+        hipLaunchKernelGGL(k_encode_linked_round, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, plan,
+                           (const uint32_t*)table, fresh ? 1 : 0, (const uint32_t*)entry, exitT, csize,
+                           (const uint32_t*)(changed + r), (const uint32_t*)flag, enc, (uint32_t)r);
+        if (nBlocks > 1)
+            hipLaunchKernelGGL(k_link_settle, dim3(nBlocks - 1), dim3(256), 0, st, (const uint32_t*)exitT, entry,
+                               nBlocks, (const uint32_t*)(changed + r), (const uint32_t*)enc, flag, changed + r + 1,
+                               firstU + r + 1, (uint32_t)r);
+    }
+    // a single block settles in round 0 (changed[1] stays 0)
+    hipLaunchKernelGGL(k_encode_linked, dim3(1), dim3(64), 0, st, src, srcSize, blockSize, nBlocks, slots, plan, table,
+                       fresh ? 1 : 0, csize, (const uint32_t*)(changed + rounds), (const uint32_t*)(firstU + rounds),
+                       (const uint32_t*)entry);
+    hipLaunchKernelGGL(k_link_final, dim3(1), dim3(256), 0, st, (const uint32_t*)exitT, nBlocks,
+                       (const uint32_t*)(changed + rounds), table);
+    link_stats("encode", changed, firstU, rounds, nBlocks, st);
     return hipGetLastError();
 }
 
@@ -1991,6 +2170,323 @@ hipError_t launch_decode_linked(const uint8_t* frame, const BlockRec* recs, uint
                                 int blockChecksum, int32_t* dsize, int32_t* status, hipStream_t st) {
     hipLaunchKernelGGL(k_decode_linked, dim3(1), dim3(64), 0, st, frame, recs, nBlocks, blockMax, out, outCap, slot,
                        hist, digest, blockChecksum, dsize, status);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Block-dependent decode in parallel rounds.  Block b's output depends on
+// the 64 KiB decoded before it; its SIZE and its errors do not (LZ4
+// withPrefix64k rules: offsets, lengths and bounds come from the token
+// stream alone).  So:
+//   round 0   every block decodes at once into its slot [64 KiB history |
+//             blockMax] (slot 0's history = the call's exact history, the
+//             others a guess); k_dlink_plan turns the sizes, checksums and
+//             outCap into output offsets and the first stopping block
+//             (nOk, code: the serial order of checks);
+//   gather    k_dlink_gather rebuilds every block's history from the
+//             current outputs (the 64 KiB before start[b] in hist0 ++
+//             outputs) and compares it with the one the block was decoded
+//             against; a block whose history changed is queued for the next
+//             round (flag[b] = r + 1);
+//   rounds    only queued blocks decode again.
+// A gather that changes nothing means every block decoded against the
+// history its predecessors really produce: by induction from block 0 (exact
+// history) the outputs are the serial decoder's.  Matches reach back at
+// most 64 KiB, so wrong bytes die out within a few rounds on real data; if
+// kLinkRounds do not settle, one wave finishes serially from the first
+// unsettled block (k_dlink_serial).  k_dlink_compact then writes the
+// outputs back to back and k_dlink_hist_out the history after the call.
+//   ctl words: changed[R + 1] | first[R + 1] | flag[nBlocks] | nOk, code, pad, pad
+//   then start[nBlocks] (u64, 8-byte aligned)
+constexpr int64_t kDHist = 65536;
+__host__ __device__ __forceinline__ uint64_t dlink_stride(uint32_t blockMax) {
+    return (uint64_t)kDHist + (((uint64_t)blockMax + 15) & ~15ull);
+}
+
+__device__ __forceinline__ int32_t dlink_decode(const uint8_t* frame, const BlockRec& r, uint32_t blockMax,
+                                                g_u8* out, l_u8* ring, l_u8* win) {
+    const int64_t len = r.bits & 0x7FFFFFFFu;
+    if (r.bits & 0x80000000u) {
+        if (len > (int64_t)blockMax) return kDecodeOutputTooSmall;
+        copy_raw(gptr(frame) + r.offset, out, len);
+        return (int32_t)len;
+    }
+    Dec<false> D;
+    D.acc = nullptr;
+    D.ts = 0;
+    D.src = gptr(frame) + r.offset;
+    D.len = len;
+    D.dst = out;
+    D.physcap = blockMax;
+    D.ring = ring;
+    D.win = win;
+    D.wlo = INT64_MIN / 4;
+    D.labase = INT64_MIN / 4;
+    D.la = 0;
+    D.flushed = 0;
+    D.completed = 0;
+    D.lowP = -65536;
+    return decode_block(D, (int64_t)blockMax);
+}
+
+__global__ void __launch_bounds__(64) k_dlink_round(const uint8_t* __restrict__ frame,
+                                                    const BlockRec* __restrict__ recs, uint32_t blockMax,
+                                                    uint8_t* __restrict__ slots, int32_t* __restrict__ dsize,
+                                                    const uint32_t* __restrict__ gate,
+                                                    const uint32_t* __restrict__ flag, const uint32_t* __restrict__ nOk,
+                                                    uint32_t round) {
+    const uint32_t b = blockIdx.x;
+    if (*gate == 0 || flag[b] != round || (round > 0 && b >= *nOk)) return;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kWinAlloc];
+    const BlockRec r = recs[b];
+    const int32_t res = dlink_decode(frame, r, blockMax, gptr(slots) + b * dlink_stride(blockMax) + kDHist,
+                                     (l_u8*)ring, (l_u8*)win);
+    if (round == 0 && laneid() == 0) dsize[b] = res;
+}
+
+// The serial order of the per-block checks (k_decode_linked): checksum,
+// decode, output room.  One workgroup; start[] = exclusive scan of the
+// sizes up to the first stopping block.
+__global__ void __launch_bounds__(1024) k_dlink_plan(const BlockRec* __restrict__ recs,
+                                                     const uint32_t* __restrict__ digest, int bck,
+                                                     const int32_t* __restrict__ dsize, uint32_t nBlocks,
+                                                     uint64_t outCap, uint64_t* __restrict__ start,
+                                                     uint32_t* __restrict__ misc, int32_t* __restrict__ status) {
+    __shared__ uint64_t sc[1024];
+    __shared__ uint32_t stopAt;
+    const uint32_t t = threadIdx.x;
+    uint64_t carry = 0;
+    uint32_t nOk = nBlocks;
+    int32_t code = 0;
+    for (uint32_t c = 0; c < nBlocks; c += 1024) {
+        const uint32_t b = c + t;
+        int32_t bad = 0;
+        uint64_t v = 0;
+        if (b < nBlocks) {
+            const BlockRec r = recs[b];
+            const int32_t d = dsize[b];
+            if (bck && digest[b] != r.checksum) bad = 16;
+            else if (d < 0) bad = 18;
+            else v = (uint64_t)d;
+        }
+        sc[t] = v;
+        if (t == 0) stopAt = 0xFFFFFFFFu;
+        __syncthreads();
+        for (uint32_t k = 1; k < 1024; k <<= 1) {   // inclusive scan
+            const uint64_t x = t >= k ? sc[t - k] : 0;
+            __syncthreads();
+            sc[t] += x;
+            __syncthreads();
+        }
+        const uint64_t st = carry + sc[t] - v;
+        if (b < nBlocks && !bad && st + v > outCap) bad = 1;
+        if (bad) atomicMin(&stopAt, b);
+        __syncthreads();
+        const uint32_t stop = stopAt;
+        if (b < nBlocks && b < stop) start[b] = st;
+        if (stop != 0xFFFFFFFFu) {
+            nOk = stop;
+            if (b == stop) misc[1] = (uint32_t)bad;   // the stopping block's code
+            break;
+        }
+        carry += sc[1023];
+        __syncthreads();
+    }
+    __syncthreads();
+    if (t == 0) {
+        misc[0] = nOk;
+        if (nOk == nBlocks) misc[1] = 0;
+    }
+    __syncthreads();
+    if (t == 0) {
+        status[0] = (int32_t)nOk;
+        status[1] = (int32_t)misc[1];
+    }
+    (void)code;
+}
+
+// history byte g (< start of the call: hist0) of the stream hist0 ++ outputs
+__device__ __forceinline__ uint8_t dlink_byte(int64_t g, uint32_t k, const uint64_t* start, const int32_t* dsize,
+                                              g_cu8* slots, uint64_t stride, g_cu8* hist0) {
+    (void)dsize;
+    return g < 0 ? hist0[kDHist + g] : slots[k * stride + kDHist + (uint64_t)(g - (int64_t)start[k])];
+}
+
+// Rebuilds block b's history (the kDHist bytes before start[b]) with
+// nThreads threads, comparing with (and overwriting) the slot's; returns
+// this thread's "differs".  Fast path: the whole history inside block b-1's
+// output at a 4-byte aligned offset.
+__device__ bool dlink_gather(uint32_t b, uint32_t t, uint32_t nThreads, const uint64_t* start, const int32_t* dsize,
+                             g_u8* slots, uint64_t stride, g_cu8* hist0) {
+    const int64_t hi = b ? (int64_t)start[b] : 0, lo = hi - kDHist;
+    g_u8* h = slots + b * stride;
+    bool diff = false;
+    if (b > 0 && (int64_t)start[b - 1] <= lo && (((uint64_t)(lo - (int64_t)start[b - 1])) & 3) == 0) {
+        g_cu8* src = slots + (b - 1) * stride + kDHist + (uint64_t)(lo - (int64_t)start[b - 1]);
+        for (uint32_t i = 4 * t; i < kDHist; i += 4 * nThreads) {
+            const uint32_t v = *(g_cu32*)(src + i);
+            g_u32* d = (g_u32*)(h + i);
+            if (*d != v) { *d = v; diff = true; }
+        }
+        return diff;
+    }
+    // general: walk back over the blocks that hold [lo, hi)
+    int64_t top = hi;
+    for (int64_t k = (int64_t)b - 1; top > lo; --k) {
+        const int64_t s0 = k >= 0 ? (int64_t)start[k] : INT64_MIN / 4;
+        const int64_t from = s0 > lo ? s0 : lo;
+        for (int64_t g = from + t; g < top; g += nThreads) {
+            const uint8_t v = k >= 0 ? slots[(uint64_t)k * stride + kDHist + (uint64_t)(g - s0)]
+                                     : hist0[kDHist + g];
+            g_u8* d = h + (g - lo);
+            if (*d != v) { *d = v; diff = true; }
+        }
+        top = from;
+        if (k < 0) break;
+    }
+    return diff;
+}
+
+__global__ void __launch_bounds__(256) k_dlink_gather(uint8_t* __restrict__ slots, uint64_t stride,
+                                                      const uint64_t* __restrict__ start,
+                                                      const int32_t* __restrict__ dsize, const uint8_t* __restrict__ hist0,
+                                                      const uint32_t* __restrict__ misc,
+                                                      const uint32_t* __restrict__ gate, uint32_t* __restrict__ flag,
+                                                      uint32_t* __restrict__ changedNext,
+                                                      uint32_t* __restrict__ firstNext, uint32_t round) {
+    const uint32_t b = blockIdx.x + 1;   // block 0's history is the call's: exact from the start
+    if (*gate == 0 || b >= misc[0]) return;
+    __shared__ uint32_t any;
+    if (threadIdx.x == 0) any = 0;
+    __syncthreads();
+    if (dlink_gather(b, threadIdx.x, 256, start, dsize, gptr(slots), stride, gptr(hist0))) atomicOr(&any, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0 && any) {
+        flag[b] = round + 1;
+        atomicAdd(changedNext, 1u);
+        atomicMin(firstNext, b);
+    }
+}
+
+// the rounds did not settle: one wave, in order, from the first unsettled block
+__global__ void __launch_bounds__(64) k_dlink_serial(const uint8_t* __restrict__ frame,
+                                                     const BlockRec* __restrict__ recs, uint32_t blockMax,
+                                                     uint8_t* __restrict__ slots, const uint64_t* __restrict__ start,
+                                                     const int32_t* __restrict__ dsize,
+                                                     const uint8_t* __restrict__ hist0,
+                                                     const uint32_t* __restrict__ misc,
+                                                     const uint32_t* __restrict__ gate,
+                                                     const uint32_t* __restrict__ firstp) {
+    if (*gate == 0) return;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kWinAlloc];
+    const uint64_t stride = dlink_stride(blockMax);
+    const uint32_t nOk = misc[0];
+    for (uint32_t b = *firstp; b < nOk; ++b) {
+        dlink_gather(b, laneid(), 64, start, dsize, gptr(slots), stride, gptr(hist0));
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the decode's far reads see the new history
+        WAVE_SYNC();
+        dlink_decode(frame, recs[b], blockMax, gptr(slots) + b * stride + kDHist, (l_u8*)ring, (l_u8*)win);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the next gather sees these bytes
+        WAVE_SYNC();
+    }
+}
+
+__global__ void __launch_bounds__(256) k_dlink_compact(const uint8_t* __restrict__ slots, uint64_t stride,
+                                                       const uint64_t* __restrict__ start,
+                                                       const int32_t* __restrict__ dsize,
+                                                       const uint32_t* __restrict__ misc, uint8_t* __restrict__ out) {
+    const uint32_t b = blockIdx.x;
+    if (b >= misc[0]) return;
+    g_cu8* src = gptr(slots) + b * stride + kDHist;
+    g_u8* dst = gptr(out) + start[b];
+    const int64_t n = dsize[b];
+    const uint32_t t = threadIdx.x;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        const int64_t n16 = n & ~int64_t(15);
+        for (int64_t i = 16 * (int64_t)t; i < n16; i += 16 * 256) *(g_u4*)(dst + i) = *(g_cu4*)(src + i);
+        for (int64_t i = n16 + t; i < n; i += 256) dst[i] = src[i];
+    } else {
+        for (int64_t i = t; i < n; i += 256) dst[i] = src[i];
+    }
+}
+
+// the history after the call: the last 64 KiB of hist0 ++ out[0, end)
+// (hist0 read from slot 0's copy: histOut may be the caller's hist0)
+__global__ void __launch_bounds__(1024) k_dlink_hist_out(const uint8_t* __restrict__ out,
+                                                         const uint8_t* __restrict__ slot0,
+                                                         const uint64_t* __restrict__ start,
+                                                         const int32_t* __restrict__ dsize,
+                                                         const uint32_t* __restrict__ misc,
+                                                         uint8_t* __restrict__ histOut) {
+    const uint32_t nOk = misc[0];
+    const int64_t end = nOk ? (int64_t)(start[nOk - 1] + (uint64_t)dsize[nOk - 1]) : 0;
+    for (int64_t i = threadIdx.x; i < kDHist; i += 1024) {
+        const int64_t g = end - kDHist + i;
+        histOut[i] = g < 0 ? slot0[kDHist + g] : out[g];
+    }
+}
+
+__global__ void k_dlink_init(uint32_t* __restrict__ ctl, uint32_t nBlocks) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t R = kLinkRounds + 1;
+    if (i < R) ctl[i] = i == 0 ? 1u : 0u;
+    else if (i < 2 * R) ctl[i] = 0xFFFFFFFFu;
+    else if (i < 2 * R + nBlocks + 4) ctl[i] = 0u;
+}
+
+uint64_t dlink_scratch_bytes(uint64_t nBlocks, uint32_t blockMax) {
+    const uint64_t ctl = ((2 * (uint64_t)(kLinkRounds + 1) + nBlocks + 4) * 4 + 15) & ~15ull;
+    return nBlocks * dlink_stride(blockMax) + ctl + nBlocks * 8;
+}
+
+hipError_t launch_decode_linked_par(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax,
+                                    uint8_t* out, uint64_t outCap, uint8_t* hist, const uint32_t* digest,
+                                    int blockChecksum, int32_t* dsize, int32_t* status, uint8_t* scratch, int rounds,
+                                    hipStream_t st) {
+    if (rounds < 1 || rounds > kLinkRounds) rounds = kLinkRounds;
+    if (nBlocks == 0) {   // nothing decoded: status {0, 0}, the history unchanged
+        return hipMemsetAsync(status, 0, 8, st);
+    }
+    const uint64_t stride = dlink_stride(blockMax);
+    uint8_t* slots = scratch;
+    uint32_t* ctl = reinterpret_cast<uint32_t*>(scratch + nBlocks * stride);
+    const uint32_t R = kLinkRounds + 1;
+    uint32_t* changed = ctl;
+    uint32_t* firstU = ctl + R;
+    uint32_t* flag = firstU + R;
+    uint32_t* misc = flag + nBlocks;
+    uint64_t* start = reinterpret_cast<uint64_t*>(
+        scratch + nBlocks * stride + (((2 * (uint64_t)R + nBlocks + 4) * 4 + 15) & ~15ull));
+    // slot 0's history: the call's (exact); the others start from a guess
+    if (hipMemcpyAsync(slots, hist, kDHist, hipMemcpyDeviceToDevice, st) != hipSuccess) return hipErrorUnknown;
+    const uint32_t nInit = 2 * R + nBlocks + 4;
+    hipLaunchKernelGGL(k_dlink_init, dim3((nInit + 255) / 256), dim3(256), 0, st, ctl, nBlocks);
+    hipLaunchKernelGGL(k_dlink_round, dim3(nBlocks), dim3(64), 0, st, frame, recs, blockMax, slots, dsize,
+                       (const uint32_t*)changed, (const uint32_t*)flag, (const uint32_t*)misc, 0u);
+    hipLaunchKernelGGL(k_dlink_plan, dim3(1), dim3(1024), 0, st, recs, digest, blockChecksum, (const int32_t*)dsize,
+                       nBlocks, outCap, start, misc, status);
+    for (int r = 0; r < rounds; ++r) {
+        if (r > 0)
+            hipLaunchKernelGGL(k_dlink_round, dim3(nBlocks), dim3(64), 0, st, frame, recs, blockMax, slots, dsize,
+                               (const uint32_t*)(changed + r), (const uint32_t*)flag, (const uint32_t*)misc,
+                               (uint32_t)r);
+        if (nBlocks > 1)
+            hipLaunchKernelGGL(k_dlink_gather, dim3(nBlocks - 1), dim3(256), 0, st, slots, stride,
+                               (const uint64_t*)start, (const int32_t*)dsize, (const uint8_t*)slots,
+                               (const uint32_t*)misc, (const uint32_t*)(changed + r), flag, changed + r + 1,
+                               firstU + r + 1, (uint32_t)r);
+    }
+    hipLaunchKernelGGL(k_dlink_serial, dim3(1), dim3(64), 0, st, frame, recs, blockMax, slots, (const uint64_t*)start,
+                       (const int32_t*)dsize, (const uint8_t*)slots, (const uint32_t*)misc,
+                       (const uint32_t*)(changed + rounds), (const uint32_t*)(firstU + rounds));
+    hipLaunchKernelGGL(k_dlink_compact, dim3(nBlocks), dim3(256), 0, st, (const uint8_t*)slots, stride,
+                       (const uint64_t*)start, (const int32_t*)dsize, (const uint32_t*)misc, out);
+    hipLaunchKernelGGL(k_dlink_hist_out, dim3(1), dim3(1024), 0, st, (const uint8_t*)out, (const uint8_t*)slots,
+                       (const uint64_t*)start, (const int32_t*)dsize, (const uint32_t*)misc, hist);
+    link_stats("decode", changed, firstU, rounds, nBlocks, st);
     return hipGetLastError();
 }
 

@@ -59,6 +59,28 @@ def test_bd_golden_frames_device(golden):
         assert r == 0 and host(out) == data, f["name"]
 
 
+@pytest.mark.parametrize("rounds", ["1", "2", "serial"])
+def test_bd_rounds_and_serial_finish(golden, monkeypatch, rounds):
+    """The parallel rounds capped at 1 or 2 leave blocks unsettled: the serial
+    kernel finishes from the first unsettled block (its entry table exact);
+    "serial" runs the one-wave kernel alone.  Same bytes as the reference."""
+    if rounds == "serial":
+        monkeypatch.setenv("LZ4MT_AMD_BD_SERIAL", "1")
+    else:
+        monkeypatch.setenv("LZ4MT_AMD_BD_ROUNDS", rounds)
+    for f in golden["bd_frames"]:
+        data = bd_input(f["bytes"], f["seed"])
+        assert host(L.compress_frame(dev(data), _sd(f))) == read_golden(f["file"]), (f["name"], rounds)
+        out, r = L.decompress_frame(dev(read_golden(f["file"])))
+        assert r == 0 and host(out) == data, (f["name"], rounds)
+    for f in golden["bd_known"]:
+        if f["bytes"] > (64 << 20):
+            continue
+        data = bd_input(f["bytes"], f["seed"])
+        frame = L.compress_frame(dev(data), _sd(f))
+        assert (frame.numel(), L.xxh32(frame)) == (f["size"], f["xxh32"]), (f["name"], rounds)
+
+
 def test_bd_known_answers_device(golden):
     for f in golden["bd_known"]:
         data = bd_input(f["bytes"], f["seed"])
@@ -123,3 +145,27 @@ def test_bd_damaged_frames_vs_oracle(golden, api):
             r, got, _ = L.decompress(bytes(b), cap, mode=L.MODE_DEVICE if api == "DEVICE" else L.MODE_PARALLEL)
         assert r == rw, (it, kind, L.result_to_string(r), L.result_to_string(rw))
         assert got == ow, (it, kind, len(got), len(ow))
+
+
+@pytest.mark.parametrize("period", [60000, 65535, 200_000])
+def test_bd_long_chains(monkeypatch, period):
+    """Input repeating with a period near the 64 KiB window: every block's
+    bytes come from the previous block's, so a wrong history propagates
+    block after block and the decoder's rounds cannot settle before the
+    serial finish takes over (60000 / 65535 with 64 KiB blocks).  The
+    parallel encode and decode must give the serial kernels' bytes, and the
+    oracle must decode the frame to the input."""
+    rnd = __import__("random").Random(period)
+    unit = bytes(rnd.randrange(256) for _ in range(period))
+    data = (unit * (3_000_000 // period + 1))[:3_000_000]
+    for bid in (4, 5):
+        sd = L.make_sd(bid, True, True, block_dependence=True)
+        fr = host(L.compress_frame(dev(data), sd))
+        monkeypatch.setenv("LZ4MT_AMD_BD_SERIAL", "1")
+        assert host(L.compress_frame(dev(data), sd)) == fr, (period, bid)
+        o_ser, r_ser = L.decompress_frame(dev(fr))
+        monkeypatch.delenv("LZ4MT_AMD_BD_SERIAL")
+        out, r = L.decompress_frame(dev(fr))
+        assert r == 0 and r_ser == 0 and host(out) == data and host(o_ser) == data, (period, bid)
+        rw, ow = oracle.decompress_frame(fr, len(data) + (1 << 20))
+        assert rw == 0 and ow == data
