@@ -145,12 +145,6 @@ bool regular(FILE* fp) {
     struct stat st;
     return fstat(fileno(fp), &st) == 0 && S_ISREG(st.st_mode);
 }
-// positional writes only where they land where fwrite would: not on
-// O_APPEND descriptors (Linux appends every pwrite there, in any order)
-bool positional_out(FILE* fp) {
-    const int fl = fcntl(fileno(fp), F_GETFL);
-    return fl != -1 && !(fl & O_APPEND) && regular(fp);
-}
 
 FILE* in_fp(const Lz4MtContext* c) { return static_cast<FILE*>(c->readCtx); }
 FILE* out_fp(const Lz4MtContext* c) { return static_cast<FILE*>(c->writeCtx); }
@@ -224,14 +218,11 @@ extern "C" int lz4mtIoWrite(const Lz4MtContext* ctx, const void* src, int srcSiz
     if (is_null_sink(ctx)) return srcSize;
     FILE* fp = out_fp(ctx);
     if (!fp) return 0;
-    if (srcSize >= (int)kParMin && positional_out(fp) && fflush(fp) == 0) {   // parallel pwrite at the position
-        const off_t off = ftello(fp);
-        if (off >= 0) {
-            const size_t put = par_pio(fileno(fp), const_cast<void*>(src), (size_t)srcSize, off, true);
-            fseeko(fp, off + (off_t)put, SEEK_SET);
-            return (int)put;
-        }
-    }
+    // One fwrite (glibc hands a large buffer to write(2) directly).  Buffered
+    // writes into one file serialise on its inode lock, so splitting them
+    // over the copy pool only adds contention: 8 GiB into tmpfs, 6.0 GiB/s
+    // from one thread vs 4.9-5.2 from 8 pwrite threads (tools/e2e.py --file,
+    // profiles/r02_e2e_file.txt).  Reads stay parallel (no such lock).
     return (int)fwrite(src, 1, (size_t)srcSize, fp);
 }
 

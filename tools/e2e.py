@@ -56,6 +56,33 @@ def run_file(fn, path_in, path_out, sd, mode):
 if fdir:
     pin, pfr, pout = (os.path.join(fdir, f"e2e_{k}") for k in ("in.bin", "frame.lz4", "out.bin"))
     src.tofile(pin)
+    # the file path's floor: writing n bytes into a fresh file of this
+    # filesystem from host memory, one thread (fwrite-like) and 8 threads
+    # (pwrite at disjoint offsets), and reading it back
+    import concurrent.futures as cf
+    pw = os.path.join(fdir, "e2e_wr.bin")
+    for rep in range(2):
+        if os.path.exists(pw):
+            os.remove(pw)
+        t = time.perf_counter()
+        src.tofile(pw)
+        w1 = n / (time.perf_counter() - t) / 2**30
+        os.remove(pw)
+        fd = os.open(pw, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+        mv = memoryview(src).cast("B")
+        step = -(-n // 8)
+        t = time.perf_counter()
+        with cf.ThreadPoolExecutor(8) as ex:
+            list(ex.map(lambda i: os.pwrite(fd, mv[i * step:min(n, (i + 1) * step)], i * step), range(8)))
+        w8 = n / (time.perf_counter() - t) / 2**30
+        os.close(fd)
+        t = time.perf_counter()
+        back = np.fromfile(pw, dtype=np.uint8)
+        r1 = n / (time.perf_counter() - t) / 2**30
+        del back
+        print(f"floor {gib:g} GiB into {fdir}: write 1 thread {w1:.2f} GiB/s, 8 threads {w8:.2f} GiB/s, "
+              f"read back {r1:.2f} GiB/s", flush=True)
+    os.remove(pw)
 for label, sck in (("-Sx -BX", False), ("default flags (serial stream XXH32 on the host)", True)):
     sd = L.make_sd(bid, stream_checksum=sck, block_checksum=not sck)
     sdo = L.init_stream_descriptor()
