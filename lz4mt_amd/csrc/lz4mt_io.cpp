@@ -7,6 +7,7 @@
 // held to one core's memcpy/page-cache rate (~6.5 GB/s into pinned memory).
 // The callbacks keep the reference's contract: they are still called from
 // one thread at a time per stream and return only when the bytes are there.
+#include <cerrno>
 #include <fcntl.h>
 #include <stdio.h>
 #include <string.h>
@@ -128,6 +129,7 @@ size_t par_pio(int fd, void* buf, size_t n, off_t off, bool wr) {
         while (d < len) {
             char* p = static_cast<char*>(buf) + o + d;
             const ssize_t r = wr ? pwrite(fd, p, len - d, off + (off_t)(o + d)) : pread(fd, p, len - d, off + (off_t)(o + d));
+            if (r < 0 && errno == EINTR) continue;   // interrupted, not the end of the file
             if (r <= 0) break;
             d += (size_t)r;
         }

@@ -64,6 +64,31 @@ def checksum_of_checksums(t, chunk=16 << 20):
     return xxhash.xxh32(d).intdigest()
 
 
+def bd_data(f):
+    """The input of a -BD golden entry: its "kind" (default "bd" =
+    bd_input) at f["bytes"] / f["seed"]; "zeros", "random" (every block
+    raw) and "mixed" (random, zero and bd_input pieces) cover the edge
+    cases (tests/golden/make_golden.py)."""
+    import random
+
+    from oracle import gen_random
+    n, seed, kind = f["bytes"], f["seed"], f.get("kind", "bd")
+    if kind == "zeros":
+        return bytes(n)
+    if kind == "random":
+        return gen_random(n, seed)
+    if kind == "mixed":
+        rnd = random.Random(seed)
+        out = bytearray()
+        while len(out) < n:
+            k = rnd.randrange(3)
+            m = rnd.randrange(1, 120_000)
+            out += gen_random(m, rnd.randrange(1 << 30)) if k == 0 else bytes(m) if k == 1 else \
+                bd_input(m, rnd.randrange(1 << 30))
+        return bytes(out[:n])
+    return bd_input(n, seed)
+
+
 def bd_input(n, seed):
     """Block-dependent (-BD) test input with matches across block
     boundaries: App. F text with pieces re-copied from up to 64 KiB back

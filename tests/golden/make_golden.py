@@ -27,7 +27,7 @@ import xxhash
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 sys.path.insert(0, os.path.dirname(HERE))
-from conftest import bd_input  # noqa: E402  (the -BD test input, shared with the GPU tests)
+from conftest import bd_data, bd_input  # noqa: E402  (the -BD test input, shared with the GPU tests)
 LZ4 = ctypes.CDLL("/lib/x86_64-linux-gnu/liblz4.so.1")
 CLI = "/opt/conda/bin/lz4"
 
@@ -178,9 +178,16 @@ def bd_decode_reference(frame):
             dptr = dbase + 65536
 
 
-BD_CASES = [  # (name, bytes, seed, block id, stream checksum, block checksum)
+BD_CASES = [  # (name, bytes, seed, block id, stream checksum, block checksum[, input kind])
     ("bd_b4_sX", 1_500_000, 11, 4, False, True), ("bd_b4_SX", 1_500_000, 11, 4, True, True),
     ("bd_b5_Sx", 1_500_000, 12, 5, True, False),
+    # edges: empty, shorter than a match, exactly one block and one byte more,
+    # a short last block, all-zero, incompressible (every block raw), mixed
+    ("bd_e0", 0, 31, 4, True, True), ("bd_e1", 1, 32, 4, False, True), ("bd_e13", 13, 33, 5, True, False),
+    ("bd_e64k", 65536, 34, 4, False, True), ("bd_e64k1", 65537, 35, 4, True, True),
+    ("bd_e3b", 3 * 65536 + 5, 36, 4, False, False), ("bd_zero", 400_000, 37, 4, False, True, "zeros"),
+    ("bd_rand", 300_000, 38, 4, True, True, "random"), ("bd_mix4", 1_300_000, 39, 4, False, True, "mixed"),
+    ("bd_mix5", 1_300_000, 40, 5, True, True, "mixed"),
 ]
 BD_KNOWN = [  # larger -BD frames pinned by size + XXH32 only: (name, bytes, seed, id, sck, bck, writer)
     ("bd_b4_9m", 9_437_184 + 4321, 21, 4, False, True, "reference"),
@@ -192,14 +199,16 @@ BD_KNOWN = [  # larger -BD frames pinned by size + XXH32 only: (name, bytes, see
 
 def bd_main(manifest):
     manifest["bd_frames"], manifest["bd_known"] = [], []
-    for name, n, seed, bid, sck, bck in BD_CASES:
-        data = bd_input(n, seed)
+    for name, n, seed, bid, sck, bck, *kind in BD_CASES:
+        entry = {"name": name, "bytes": n, "seed": seed, "bid": bid, "stream_checksum": sck, "block_checksum": bck}
+        if kind:
+            entry["kind"] = kind[0]
+        data = bd_data(entry)
         f = bd_frame_reference(data, bid, sck, bck)
         assert bd_decode_reference(f) == data, name
         open(os.path.join(HERE, "frames", f"{name}.lz4"), "wb").write(f)
-        manifest["bd_frames"].append({"name": name, "bytes": n, "seed": seed, "bid": bid, "stream_checksum": sck,
-                                      "block_checksum": bck, "file": f"frames/{name}.lz4", "size": len(f),
-                                      "xxh32": xxh(f), "content_xxh32": xxh(data)})
+        entry.update({"file": f"frames/{name}.lz4", "size": len(f), "xxh32": xxh(f), "content_xxh32": xxh(data)})
+        manifest["bd_frames"].append(entry)
     for name, n, seed, bid, sck, bck, writer in BD_KNOWN:
         data = bd_input(n, seed)
         f = (bd_frame_reference if writer == "reference" else bd_frame_contiguous)(data, bid, sck, bck)

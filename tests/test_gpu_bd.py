@@ -17,7 +17,7 @@ import torch
 import xxhash
 
 import oracle
-from conftest import bd_input, read_golden
+from conftest import bd_data, bd_input, read_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -51,7 +51,7 @@ def _sd(f):
 
 def test_bd_golden_frames_device(golden):
     for f in golden["bd_frames"]:
-        data = bd_input(f["bytes"], f["seed"])
+        data = bd_data(f)
         frame = read_golden(f["file"])
         got = host(L.compress_frame(dev(data), _sd(f)))
         assert got == frame, f["name"]
@@ -69,21 +69,21 @@ def test_bd_rounds_and_serial_finish(golden, monkeypatch, rounds):
     else:
         monkeypatch.setenv("LZ4MT_AMD_BD_ROUNDS", rounds)
     for f in golden["bd_frames"]:
-        data = bd_input(f["bytes"], f["seed"])
+        data = bd_data(f)
         assert host(L.compress_frame(dev(data), _sd(f))) == read_golden(f["file"]), (f["name"], rounds)
         out, r = L.decompress_frame(dev(read_golden(f["file"])))
         assert r == 0 and host(out) == data, (f["name"], rounds)
     for f in golden["bd_known"]:
         if f["bytes"] > (64 << 20):
             continue
-        data = bd_input(f["bytes"], f["seed"])
+        data = bd_data(f)
         frame = L.compress_frame(dev(data), _sd(f))
         assert (frame.numel(), L.xxh32(frame)) == (f["size"], f["xxh32"]), (f["name"], rounds)
 
 
 def test_bd_known_answers_device(golden):
     for f in golden["bd_known"]:
-        data = bd_input(f["bytes"], f["seed"])
+        data = bd_data(f)
         assert xxhash.xxh32(data).intdigest() == f["content_xxh32"]
         frame = L.compress_frame(dev(data), _sd(f))
         assert (frame.numel(), L.xxh32(frame)) == (f["size"], f["xxh32"]), f["name"]
@@ -103,7 +103,7 @@ def test_bd_callback_api(golden, monkeypatch, mode, batches):
         monkeypatch.setenv("LZ4MT_AMD_BATCH_MIB", "1")
     m = {"DEVICE": L.MODE_DEVICE, "PARALLEL": L.MODE_PARALLEL, "SEQUENTIAL": L.MODE_SEQUENTIAL}[mode]
     for f in golden["bd_frames"] + [k for k in golden["bd_known"] if k["bid"] >= 6]:
-        data = bd_input(f["bytes"], f["seed"])
+        data = bd_data(f)
         r, frame = L.compress(data, _sd(f), mode=m)
         assert r == 0, (f["name"], L.result_to_string(r))
         if "file" in f:
@@ -123,7 +123,7 @@ def test_bd_damaged_frames_vs_oracle(golden, api):
     import random
     rnd = random.Random({"device": 1, "DEVICE": 2, "PARALLEL": 3}[api])
     f = golden["bd_frames"][0]   # 64 KiB blocks, block checksums
-    data = bd_input(f["bytes"], f["seed"])
+    data = bd_data(f)
     frame = read_golden(f["file"])
     cap = len(data) + (1 << 20)
     for it in range(40):
