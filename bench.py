@@ -108,11 +108,17 @@ def usable_cores():
     return max(1, n), hw
 
 
-def cpu_baseline(mib, block_id, sck):
-    """lz4mt-shaped CPU pipeline (one task per block, nPool = threads + 1,
-    in-order writer, block/stream XXH32) over liblz4 (the codec lz4mt links)
-    when the box has it, else over the oracle's restatement.  Rank 0, N = 1,
-    bounded sample; best of 3 at full width, one pass single-threaded."""
+def cpu_baseline(mib, block_id, sck, level=0, bd=False):
+    """The reference's CPU path for this run's codec, timed on the host.
+
+    Independent blocks: the lz4mt-shaped pipeline (one task per block, nPool =
+    threads + 1, in-order writer, block/stream XXH32) over the codec lz4mt
+    links -- liblz4's LZ4_compress_limitedOutput, or for level >= 3
+    LZ4_compressHC2_limitedOutput at that level (src/main.cpp:749-785) --
+    when the box has liblz4, else over the oracle's restatements; best of 3
+    at full width, one pass single-threaded.  -BD: single-threaded, as
+    compressBlockDependency is (src/lz4mt.cpp:460-538, 737-845), one LZ4
+    stream over liblz4 (orc_bd_roundtrip).  Rank 0, N = 1, bounded sample."""
     import oracle
     threads, hw = usable_cores()
     n = mib << 20
@@ -120,26 +126,40 @@ def cpu_baseline(mib, block_id, sck):
     oracle.lib.orc_gen_synthetic(buf, n, 42)
     p = oracle.params(block_id, stream_checksum=sck, block_checksum=not sck)
     lz = oracle.liblz4_codec()
-    codec, codec_name = (lz[0], f"liblz4 {lz[1]}") if lz else (None, "oracle restatement")
-    n1 = min(n, 256 << 20)
+    flags = ("default flags" if sck else "-Sx -BX") + (f" level {level}" if level >= 3 else "") + (" -BD" if bd else "")
+    line = {"unit": "GiB/s", "kind": "port", "hardware_concurrency": hw, "cpu_model": _cpu_model()}
+    if bd:
+        if not lz:
+            return None   # the stream API comes from liblz4 only
+        tc, td, _ = oracle.bd_roundtrip(buf, n, block_id, sck, not sck, lz[2])
+        line.update({"value": round(n / GiB / (tc + td), 3), "cores": 1, "codec": f"liblz4 {lz[1]}",
+                     "sample": f"{mib} MiB App.F synthetic, B{block_id} {flags}: one LZ4 stream "
+                               f"(LZ4_compress_fast_continue, cap n-1; LZ4_decompress_safe_usingDict), block/stream "
+                               f"XXH32, single thread as the reference's -BD path",
+                     "compress_GiBps": round(n / GiB / tc, 3), "decompress_GiBps": round(n / GiB / td, 3)})
+        return line
+    if level >= 3:
+        codec = oracle.hc_codec(level, lz[2] if lz else None)
+        codec_name = f"liblz4 {lz[1]} HC" if lz else "oracle HC restatement"
+    else:
+        codec, codec_name = (lz[0], f"liblz4 {lz[1]}") if lz else (None, "oracle restatement")
+    n1 = min(n, 256 << 20 if level < 3 else 64 << 20)
     tc1, td1, _ = oracle.pipeline_roundtrip(buf, n1, p, 1, codec)
     best = None
-    for _ in range(3):
+    for _ in range(3 if level < 3 else 1):
         tc, td, _ = oracle.pipeline_roundtrip(buf, n, p, threads, codec)
         if best is None or tc + td < best[0] + best[1]:
             best = (tc, td)
     tcN, tdN = best
-    return {
-        "value": round(n / GiB / (tcN + tdN), 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-        "codec": codec_name,
-        "sample": f"{mib} MiB App.F synthetic, B{block_id} {'default flags' if sck else '-Sx -BX'}, compress+decompress "
+    line.update({
+        "value": round(n / GiB / (tcN + tdN), 3), "cores": threads, "codec": codec_name,
+        "sample": f"{mib} MiB App.F synthetic, B{block_id} {flags}, compress+decompress "
                   f"through an lz4mt-shaped pipeline (nPool=threads+1, in-order writer, checksums) over {codec_name}; "
-                  f"best of 3; single thread on {n1 >> 20} MiB",
+                  f"best of {3 if level < 3 else 1}; single thread on {n1 >> 20} MiB",
         "compress_GiBps": round(n / GiB / tcN, 3), "decompress_GiBps": round(n / GiB / tdN, 3),
         "single_thread_compress_GiBps": round(n1 / GiB / tc1, 3),
-        "single_thread_decompress_GiBps": round(n1 / GiB / td1, 3),
-        "hardware_concurrency": hw, "cpu_model": _cpu_model(),
-    }
+        "single_thread_decompress_GiBps": round(n1 / GiB / td1, 3)})
+    return line
 
 
 def pmc_traffic(kernel, n, bm, flg):
@@ -323,7 +343,8 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
-            cpu = cpu_baseline(a.cpu_mib, a.block_id, sck)
+            cpu = cpu_baseline(a.cpu_mib if a.level < 3 and not a.block_dependent else min(a.cpu_mib, 256),
+                               a.block_id, sck, a.level, a.block_dependent)
         flags = ("default flags (FLG.2 content checksum)" if sck else "-Sx -BX") + \
             (" -BD" if a.block_dependent else "") + (f" level {a.level} (LZ4-HC)" if a.level >= 3 else "")
         line = {

@@ -20,6 +20,7 @@
 
 #include "../../include/lz4mt_hip.h"
 #include "lz4mt_device.h"
+#include <chrono>
 #include "lz4mt_host.h"
 
 using namespace lz4mt;
@@ -239,14 +240,28 @@ public:
             return hipMemcpyAsync(pin_[i & 1], d + o, k, hipMemcpyDeviceToHost, cp_) == hipSuccess &&
                    hipEventRecord(ev_[i & 1], cp_) == hipSuccess;
         };
+        const char* st = getenv("LZ4MT_AMD_HASH_STATS");   // 1: wait / hash split to stderr
+        const bool stats = st && st[0] == '1';
+        double tWait = 0, tHash = 0;
+        auto now = [] { return std::chrono::steady_clock::now(); };
+        const auto t0 = now();
         if (nc && !issue(0)) return false;
         for (uint64_t i = 0; i < nc; ++i) {
             if (i + 1 < nc && !issue(i + 1)) return false;   // its buffer held chunk i-1, hashed already
+            const auto a = now();
             if (hipEventSynchronize(ev_[i & 1]) != hipSuccess) return false;
+            const auto b = now();
             const uint64_t o = i * kChunk;
             x.update(pin_[i & 1], std::min(kChunk, len - o));
+            if (stats) {
+                tWait += std::chrono::duration<double>(b - a).count();
+                tHash += std::chrono::duration<double>(now() - b).count();
+            }
         }
         *out = x.digest();
+        if (stats)
+            fprintf(stderr, "[lz4mt host hash] %.3f GB in %.1f ms: waiting for copies %.1f ms, hashing %.1f ms\n",
+                    len / 1e9, std::chrono::duration<double>(now() - t0).count() * 1e3, tWait * 1e3, tHash * 1e3);
         return true;
     }
     hipStream_t stream() const { return cp_; }

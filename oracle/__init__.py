@@ -50,6 +50,10 @@ def _load():
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz)]
     lib.orc_pipeline_roundtrip_codec.argtypes = [u8p, sz, ctypes.POINTER(FrameParams), ctypes.c_int,
                                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz), u8p, u8p]
+    lib.orc_hc_codec_set.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.orc_bd_roundtrip.argtypes = [u8p, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz)]
     lib.orc_stream_known_answer.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(FrameParams),
                                             ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(KnownAnswer)]
     return lib
@@ -160,6 +164,36 @@ def liblz4_codec(path="liblz4.so.1"):
     cf = ctypes.cast(lz.LZ4_compress_limitedOutput, ctypes.c_void_p).value
     df = ctypes.cast(lz.LZ4_decompress_safe, ctypes.c_void_p).value
     return (cf, df), f"{v // 10000}.{v // 100 % 100}.{v % 100}", lz
+
+
+def hc_codec(level, lz=None):
+    """(compress, decompress) pointers for the pipeline with lz4mt's level >= 3
+    codec, LZ4_compressHC2_limitedOutput(src, dst, n, cap, level)
+    (src/main.cpp:778-785), from liblz4 ``lz`` (a ctypes CDLL) or, when None,
+    this restatement (orc_lz4hc_compress); decompression is the fast
+    codec's (the same LZ4 block format)."""
+    fn = None
+    if lz is not None:
+        fn = ctypes.cast(getattr(lz, "LZ4_compressHC2_limitedOutput", None) or lz.LZ4_compress_HC,
+                         ctypes.c_void_p).value
+    lib.orc_hc_codec_set(fn, level)
+    tramp = ctypes.cast(lib.orc_hc_compress_tramp, ctypes.c_void_p).value
+    dec = ctypes.cast(lz.LZ4_decompress_safe, ctypes.c_void_p).value if lz is not None else None
+    return tramp, dec
+
+
+def bd_roundtrip(data_buf, n, block_max_id, stream_checksum, block_checksum, lz):
+    """Single-thread -BD round trip over liblz4's stream API (the reference's
+    compressBlockDependency / decompressBlockDependency shape):
+    (compress_s, decompress_s, frame_bytes)."""
+    ptr = [ctypes.cast(getattr(lz, f), ctypes.c_void_p).value for f in
+           ("LZ4_createStream", "LZ4_freeStream", "LZ4_compress_fast_continue", "LZ4_decompress_safe_usingDict")]
+    secs = (ctypes.c_double * 2)()
+    fs = ctypes.c_size_t(0)
+    if lib.orc_bd_roundtrip(data_buf, n, block_max_id, int(stream_checksum), int(block_checksum), *ptr, secs,
+                            ctypes.byref(fs)) != 0:
+        raise RuntimeError("-BD CPU round trip failed")
+    return secs[0], secs[1], fs.value
 
 
 def known_answer(n, p, seed=42, chunk=16 << 20, threads=8):

@@ -729,7 +729,7 @@ typedef struct {
     orc_codec_fn cfn, dfn;
     uint8_t** out; int* res; int* done; uint8_t** cin; int* clen; int* craw;
     size_t next, written; pthread_mutex_t mu; pthread_cond_t cv; size_t npool;
-    orc_xxh32_state sx; size_t frameBytes; int err;
+    orc_xxh32_state sx; size_t frameBytes; int err; int writing;
 } pipe_ctx;
 
 static void* pipe_worker(void* a) {
@@ -741,34 +741,43 @@ static void* pipe_worker(void* a) {
         size_t i = c->next++;
         pthread_mutex_unlock(&c->mu);
         const size_t off = i * c->bm, len = c->n - off < c->bm ? c->n - off : c->bm;
+        /* the worker: codec and block XXH32 (ref src/lz4mt.cpp:390-401 compress,
+         * 629-650 decompress: the checksum is verified before the decode) */
         if (!c->decode) {
             c->res[i] = c->cfn((const char*)c->src + off, (char*)c->out[i % c->npool], (int)len, (int)len);
+            const int cs = c->res[i];
+            if (c->p->blockChecksum)
+                (void)orc_xxh32(cs > 0 ? c->out[i % c->npool] : c->src + off, cs > 0 ? (size_t)cs : len, 0);
         } else {
+            if (c->p->blockChecksum) (void)orc_xxh32(c->cin[i], (size_t)c->clen[i], 0);
             if (c->craw[i]) { memcpy(c->out[i % c->npool], c->cin[i], (size_t)c->clen[i]); c->res[i] = c->clen[i]; }
             else c->res[i] = c->dfn((const char*)c->cin[i], (char*)c->out[i % c->npool], c->clen[i], (int)c->bm);
         }
-        /* in-order write chain */
+        /* in-order write chain: ONE writer at a time (the reference's
+         * futures[i-1].wait() chain), the stream XXH32 inside it */
         pthread_mutex_lock(&c->mu);
         c->done[i] = 1;
-        while (c->written < c->nb && c->done[c->written]) {
-            const size_t k = c->written;
-            const size_t ko = k * c->bm, klen = c->n - ko < c->bm ? c->n - ko : c->bm;
-            pthread_mutex_unlock(&c->mu);
-            if (!c->decode) {
-                const int cs = c->res[k];
-                const uint8_t* stored = cs > 0 ? c->out[k % c->npool] : c->src + ko;
-                const size_t slen = cs > 0 ? (size_t)cs : klen;
-                if (c->p->blockChecksum) (void)orc_xxh32(stored, slen, 0);
-                if (c->p->streamChecksum) orc_xxh32_update(&c->sx, c->src + ko, klen);
-                c->frameBytes += 4 + slen + (c->p->blockChecksum ? 4 : 0);
-            } else {
-                if (c->res[k] < 0) c->err = 1;
-                if (c->p->blockChecksum) (void)orc_xxh32(c->cin[k], (size_t)c->clen[k], 0);
-                if (c->p->streamChecksum && c->res[k] > 0) orc_xxh32_update(&c->sx, c->out[k % c->npool], (size_t)c->res[k]);
+        if (!c->writing) {
+            c->writing = 1;
+            while (c->written < c->nb && c->done[c->written]) {
+                const size_t k = c->written;
+                const size_t ko = k * c->bm, klen = c->n - ko < c->bm ? c->n - ko : c->bm;
+                pthread_mutex_unlock(&c->mu);
+                if (!c->decode) {
+                    const int cs = c->res[k];
+                    const size_t slen = cs > 0 ? (size_t)cs : klen;
+                    if (c->p->streamChecksum) orc_xxh32_update(&c->sx, c->src + ko, klen);
+                    c->frameBytes += 4 + slen + (c->p->blockChecksum ? 4 : 0);
+                } else {
+                    if (c->res[k] < 0) c->err = 1;
+                    if (c->p->streamChecksum && c->res[k] > 0)
+                        orc_xxh32_update(&c->sx, c->out[k % c->npool], (size_t)c->res[k]);
+                }
+                pthread_mutex_lock(&c->mu);
+                c->written++;
+                pthread_cond_broadcast(&c->cv);
             }
-            pthread_mutex_lock(&c->mu);
-            c->written++;
-            pthread_cond_broadcast(&c->cv);
+            c->writing = 0;
         }
         pthread_mutex_unlock(&c->mu);
     }
@@ -837,7 +846,7 @@ int orc_pipeline_roundtrip_codec(const uint8_t* src, size_t n, const orc_frame_p
     }
     free(tmp);
     memset(c.done, 0, (nb + 1) * sizeof(int));
-    c.next = 0; c.written = 0; c.decode = 1; c.err = 0;
+    c.next = 0; c.written = 0; c.decode = 1; c.err = 0; c.writing = 0;
     orc_xxh32_reset(&c.sx, 0);
     t0 = now_s();
     pipe_run(&c, nthreads);

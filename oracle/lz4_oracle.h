@@ -106,6 +106,14 @@ int orc_pipeline_roundtrip_codec(const uint8_t* src, size_t n,
                                  double* secs, size_t* frameSize,
                                  orc_codec_fn compress, orc_codec_fn decompress);
 
+/* cpu_baselines.c: the reference's CPU path for LZ4-HC (through the
+ * pipeline, via a trampoline fixing the level) and for -BD (single thread,
+ * one LZ4 stream), over liblz4 function pointers (bench.py cpu_baseline) */
+void orc_hc_codec_set(void* fn, int level);
+int orc_hc_compress_tramp(const char* src, char* dst, int n, int cap);
+int orc_bd_roundtrip(const uint8_t* src, size_t n, int blockMaxId, int sck, int bck, void* create, void* freefn,
+                     void* cont, void* decdict, double* secs, size_t* frameSize);
+
 /* ---- streamed known answers for large configs ------------------------- */
 typedef struct {
     uint64_t frameSize;
