@@ -854,7 +854,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         // the previous sequence's stores go out behind them.
         w = 64;
         bool dd = false, twDone = false, twRedo = false;
-        uint64_t gmask = 0, aliased = 0;
+        uint64_t gmask, aliased = 0;   // gmask: read only after dd set it
         // table writes for stop w: lanes past the stop put the old entry
         // back; on a collision (or when redone after a tag alias moved the
         // stop) the lanes up to the stop re-insert (last member of each group)
@@ -869,8 +869,8 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             }
             WAVE_SYNC();
         };
-        ip = 0; cd = 0; maxb = 0; cw = 0; iw = 0; bi = 0; bc = 0;
-        wTerm = false;
+        // ip .. bc and wTerm are set on the path that reads them (a stop
+        // inside the window): no per-window zeroing
         bool again = true;
         while (again) {
             w = sff1(sm);

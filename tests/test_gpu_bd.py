@@ -169,3 +169,20 @@ def test_bd_long_chains(monkeypatch, period):
         assert r == 0 and r_ser == 0 and host(out) == data and host(o_ser) == data, (period, bid)
         rw, ow = oracle.decompress_frame(fr, len(data) + (1 << 20))
         assert rw == 0 and ow == data
+
+
+@pytest.mark.parametrize("bid", [4, 5])
+def test_bd_parallel_equals_serial_64mib(monkeypatch, bid):
+    """64 MiB of App. F input (1024 / 256 blocks): the parallel rounds write
+    the one-wave serial kernel's frame, and both decoders give the input
+    back (size-independent check beside the 9 MiB known answers)."""
+    src = L.gen_synthetic(64 << 20, seed=77)
+    sd = L.make_sd(bid, False, True, block_dependence=True)
+    fr = L.compress_frame(src, sd)
+    monkeypatch.setenv("LZ4MT_AMD_BD_SERIAL", "1")
+    fr_ser = L.compress_frame(src, sd)
+    out_ser, r_ser = L.decompress_frame(fr)
+    monkeypatch.delenv("LZ4MT_AMD_BD_SERIAL")
+    assert fr.numel() == fr_ser.numel() and torch.equal(fr, fr_ser)
+    out, r = L.decompress_frame(fr)
+    assert r == 0 and r_ser == 0 and torch.equal(out, src) and torch.equal(out_ser, src)
