@@ -1,5 +1,5 @@
 set -euo pipefail
-out=gpurun_out/r02n
+out=gpurun_out/r02u
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 900 python3 -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread tests/ > $out/pytest.log 2>&1
