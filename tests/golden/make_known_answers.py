@@ -29,6 +29,8 @@ CASES = {
     "configs2_32gib_b7_SxBX": (32 * GiB, 7, False, True,
                                "BASELINE configs[2]: 32 GiB stream, frame and record offsets past 2^32"),
     "10gib_b6_SxBX": (10 * GiB, 6, False, True, "1 MiB blocks: parallel frame walk over a frame past 2^32"),
+    "8gib_b5_SxBX": (8 * GiB, 5, False, True, "sweep: 256 KiB blocks (32768) at the bench size"),
+    "8gib_b4_SxBX": (8 * GiB, 4, False, True, "sweep: 64 KiB blocks (131072, lz4's byU16 table, k_encode16)"),
 }
 
 
@@ -37,7 +39,12 @@ def main():
     pin = oracle.known_answer(256 << 20, oracle.params(7, False, True), chunk=CHUNK)
     assert (pin["frame_size"], pin["frame_xxh32"], pin["content_xxh32"]) == (133159392, 0x1686045A, 0xE6F24EBA)
     out = {"chunk": CHUNK, "seed": 42, "generator": "SURVEY.md App. F", "cases": {}}
+    only = [a for a in sys.argv[1:] if a in CASES]   # regenerate just these (merged into the file)
+    if only:
+        out = json.load(open(os.path.join(HERE, "known_answers.json")))
     for name, (n, bid, sck, bck, what) in CASES.items():
+        if only and name not in only:
+            continue
         ka = oracle.known_answer(n, oracle.params(bid, sck, bck), seed=42, chunk=CHUNK, threads=os.cpu_count() or 8)
         ka.update({"bytes": n, "block_id": bid, "stream_checksum": sck, "block_checksum": bck, "pins": what})
         out["cases"][name] = ka

@@ -49,7 +49,7 @@ def host(t):
 # large configs against the oracle's known answers
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("case", ["configs1_8gib_b7_SxBX", "8gib_b7_default", "configs2_32gib_b7_SxBX",
-                                  "10gib_b6_SxBX"])
+                                  "10gib_b6_SxBX", "8gib_b5_SxBX", "8gib_b4_SxBX"])
 def test_known_answers_large(known_answers, case):
     ka = known_answers["cases"][case]
     chunk = known_answers["chunk"]
