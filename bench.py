@@ -196,9 +196,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # LZ4MT_BENCH_BACKEND=gloo rehearses the N > 1 orchestration with several
+    # ranks sharing the GPUs there are (gloo moves CUDA tensors through the
+    # host); the measured multi-GPU path is RCCL, one rank per GPU
+    backend = os.environ.get("LZ4MT_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     stream = torch.cuda.current_stream()
 
@@ -274,7 +282,8 @@ def main():
         t1 = sync_all()
         tgr = time.perf_counter() - tl if world > 1 else 0.0
         if world > 1:
-            piece = D.scatter_frame(full if rank == 0 else None, full.numel() if rank == 0 else 0, src=0)
+            piece = D.scatter_frame(full if rank == 0 else None, full.numel() if rank == 0 else 0, src=0,
+                                    device=dev)
             torch.cuda.synchronize()
             t2 = sync_all()
         else:

@@ -211,12 +211,13 @@ def device_records(frame, frame_len=None):
     return hdr, starts
 
 
-def scatter_frame(frame, frame_len, src=0, group=None, records=None, async_op=False):
+def scatter_frame(frame, frame_len, src=0, group=None, records=None, async_op=False, device=None):
     """Cuts ONE -Sx frame held by ``src`` into per-rank sub-frames of whole
     records and delivers piece r to rank r (the decompress side of SURVEY.md
     §8(e): blocks are independent, src/lz4mt.cpp:914-918,991-995).
 
-    ``frame`` is the uint8 tensor on ``src`` (None elsewhere); ``records``
+    ``frame`` is the uint8 tensor on ``src`` (None elsewhere; ``device``: where
+    the other ranks receive, default CUDA under RCCL, CPU otherwise); ``records``
     maps (frame, frame_len) to (header length, record starts + EOS offset):
     default the device walk for device tensors, the host walk otherwise.
     Rank r receives blocks ``rank_blocks(nb, world, r)`` as a valid frame
@@ -245,8 +246,11 @@ def scatter_frame(frame, frame_len, src=0, group=None, records=None, async_op=Fa
             table[5 + 2 * r] = starts[first + count] - starts[first]
         table = table.to(dev)
     else:
-        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
-            else torch.device("cpu")
+        if device is not None:   # where this rank decodes (gloo can carry CUDA tensors too)
+            dev = torch.device(device)
+        else:
+            dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
+                else torch.device("cpu")
         table = torch.zeros(4 + 2 * world, dtype=torch.int64, device=dev)
     dist.broadcast(table, peer(src), group=group)
     t = table.cpu().tolist()
