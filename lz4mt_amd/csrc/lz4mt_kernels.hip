@@ -31,6 +31,12 @@
 
 namespace lz4mt {
 
+// LZ4MT_AMD_BD_COLD=1: -BD encode rounds start from all-stale tables (A/B of k_link_warm)
+[[maybe_unused]] static bool link_cold() {
+    const char* e = getenv("LZ4MT_AMD_BD_COLD");
+    return e && e[0] == '1';
+}
+
 // LZ4MT_AMD_BD_STATS=1: print the -BD rounds' work (blocks redone per
 // round, first unsettled block) to stderr -- synchronises the stream
 static void link_stats(const char* what, const uint32_t* changed, const uint32_t* firstU, int rounds,
@@ -1279,6 +1285,48 @@ __global__ void k_link_init(uint32_t* __restrict__ ctl, uint32_t nBlocks) {
     else if (i < 2 * R + nBlocks) ctl[i] = 0u;            // flag: every block in round 0
 }
 
+// The first guess of block b's entry table for 4 MiB blocks:
+// lz4's table after block b-1 holds only positions of b-1's last 64 KiB
+// (older ones are stale), and two greedy parses of the same bytes from
+// different tables end up making the same choices once their tables agree
+// on the window (see link_warm_bytes for how long that takes).  So the table after
+// parsing b-1's last W bytes from an empty table is, almost always, exactly
+// the table the stream has, and round 0 then rarely needs a second round.
+// The warm parse writes its (discarded) output into block b's own slot,
+// which round 0 overwrites.  A wrong guess costs a round, never a byte.
+__global__ void __launch_bounds__(64) k_link_warm(const uint8_t* __restrict__ src, uint32_t blockSize, uint32_t W,
+                                                  uint8_t* __restrict__ slots, uint32_t* __restrict__ entry) {
+    ENCODE_LDS
+    l_u32* Tl = (l_u32*)T;
+    const uint32_t L = laneid();
+    const uint32_t b = blockIdx.x + 1;
+    const uint64_t off = (uint64_t)b * blockSize;   // block b's start; the warm bytes end there
+    const LinkArgs lk{kLinkO0, kLinkO0, kLinkO0, true};   // no history: a fresh stream over the W bytes
+    (void)encode_block<false, false, false, true>(gptr(src) + off - W - kLinkO0, kLinkO0 + W, gptr(slots) + off,
+                                                  W + W / 255 + 16, Tl, (l_u8*)S, (l_u32*)X, (l_u8*)X + kRingE,
+                                                  nullptr, lk);
+    WAVE_SYNC();
+    uint32_t* o = entry + (uint64_t)b * 4096;
+    for (uint32_t i = L; i < 4096; i += 64) {
+        const uint32_t e = Tl[i];
+        o[i] = e > W ? e - W : 0u;
+    }
+}
+
+// bytes of the warm parse for a block size (0 = no warm start):
+// LZ4MT_AMD_BD_WARM_KIB overrides (A/B)
+static uint32_t link_warm_bytes(uint32_t blockSize) {
+    const char* e = getenv("LZ4MT_AMD_BD_WARM_KIB");
+    // measured on App. F (LZ4MT_AMD_BD_STATS=1, 1 GiB, tools/r02ab.sh): two
+    // parses agree only after ~0.5-1 MiB -- 4 MiB blocks with W = 256 / 512 /
+    // 1024 KiB leave 212 / 47 / 0 of 255 entries wrong; 1 MiB blocks cannot
+    // hold a long enough warm-up (512 KiB: 147 of 1023 wrong), so they start cold
+    uint32_t w = blockSize >= (4u << 20) ? (1u << 20) : 0u;
+    if (e) w = (uint32_t)atoi(e) << 10;
+    if (w + kLinkO0 > blockSize) w = 0;   // the warm bytes and their 64 KiB lie in the previous block
+    return w;
+}
+
 uint64_t link_round_bytes(uint64_t nBlocks) {
     return nBlocks * 4096 * 4 * 2 + (2 * (uint64_t)(kLinkRounds + 1) + 2 * nBlocks) * 4;
 }
@@ -1299,8 +1347,12 @@ hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32
     uint32_t* firstU = ctl + kLinkRounds + 1;
     uint32_t* flag = firstU + kLinkRounds + 1;
     uint32_t* enc = flag + nBlocks;
-    // first guess: blocks 1.. start from an all-stale table
+    // first guess: blocks 1.. start from the warm table (blocks of 256 KiB and
+    // up, k_link_warm) or an all-stale one
     if (hipMemsetAsync(entry, 0, (uint64_t)nBlocks * 4096 * 4, st) != hipSuccess) return hipErrorUnknown;
+    const uint32_t warm = link_cold() ? 0u : link_warm_bytes(blockSize);
+    if (nBlocks > 1 && warm)
+        hipLaunchKernelGGL(k_link_warm, dim3(nBlocks - 1), dim3(64), 0, st, src, blockSize, warm, slots, entry);
     const uint32_t nInit = 2 * (kLinkRounds + 1) + nBlocks;
     hipLaunchKernelGGL(k_link_init, dim3((nInit + 255) / 256), dim3(256), 0, st, ctl, nBlocks);
     for (int r = 0; r < rounds; ++r) {
