@@ -635,10 +635,10 @@ struct SrcRing {
         *(l_u64*)(r + o) = v;
         if (o < kSRMirror) *(l_u64*)(r + kSR + o) = v;
     }
-    __device__ __forceinline__ void init() {
-        B = 0;
-        for (uint32_t c = 0; c < kSR; c += 512) store(c, fetch(c));
-        pfPos = kSR;
+    __device__ __forceinline__ void init(uint32_t b0 = 0) {   // b0: a multiple of 512
+        B = b0;
+        for (uint32_t c = b0; c < b0 + kSR; c += 512) store(c, fetch(c));
+        pfPos = b0 + kSR;
         pf = fetch(pfPos);
         WAVE_SYNC();
     }
@@ -681,9 +681,11 @@ __device__ __forceinline__ uint32_t sff1(uint64_t m) { return m ? (uint32_t)__bu
 // SPLIT (byU16 only): positions in a u16 array and 8-bit tags in a u8
 // array (26 KiB of LDS in all: 6 waves per CU instead of 4); the marker
 // readback compares positions only (distinct per live lane).
-template <bool U16, bool SPLIT = false> struct V5Geo {
+template <bool U16, bool SPLIT = false, bool LINK = false> struct V5Geo {
     static constexpr uint32_t kTE = U16 ? 8192u : 4096u;
-    static constexpr uint32_t PB = U16 ? 16u : kPosBits;
+    // LINK: positions in the block-dependent coordinates (64 KiB of history
+    // before the block) need one more bit: 23-bit positions, 9-bit tags
+    static constexpr uint32_t PB = U16 ? 16u : (LINK ? kPosBits + 1 : kPosBits);
     static constexpr uint32_t PM = (1u << PB) - 1u;
     static constexpr uint32_t TB = SPLIT ? 8u : 32u - PB;   // tag bits
     static __device__ __forceinline__ uint32_t tag(uint32_t w0) { return (w0 * 0x85EBCA77u) >> (32 - TB); }
@@ -764,31 +766,39 @@ __device__ __forceinline__ void store_pend(const PendSeq& p, const SrcRing& V, g
     }
 }
 
-template <bool ST, bool U16, bool SPLIT = false>
+// LINK: one step of LZ4_compress_fast_continue (block-dependent frames):
+// positions in the coordinates of k_encode_linked (block at o0 = 65536, its
+// 64 KiB history below), the table carried in T unless lk.fresh, candidates
+// bounded by lk (see LinkArgs); n = o0 + block length.
+template <bool ST, bool U16, bool SPLIT = false, bool LINK = false>
 __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
-                                   l_u32* __restrict__ T, l_u8* __restrict__ R, uint64_t* acc) {
-    using G = V5Geo<U16, SPLIT>;
+                                   l_u32* __restrict__ T, l_u8* __restrict__ R, uint64_t* acc,
+                                   LinkArgs lk = LinkArgs{0, 0, 0, true}) {
+    using G = V5Geo<U16, SPLIT, LINK>;
     const G tab{T};
     const uint32_t L = laneid();
     uint64_t ts = STAMP_T();
-    const uint32_t bound = n + n / 255 + 16;
+    const uint32_t o0 = LINK ? kLinkO0 : 0u;   // position of the block's first byte
+    const uint32_t blen = n - o0;
+    const uint32_t bound = blen + blen / 255 + 16;
     const bool limited = cap < bound;
-    if (n < (uint32_t)kMinLength) {   // too short to search: one literal run (1.9.3 _last_literals)
-        if (limited && n + 1 + (n + 240) / 255 > cap) return 0;
-        if (L == 0) d[0] = (uint8_t)(n << 4);
-        for (uint32_t x = L; x < n; x += 64) d[1 + x] = s[x];
-        return (int32_t)(n + 1);
+    if (blen < (uint32_t)kMinLength) {   // too short to search: one literal run (1.9.3 _last_literals)
+        if (limited && (LINK && blen == 0 ? cap == 0 : blen + 1 + (blen + 240) / 255 > cap)) return 0;
+        if (L == 0) d[0] = (uint8_t)(blen << 4);
+        for (uint32_t x = L; x < blen; x += 64) d[1 + x] = s[o0 + x];
+        return (int32_t)(blen + 1);
     }
-    {
-        tab.init(G::tag(gld4u(s)) << G::PB);   // fresh entry = position 0 (a real candidate)
+    if (!LINK || lk.fresh) {
+        // a fresh entry is the block's position 0 -- a real candidate in LZ4 1.9.3
+        tab.init(o0 | (G::tag(gld4u(s + o0)) << G::PB));
     }
     SrcRing V{s, n, R, 0, 0, 0};
-    V.init();
+    V.init(o0);
     const uint32_t mflimitP1 = n - kMfLimit + 1;
     const uint32_t matchlimit = n - kLastLiterals;
     const uint32_t last4 = n - 4;
     const uint32_t dumIdx = G::kTE + L;
-    uint32_t anchor = 0, op = 0;
+    uint32_t anchor = o0, op = 0;
     PendSeq pe{};
     bool havePe = false;
     // window: lane 0 INSERT insPos, lane 1 TEST testPos, lane L >= 2 SEARCH
@@ -796,7 +806,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     // window state: sBase, k0 (+ s0, j1 derived from it) and the mode
     // (0 continuation: search only; 1 after a match ending at sBase - 1:
     // INSERT sBase - 3, TEST sBase - 1; 2 first window: INSERT 0)
-    uint32_t sBase = 1, k0 = 0, s0 = 1, j1 = 65, mode = 2;
+    uint32_t sBase = o0 + 1, k0 = 0, s0 = 1, j1 = 65, mode = 2;
     // ONE exit and no continue: the structurizer then needs no flow
     // variables and the loop-carried state stays in place across windows
     bool done = false, fail = false;
@@ -818,7 +828,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         const uint32_t step = s0 + (jx >= 0 ? 1u : 0u);
         const uint32_t sHi = sBase + 61 * s0 + (61 > j1 ? 61 - j1 : 0u);
         const bool insOn = mode != 0, testOn = mode == 1;
-        const uint32_t insPos = mode == 2 ? 0u : sBase - 3, testPos = sBase - 1;
+        const uint32_t insPos = mode == 2 ? o0 : sBase - 3, testPos = sBase - 1;
         p = L == 0 ? insPos : (L == 1 ? testPos : p);
         const bool srch = L >= 2;
         const bool live = srch ? p <= mflimitP1 : (L == 0 ? insOn : testOn);
@@ -847,7 +857,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         const uint32_t sv = tab.rb(ti);
         const uint64_t pend = bal(sv != (mark & G::kRbMask));   // same-bucket collision inside the window
         uint32_t cand = told & G::PM;
-        const bool cok = live && L != 0 && !term && cand + kDistMax >= p;
+        const bool cok = live && L != 0 && !term && cand + kDistMax >= p && (!LINK || cand >= lk.candLow);
         bool maybe = cok && (told >> G::PB) == (mark >> G::PB);
         const uint64_t tmk = bal(term);
         uint64_t mm = bal(maybe);
@@ -898,7 +908,8 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                 const int pi = (pred < 0 ? 0 : pred) * 4;
                 const uint32_t pw = (uint32_t)__builtin_amdgcn_ds_bpermute(pi, (int)w0);   // predecessor's bytes
                 const uint32_t pp = (uint32_t)__builtin_amdgcn_ds_bpermute(pi, (int)p);    // and position
-                const bool ok = live && L != 0 && !term && pred >= 0 && pp + kDistMax >= p && pw == w0;
+                const bool ok = live && L != 0 && !term && pred >= 0 && pp + kDistMax >= p && pw == w0 &&
+                                (!LINK || pp >= lk.candLow);
                 maybe = maybe && pred < 0;
                 cand = pred >= 0 ? pp : cand;
                 mm = bal(maybe);
@@ -909,13 +920,16 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                 if (w < 64 && !wTerm) {
                     ip = rdlane(p, (int)w);
                     cd = rdlane(cand, (int)w);
-                    maxb = w == 1 ? 0u : min(ip - anchor, cd);
+                    {   // catch-up bound: lz4's lowLimit for the candidate's side
+                        const uint32_t lowL = !LINK ? 0u : (cd >= o0 ? lk.lowIn : lk.lowDict);
+                        maxb = w == 1 ? 0u : min(ip - anchor, cd > lowL ? cd - lowL : 0u);
+                    }
                     const uint32_t ci = cd + 4 * L, ii = ip + 4 * L;
                     cw = gld4u(s + (ci < last4 ? ci : last4));   // lane 0: verify word; lanes >= 1: count words
                     iw = gld4u(s + (ii < last4 ? ii : last4));
                     const bool bOn = L < maxb;
-                    bi = s[bOn ? ip - L - 1 : 0u];
-                    bc = s[bOn ? cd - L - 1 : 0u];
+                    bi = s[bOn ? ip - L - 1 : o0];   // (o0: a byte of the block itself)
+                    bc = s[bOn ? cd - L - 1 : o0];
                     if (havePe) {
                         store_pend(pe, V, s, d);
                         havePe = false;
@@ -964,7 +978,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                 back += 64;
                 const uint32_t kb = back + L + 1;
                 const bool on = kb <= maxb;
-                fm = ~bal(on && s[on ? ip - kb : 0u] == s[on ? cd - kb : 0u]);
+                fm = ~bal(on && s[on ? ip - kb : o0] == s[on ? cd - kb : o0]);
             }
             back = fm ? back + (uint32_t)__builtin_ctzll(fm) : maxb;
             const uint32_t lim = matchlimit - (ip + kMinMatch);
@@ -1125,6 +1139,16 @@ __global__ void __launch_bounds__(64) k_encode16(const uint8_t* __restrict__ src
     if (laneid() == 0) csize[b] = r;
 }
 
+// A block-dependent table entry (position | tag, V5Geo<false, false, true>)
+// in the next block's coordinates: position x -> x - n; positions at or
+// below n (older than the next block's 64 KiB window) -> 0, stale like an
+// empty entry.
+constexpr uint32_t kLinkPM = (1u << (kPosBits + 1)) - 1u;
+__device__ __forceinline__ uint32_t link_rebase(uint32_t e, uint32_t n) {
+    const uint32_t pos = e & kLinkPM;
+    return pos > n ? (e & ~kLinkPM) | (pos - n) : 0u;
+}
+
 // Block-dependent frames (-BD, reference compressBlockDependency,
 // src/lz4mt.cpp:460-538): ONE wave encodes the blocks in order, as lz4's
 // LZ4_compress_limitedOutput_continue does (cap = inSize - 1): the byU32
@@ -1145,7 +1169,7 @@ __global__ void __launch_bounds__(64) k_encode_linked(const uint8_t* __restrict_
     if (gate && *gate == 0) return;   // the parallel rounds settled: nothing to redo
     ENCODE_LDS
     l_u32* Tl = (l_u32*)T;
-    l_u8* Sl = (l_u8*)S;
+    (void)S;
     l_u8* Xl = (l_u8*)X;
     const uint32_t L = laneid();
     // after parallel rounds: resume at the first unsettled block, whose
@@ -1162,15 +1186,14 @@ __global__ void __launch_bounds__(64) k_encode_linked(const uint8_t* __restrict_
         const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
         const LinkPlan pl = plan[b];
         const LinkArgs lk{pl.lowIn, pl.lowDict, pl.candLow, fresh && b == 0};
-        const int32_t r = encode_block<false, false, false, true>(gptr(src) + off - kLinkO0, kLinkO0 + n,
-                                                                  gptr(slots) + off, n - 1, Tl, Sl, (l_u32*)Xl,
-                                                                  Xl + kRingE, nullptr, lk);
+        const int32_t r = encode_block_v5<false, false, false, true>(gptr(src) + off - kLinkO0, kLinkO0 + n,
+                                                                     gptr(slots) + off, n - 1, Tl, Xl, nullptr, lk);
         if (L == 0) csize[b] = r;
         WAVE_SYNC();
         // the next block's coordinates: x -> x - n; older than the window -> 0
         for (uint32_t i = L; i < 4096; i += 64) {
             const uint32_t e = Tl[i];
-            Tl[i] = e > n ? e - n : 0u;
+            Tl[i] = link_rebase(e, n);
         }
         WAVE_SYNC();
     }
@@ -1216,6 +1239,7 @@ __global__ void __launch_bounds__(64) k_encode_linked_round(const uint8_t* __res
     const uint32_t b = blockIdx.x;
     if (*gate == 0 || flag[b] != round) return;   // settled / this block's entry did not change
     ENCODE_LDS
+    (void)S;
     l_u32* Tl = (l_u32*)T;
     const uint32_t L = laneid();
     const uint32_t* in = b == 0 ? first : entry + (uint64_t)b * 4096;
@@ -1228,9 +1252,8 @@ __global__ void __launch_bounds__(64) k_encode_linked_round(const uint8_t* __res
     const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
     const LinkPlan pl = plan[b];
     const LinkArgs lk{pl.lowIn, pl.lowDict, pl.candLow, fr};
-    const int32_t r = encode_block<false, false, false, true>(gptr(src) + off - kLinkO0, kLinkO0 + n,
-                                                              gptr(slots) + off, n - 1, Tl, (l_u8*)S, (l_u32*)X,
-                                                              (l_u8*)X + kRingE, nullptr, lk);
+    const int32_t r = encode_block_v5<false, false, false, true>(gptr(src) + off - kLinkO0, kLinkO0 + n,
+                                                                 gptr(slots) + off, n - 1, Tl, (l_u8*)X, nullptr, lk);
     if (L == 0) {
         csize[b] = r;
         enc[b] = round;
@@ -1239,7 +1262,7 @@ __global__ void __launch_bounds__(64) k_encode_linked_round(const uint8_t* __res
     uint32_t* o = exitT + (uint64_t)b * 4096;
     for (uint32_t i = L; i < 4096; i += 64) {
         const uint32_t e = Tl[i];
-        o[i] = e > n ? e - n : 0u;
+        o[i] = link_rebase(e, n);
     }
 }
 
@@ -1297,19 +1320,19 @@ __global__ void k_link_init(uint32_t* __restrict__ ctl, uint32_t nBlocks) {
 __global__ void __launch_bounds__(64) k_link_warm(const uint8_t* __restrict__ src, uint32_t blockSize, uint32_t W,
                                                   uint8_t* __restrict__ slots, uint32_t* __restrict__ entry) {
     ENCODE_LDS
+    (void)S;
     l_u32* Tl = (l_u32*)T;
     const uint32_t L = laneid();
     const uint32_t b = blockIdx.x + 1;
     const uint64_t off = (uint64_t)b * blockSize;   // block b's start; the warm bytes end there
     const LinkArgs lk{kLinkO0, kLinkO0, kLinkO0, true};   // no history: a fresh stream over the W bytes
-    (void)encode_block<false, false, false, true>(gptr(src) + off - W - kLinkO0, kLinkO0 + W, gptr(slots) + off,
-                                                  W + W / 255 + 16, Tl, (l_u8*)S, (l_u32*)X, (l_u8*)X + kRingE,
-                                                  nullptr, lk);
+    (void)encode_block_v5<false, false, false, true>(gptr(src) + off - W - kLinkO0, kLinkO0 + W, gptr(slots) + off,
+                                                     W + W / 255 + 16, Tl, (l_u8*)X, nullptr, lk);
     WAVE_SYNC();
     uint32_t* o = entry + (uint64_t)b * 4096;
     for (uint32_t i = L; i < 4096; i += 64) {
         const uint32_t e = Tl[i];
-        o[i] = e > W ? e - W : 0u;
+        o[i] = link_rebase(e, W);
     }
 }
 
