@@ -68,8 +68,9 @@ Lz4MtResult lz4mtHipCompressFrameAsync(const void* d_src, uint64_t srcSize, void
 
 /* The same with a compression level: 0..2 fast LZ4, 3..9 LZ4-HC (the
  * workspace then holds 2 more bytes per input byte: use
- * lz4mtHipCompressWorkspaceSizeEx).  BAD_ARG for levels 10..12 and for HC
- * on block-dependent frames. */
+ * lz4mtHipCompressWorkspaceSizeEx).  BAD_ARG for levels 10..12 on
+ * independent blocks; block-dependent frames at any level >= 3 are the
+ * reference's HC stream, which runs at lz4hc's level 9. */
 uint64_t lz4mtHipCompressWorkspaceSizeEx(uint64_t srcSize, const Lz4MtStreamDescriptor* sd, int level);
 Lz4MtResult lz4mtHipCompressFrameEx(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
                                     uint64_t* frameSize, const Lz4MtStreamDescriptor* sd, int level,

@@ -40,6 +40,9 @@ struct LinkState {
     uint32_t* table;
     bool fresh;
     uint32_t* rounds;    // parallel rounds' scratch, link_round_bytes(nBlocks) (null: the serial kernel)
+    // level >= 3: the HC stream's segments (hc_bd_pack's layout on the device)
+    const uint8_t* hcSegs = nullptr;
+    uint32_t nSeg = 0;
 };
 
 // Frame-walk summary written by the walk kernel.
@@ -120,6 +123,12 @@ hipError_t launch_encode_hc(const uint8_t* src, uint64_t srcSize, uint32_t block
                             uint8_t* slots, uint64_t slotStride, uint32_t capOverride, int level, uint16_t* delta,
                             int32_t* csize, hipStream_t st);
 uint32_t hc_attempts(int level);   // 0 for levels the library does not run (10..12)
+// -BD at level >= 3: segments [begin[k], end[k]) of src (begin >= -64 KiB),
+// blockSeg[b] = block b's segment; delta0 = chain scratch for src[0], with
+// 64 Ki entries before it.
+hipError_t launch_encode_hc_bd(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                               uint8_t* slots, const int64_t* segBegin, const int64_t* segEnd, uint32_t nSeg,
+                               const uint32_t* blockSeg, uint16_t* delta0, int32_t* csize, hipStream_t st);
 hipError_t launch_encode_linked(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                                 uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh, int32_t* csize,
                                 hipStream_t st);

@@ -71,7 +71,8 @@ CompressWs carve_compress(uint8_t* base, uint64_t nb, uint64_t bm, int level = 0
     uint64_t o = 0;
     auto take = [&](uint64_t n) { uint8_t* p = base ? base + o : nullptr; o = align_up(o + n, 256); return p; };
     w.slots = take(nb * bm + 64);
-    w.delta = level >= 3 ? reinterpret_cast<uint16_t*>(take(nb * bm * 2 + 64)) : nullptr;
+    // (-BD: 64 Ki entries more, for a segment that starts in the history before src)
+    w.delta = level >= 3 ? reinterpret_cast<uint16_t*>(take((nb * bm + 65536) * 2 + 64)) : nullptr;
     w.csize = reinterpret_cast<int32_t*>(take((nb + 1) * 4));
     w.bsum = reinterpret_cast<uint32_t*>(take((nb + 1) * 4));
     w.recOff = reinterpret_cast<uint64_t*>(take((nb + 1) * 8));
@@ -322,7 +323,14 @@ Lz4MtResult device_compress_body(const uint8_t* src, uint64_t n, uint32_t bm, in
     const uint64_t nb = (n + bm - 1) / bm;
     CompressWs w = carve_compress(ws, nb, bm, level);
     g_timing.mark(0, st);
-    if (link && link->rounds && !bd_serial())   // block-dependent: parallel rounds (exact; serial fallback)
+    if (link && level >= 3) {   // block-dependent LZ4-HC: the stream's segments, a wave per block
+        const uint8_t* g = link->hcSegs;
+        const uint32_t ns = link->nSeg;
+        HIPCHK(launch_encode_hc_bd(src, n, bm, (uint32_t)nb, w.slots, reinterpret_cast<const int64_t*>(g),
+                                   reinterpret_cast<const int64_t*>(g + 8 * (size_t)ns), ns,
+                                   reinterpret_cast<const uint32_t*>(g + 16 * (size_t)ns), w.delta + 65536, w.csize,
+                                   st));
+    } else if (link && link->rounds && !bd_serial())   // block-dependent: parallel rounds (exact; serial fallback)
         HIPCHK(launch_encode_linked_par(src, n, bm, (uint32_t)nb, w.slots, link->plan, link->table, link->fresh,
                                         link->rounds, w.csize, env_rounds(), st));
     else if (link)             // block-dependent frame: one wave, blocks in order (k_encode_linked)
@@ -470,10 +478,10 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
     if (v != LZ4MT_RESULT_OK) return v;
     if (!have_device()) return LZ4MT_RESULT_ERROR;
     if (frameCap < lz4mtHipFrameBound(srcSize, sd)) return LZ4MT_RESULT_BAD_ARG;
-    // LZ4-HC runs for levels 3..9 on independent blocks; the block-dependent
-    // HC stream (LZ4_compressHC_limitedOutput_continue) and levels 10..12
-    // (the optimal parser) are not provided
-    if (level >= 3 && (!sd->flg.blockIndependence || hc_attempts(level) == 0)) return LZ4MT_RESULT_BAD_ARG;
+    // LZ4-HC runs for levels 3..9 on independent blocks; levels 10..12 (the
+    // optimal parser) are not provided.  Block-dependent frames at any level
+    // >= 3 are the reference's HC stream, which runs at level 9 (HcBdSim).
+    if (level >= 3 && sd->flg.blockIndependence && hc_attempts(level) == 0) return LZ4MT_RESULT_BAD_ARG;
     if (level < 3) level = 0;
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     const uint64_t need = compress_ws_bytes(srcSize, bm, level);
@@ -513,7 +521,21 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
     // table buffer, kept per thread (the kernels of an async call use them)
     LinkState ls{};
     const LinkState* lsp = nullptr;
-    if (!sd->flg.blockIndependence) {
+    if (!sd->flg.blockIndependence && level >= 3) {
+        thread_local DevBuf segBuf;
+        thread_local std::vector<uint64_t> segAbs;
+        thread_local std::vector<uint8_t> packed;
+        const uint64_t nb = (srcSize + bm - 1) / bm;
+        segAbs.assign(nb, 0);
+        HcBdSim sim(sd->bd.blockMaximumSize);
+        for (uint64_t b = 0; b < nb; ++b) segAbs[b] = sim.next((uint32_t)std::min<uint64_t>(bm, srcSize - b * bm));
+        ls.nSeg = hc_bd_pack(segAbs.data(), nb, 0, srcSize, 0, packed);
+        if (!segBuf.ensure(packed.size() + 64)) return LZ4MT_RESULT_ERROR;
+        if (!packed.empty())
+            HIPCHK(hipMemcpyAsync(segBuf.p, packed.data(), packed.size(), hipMemcpyHostToDevice, st));
+        ls.hcSegs = static_cast<const uint8_t*>(segBuf.p);
+        lsp = &ls;
+    } else if (!sd->flg.blockIndependence) {
         thread_local DevBuf planBuf, tableBuf, roundBuf;
         thread_local std::vector<LinkPlan> hplan;
         const uint64_t nb = (srcSize + bm - 1) / bm;

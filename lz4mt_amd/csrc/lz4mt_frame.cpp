@@ -513,10 +513,11 @@ struct CallBuf {
 
 void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
     if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return; }
-    // LZ4-HC (levels 3..9) on independent blocks; the block-dependent HC
-    // stream and lz4's optimal parser (10..12) are not provided
+    // LZ4-HC (levels 3..9) on independent blocks; lz4's optimal parser
+    // (10..12) is not provided.  Block-dependent frames at any level >= 3 are
+    // the reference's HC stream, at level 9 (HcBdSim).
     const int level = s.level() >= 3 ? s.level() : 0;
-    if (level && (!sd->flg.blockIndependence || hc_attempts(level) == 0)) { s.quit(LZ4MT_RESULT_BAD_ARG); return; }
+    if (level && sd->flg.blockIndependence && hc_attempts(level) == 0) { s.quit(LZ4MT_RESULT_BAD_ARG); return; }
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
     // Block-dependent frames (compressBlockDependency, src/lz4mt.cpp:460-538)
@@ -528,11 +529,14 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
     PipeShape P = pipe_shape(true);
     if (linked) P.slots = 1;
     BdSim sim(sd->bd.blockMaximumSize);
+    HcBdSim hsim(sd->bd.blockMaximumSize);   // level >= 3
     std::vector<uint8_t> hist(linked ? 65536 : 0, 0);
     std::vector<LinkPlan> plan;
+    std::vector<uint64_t> segAbs;
+    std::vector<uint8_t> packed;
     CallBuf table, dplan, rounds;
     if (linked && !table.alloc(4096 * 4)) { s.quit(LZ4MT_RESULT_ERROR); return; }
-    uint64_t batch = 0, planCap = 0, roundCap = 0;
+    uint64_t batch = 0, planCap = 0, roundCap = 0, streamPos = 0;
     auto fill = [&](Slot& S, bool* stop) -> bool {
         const uint64_t K = batch_blocks(P, bm, batch++), inCap = K * bm;
         if (!S.ensure(pre + inCap, inCap + K * 8 + 64, compress_ws_bytes(inCap, bm, level), 0)) {
@@ -555,7 +559,22 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
         uint64_t* dRecOff = nullptr;
         const uint64_t nb = (total + bm - 1) / bm;
         LinkState ls{};
-        if (linked) {
+        if (linked && level) {   // the HC stream's segments over (hist ++ this input)
+            memcpy(S.hIn, hist.data(), 65536);
+            segAbs.resize(nb);
+            for (uint64_t b = 0; b < nb; ++b) segAbs[b] = hsim.next((uint32_t)std::min<uint64_t>(bm, total - b * bm));
+            ls.nSeg = hc_bd_pack(segAbs.data(), nb, streamPos, total, 65536, packed);
+            if (packed.size() + 64 > planCap * sizeof(LinkPlan)) {
+                if (dplan.p) { hipStreamSynchronize(S.st); hipFree(dplan.p); dplan.p = nullptr; }
+                planCap = (packed.size() + 64 + sizeof(LinkPlan) - 1) / sizeof(LinkPlan);
+                if (!dplan.alloc(planCap * sizeof(LinkPlan))) { s.quit(LZ4MT_RESULT_ERROR); return false; }
+            }
+            if (hipMemcpyAsync(dplan.p, packed.data(), packed.size(), hipMemcpyHostToDevice, S.st) != hipSuccess) {
+                s.quit(LZ4MT_RESULT_ERROR);
+                return false;
+            }
+            ls.hcSegs = static_cast<const uint8_t*>(dplan.p);
+        } else if (linked) {
             memcpy(S.hIn, hist.data(), 65536);
             plan.resize(nb);
             for (uint64_t b = 0; b < nb; ++b)
@@ -578,13 +597,15 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
             }
             ls = LinkState{static_cast<LinkPlan*>(dplan.p), static_cast<uint32_t*>(table.p), batch == 1,
                            static_cast<uint32_t*>(rounds.p)};
-            // the history of the next batch: the last 64 KiB of (hist ++ this input)
+        }
+        if (linked) {   // the history of the next batch: the last 64 KiB of (hist ++ this input)
             if (total >= 65536) memcpy(hist.data(), in + total - 65536, 65536);
             else {
                 memmove(hist.data(), hist.data() + total, 65536 - total);
                 memcpy(hist.data() + 65536 - total, in, total);
             }
         }
+        streamPos += total;
         if (hipMemcpyAsync(S.dIn, S.hIn, pre + total, hipMemcpyHostToDevice, S.st) != hipSuccess ||
             device_compress_body(S.dIn + pre, total, bm, bck, S.dWs, S.dOut, 0, S.st, &dRecOff, nullptr,
                                  linked ? &ls : nullptr, level) != LZ4MT_RESULT_OK ||

@@ -69,15 +69,8 @@ __device__ __forceinline__ uint32_t hc_hash(uint32_t v) { return (v * 2654435761
 // k_hc_prev: delta[p] = p - (previous position with the same hash), 0 if
 // none within 65535, for p in [0, n - 4] (positions lz4hc may insert)
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_hc_prev(const uint8_t* __restrict__ src, uint64_t srcSize, uint32_t blockSize,
-                                                uint16_t* __restrict__ delta) {
-    __shared__ uint32_t last[1u << kHashLog];   // position + 1 of the latest occurrence (0 = none)
-    __shared__ uint8_t dd[1024];                // duplicate-hash detection inside a step
-    const uint32_t b = blockIdx.x;
-    const uint64_t off = (uint64_t)b * blockSize;
-    const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
-    g_cu8* s = (g_cu8*)src + off;
-    g_u16* dl = (g_u16*)delta + off;
+// one wave over the n bytes at s: dl[p] for p in [0, n - 4]
+__device__ void hc_prev_range(g_cu8* s, uint32_t n, g_u16* dl, l_u32* last, l_u8* dd) {
     const uint32_t L = laneid();
     for (uint32_t i = L; i < (1u << kHashLog); i += 64) last[i] = 0;
     WAVE_SYNC();
@@ -88,9 +81,9 @@ __global__ void __launch_bounds__(64) k_hc_prev(const uint8_t* __restrict__ src,
         const bool live = p < np;
         const uint32_t h = live ? hc_hash(rd32(s + p)) : 0u;
         // lanes sharing a hash: the group's earlier member is the predecessor
-        if (live) ((l_u8*)dd)[h & 1023] = (uint8_t)L;
+        if (live) dd[h & 1023] = (uint8_t)L;
         WAVE_SYNC();
-        const uint32_t sv = live ? ((l_u8*)dd)[h & 1023] : L;
+        const uint32_t sv = live ? dd[h & 1023] : L;
         uint64_t pending = ballot(live && sv != L);
         int pred = -1;
         uint64_t gm = 1ull << L;
@@ -106,15 +99,37 @@ __global__ void __launch_bounds__(64) k_hc_prev(const uint8_t* __restrict__ src,
             pending &= ~m;
         }
         if (live) {
-            uint32_t q1 = pred >= 0 ? base + (uint32_t)pred + 1 : ((l_u32*)last)[h];   // position + 1 of the previous
+            uint32_t q1 = pred >= 0 ? base + (uint32_t)pred + 1 : last[h];   // position + 1 of the previous
             const uint32_t d = (q1 && p + 1 - q1 <= kHcDist) ? p + 1 - q1 : 0u;
             dl[p] = (uint16_t)d;
         }
         WAVE_SYNC();
         // the group's last member records its position
-        if (live && !(gm & ~((2ull << L) - 1ull))) ((l_u32*)last)[h] = p + 1;
+        if (live && !(gm & ~((2ull << L) - 1ull))) last[h] = p + 1;
         WAVE_SYNC();
     }
+}
+
+__global__ void __launch_bounds__(64) k_hc_prev(const uint8_t* __restrict__ src, uint64_t srcSize, uint32_t blockSize,
+                                                uint16_t* __restrict__ delta) {
+    __shared__ uint32_t last[1u << kHashLog];   // position + 1 of the latest occurrence (0 = none)
+    __shared__ uint8_t dd[1024];                // duplicate-hash detection inside a step
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
+    hc_prev_range((g_cu8*)src + off, n, (g_u16*)delta + off, (l_u32*)last, (l_u8*)dd);
+}
+
+// -BD at level >= 3: the chain over each stream segment (the bytes between
+// two resets of the reference's HC stream), segment k = src[begin, end)
+// (begin may lie up to 64 KiB before src: the previous batch's history)
+__global__ void __launch_bounds__(64) k_hc_prev_seg(const uint8_t* __restrict__ src, const int64_t* __restrict__ begin,
+                                                    const int64_t* __restrict__ end, uint16_t* __restrict__ delta0) {
+    __shared__ uint32_t last[1u << kHashLog];
+    __shared__ uint8_t dd[1024];
+    const uint32_t k = blockIdx.x;
+    const int64_t b0 = begin[k];
+    hc_prev_range((g_cu8*)src + b0, (uint32_t)(end[k] - b0), (g_u16*)delta0 + b0, (l_u32*)last, (l_u8*)dd);
 }
 
 // ---------------------------------------------------------------------------
@@ -311,16 +326,19 @@ __device__ bool hc_encode(g_cu8* s, g_u8* d, uint32_t& ip, uint32_t& op, uint32_
 }
 
 // LZ4HC_compress_hashChain; 0 = does not fit cap (store raw)
-__device__ int32_t encode_block_hc(const HcBlock& B, g_u8* d, uint32_t cap) {
+// The block is [start, B.n) of B.s (start > 0: the rest of a stream segment
+// before it, -BD at level >= 3).
+__device__ int32_t encode_block_hc(const HcBlock& B, g_u8* d, uint32_t cap, uint32_t start = 0) {
     const uint32_t L = laneid();
     const uint32_t n = B.n;
+    const uint32_t blen = n - start;
     g_cu8* s = B.s;
-    const bool limit = (uint64_t)cap < (uint64_t)n + n / 255 + 16;
-    uint32_t ip = 0, anchor = 0, op = 0;
+    const bool limit = (uint64_t)cap < (uint64_t)blen + blen / 255 + 16;
+    uint32_t ip = start, anchor = start, op = 0;
     const uint32_t mflimit = n >= 12 ? n - 12 : 0, matchlimit = n >= 5 ? n - 5 : 0;
     int ml0, ml, ml2, ml3;
     uint32_t start0 = 0, ref0 = 0, ref = 0, start2 = 0, ref2 = 0, start3 = 0, ref3 = 0;
-    if (n < 13) goto last_literals;
+    if (blen < 13) goto last_literals;
     while (ip <= mflimit) {
         {
             uint32_t useless = ip;
@@ -424,6 +442,39 @@ __global__ void __launch_bounds__(64) k_encode_hc(const uint8_t* __restrict__ sr
     HcBlock B{(g_cu8*)src + off, n, (g_cu16*)delta + off, maxAttempts, maxAttempts > 128};
     const int32_t r = encode_block_hc(B, (g_u8*)slots + (uint64_t)b * slotStride, cap);
     if (laneid() == 0) csize[b] = r;
+}
+
+// -BD at level >= 3 (compressBlockDependency with the HC stream, reference
+// src/lz4mt.cpp:295-332): LZ4_resetStreamStateHC leaves the stream at lz4hc's
+// default level 9 whatever the context asks for, LZ4_slideInputBufferHC
+// resets it, and every position is inserted into the chain (LZ4HC_Insert),
+// so block b's parse depends only on the bytes of its segment before it:
+// the hashChain parse of [o, o + len) over the segment, lowest match index
+// = the segment start (or 64 KiB back), chain = k_hc_prev_seg.  No rounds.
+__global__ void __launch_bounds__(64) k_encode_hc_bd(const uint8_t* __restrict__ src, uint64_t srcSize,
+                                                     uint32_t blockSize, uint8_t* __restrict__ slots,
+                                                     const int64_t* __restrict__ begin,
+                                                     const uint32_t* __restrict__ blockSeg,
+                                                     const uint16_t* __restrict__ delta0,
+                                                     int32_t* __restrict__ csize) {
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t len = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
+    const int64_t S = begin[blockSeg[b]];
+    const uint32_t o = (uint32_t)((int64_t)off - S);
+    HcBlock B{(g_cu8*)src + S, o + len, (g_cu16*)delta0 + S, 256u, true};   // level 9
+    const int32_t r = encode_block_hc(B, (g_u8*)slots + off, len - 1, o);   // cap = inSize - 1
+    if (laneid() == 0) csize[b] = r;
+}
+
+hipError_t launch_encode_hc_bd(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                               uint8_t* slots, const int64_t* segBegin, const int64_t* segEnd, uint32_t nSeg,
+                               const uint32_t* blockSeg, uint16_t* delta0, int32_t* csize, hipStream_t st) {
+    if (nBlocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hc_prev_seg, dim3(nSeg), dim3(64), 0, st, src, segBegin, segEnd, delta0);
+    hipLaunchKernelGGL(k_encode_hc_bd, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, segBegin,
+                       blockSeg, (const uint16_t*)delta0, csize);
+    return hipGetLastError();
 }
 
 // level -> maxNbAttempts (lz4 1.9.3 clTable, levels 1..9; < 1 = default 9)

@@ -7,6 +7,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <vector>
+
 #include "../../include/lz4mt.h"
 
 namespace lz4mt {
@@ -219,5 +221,52 @@ struct BdSim {
         inStart += n;
     }
 };
+
+// -BD at level >= 3 (the same loop over the HC stream, src/lz4mt.cpp:295-332):
+// LZ4_slideInputBufferHC resets lz4 1.9.3's HC stream, and the next block
+// starts a new segment at the front of the buffer; inside a segment every
+// block continues the one before it (one prefix, every position inserted).
+// next() returns the stream offset where the next block's segment starts.
+struct HcBdSim {
+    uint64_t bm = 0, bufSize = 0, inStart = 0, pos = 0, seg = 0;
+    explicit HcBdSim(int blockMaxId) {
+        bm = (uint64_t)1 << (8 + 2 * blockMaxId);
+        const uint64_t b = bm + 65536, m = (1024 + 64) * 1024;
+        bufSize = b > m ? b : m;
+    }
+    uint64_t next(uint32_t n) {
+        if (inStart + bm > bufSize) { inStart = 0; seg = pos; }   // translate(): a fresh stream
+        inStart += n;
+        pos += n;
+        return seg;
+    }
+};
+
+// The segments of a batch of blocks for k_hc_prev_seg / k_encode_hc_bd:
+// segAbs[b] = stream offset of block b's segment (HcBdSim), the batch
+// starting at stream offset A with `hist` (<= 64 KiB) bytes of history
+// before it, `total` input bytes.  Packs begin[nSeg], end[nSeg] (int64,
+// relative to A; a begin before A - hist is clamped there: no match or chain
+// link reaches more than 64 KiB back) and blockSeg[nb] (uint32) into `out`.
+inline uint32_t hc_bd_pack(const uint64_t* segAbs, uint64_t nb, uint64_t A, uint64_t total, uint64_t hist,
+                           std::vector<uint8_t>& out) {
+    std::vector<int64_t> begin, end;
+    std::vector<uint32_t> blockSeg(nb);
+    for (uint64_t b = 0; b < nb; ++b) {
+        if (b == 0 || segAbs[b] != segAbs[b - 1]) {
+            const int64_t lo = (int64_t)segAbs[b] - (int64_t)A, floor = -(int64_t)hist;
+            if (!begin.empty()) end.push_back(lo);
+            begin.push_back(lo > floor ? lo : floor);
+        }
+        blockSeg[b] = (uint32_t)(begin.size() - 1);
+    }
+    end.push_back((int64_t)total);
+    const uint32_t nSeg = (uint32_t)begin.size();
+    out.resize(16 * (size_t)nSeg + 4 * nb);
+    memcpy(out.data(), begin.data(), 8 * (size_t)nSeg);
+    memcpy(out.data() + 8 * (size_t)nSeg, end.data(), 8 * (size_t)nSeg);
+    memcpy(out.data() + 16 * (size_t)nSeg, blockSeg.data(), 4 * nb);
+    return nSeg;
+}
 
 }  // namespace lz4mt

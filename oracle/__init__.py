@@ -6,6 +6,7 @@ this module, and only as the checker / CPU baseline.  The product
 how it is pinned (liblz4 1.9.3, python-xxhash, lz4 CLI).
 """
 import ctypes
+import struct
 import os
 import subprocess
 
@@ -50,6 +51,8 @@ def _load():
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz)]
     lib.orc_pipeline_roundtrip_codec.argtypes = [u8p, sz, ctypes.POINTER(FrameParams), ctypes.c_int,
                                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz), u8p, u8p]
+    lib.orc_bd_hc_body.restype = ctypes.c_int64
+    lib.orc_bd_hc_body.argtypes = [u8p, sz, ctypes.c_int, ctypes.c_int, u8p]
     lib.orc_hc_codec_set.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.orc_bd_roundtrip.argtypes = [u8p, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -86,6 +89,20 @@ def compress_block_hc(data, cap=None, level=9):
     if n < 0:
         raise ValueError("HC levels above 9 (the optimal parser) are not restated")
     return dst.raw[:n]
+
+
+def bd_hc_frame(data, block_max_id, stream_checksum, block_checksum):
+    """A -BD frame at compression level >= 3 (compressBlockDependency over
+    the legacy HC stream, reference src/lz4mt.cpp:295-332, 460-538):
+    header (FLG.5 = 0), orc_bd_hc_body's records, end mark, [content XXH32]."""
+    flg = 0x40 | (0x10 if block_checksum else 0) | (0x04 if stream_checksum else 0)
+    desc = bytes([flg, block_max_id << 4])
+    hdr = struct.pack("<I", 0x184D2204) + desc + bytes([(xxh32(desc) >> 8) & 0xFF])
+    nb = (len(data) + (1 << (8 + 2 * block_max_id)) - 1) >> (8 + 2 * block_max_id)
+    dst = ctypes.create_string_buffer(len(data) + 8 * nb + 16)
+    n = lib.orc_bd_hc_body(_buf(data), len(data), block_max_id, int(block_checksum), dst)
+    tail = b"\0\0\0\0" + (struct.pack("<I", xxh32(data)) if stream_checksum else b"")
+    return hdr + dst.raw[:n] + tail
 
 
 def decompress_block(block, cap):

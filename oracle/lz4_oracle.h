@@ -58,6 +58,8 @@ int orc_lz4_decompress_safe(const uint8_t* src, uint8_t* dst, int srcSize,
 /* LZ4-HC 1.9.3 LZ4_compress_HC (= LZ4_compressHC2_limitedOutput, lz4mt's
  * codec for levels >= 3): levels 1..9 (hash chain); -1 for 10..12. */
 int orc_lz4hc_compress(const uint8_t* src, uint8_t* dst, int n, int cap, int level);
+/* -BD frame body at level >= 3 (the legacy HC stream, level 9); returns its size. */
+int64_t orc_bd_hc_body(const uint8_t* src, size_t n, int blockMaxId, int bck, uint8_t* out);
 
 /* LZ4_decompress_safe_withPrefix64k 1.9.3: dst[-65536..-1] is history. */
 int orc_lz4_decompress_safe_prefix64k(const uint8_t* src, uint8_t* dst,

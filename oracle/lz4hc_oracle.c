@@ -215,21 +215,13 @@ static int hc_encode(const uint8_t** ip, uint8_t** op, const uint8_t** anchor, i
     return 0;
 }
 
-int orc_lz4hc_compress(const uint8_t* src, uint8_t* dst, int n, int cap, int level) {
-    static const int kAttempts[10] = {2, 2, 2, 4, 8, 16, 32, 64, 128, 256};   /* clTable[0..9] */
-    if ((unsigned)n > 0x7E000000u) return 0;
-    if (level < 1) level = 9;   /* LZ4HC_CLEVEL_DEFAULT */
-    if (level > 9) return -1;   /* the optimal parser (10..12) is not restated */
-    const int maxNbAttempts = kAttempts[level];
-    const int patternAnalysis = maxNbAttempts > 128;
+/* LZ4HC_compress_hashChain over the n bytes at ip0 (inside c->s: the bytes
+ * of c->s before ip0 are the prefix the stream has already seen, every
+ * position of it inserted as LZ4HC_Insert does); 0 = does not fit cap. */
+static int hc_compress_range(hc_ctx* c, const uint8_t* ip0, uint8_t* dst, int n, int cap, int maxNbAttempts,
+                             int patternAnalysis) {
     const int limit = cap < orc_lz4_compress_bound(n);
-    hc_ctx c;
-    c.s = src;
-    c.n = n;
-    c.hashTable = (uint32_t*)calloc(1u << HC_HASH_LOG, sizeof(uint32_t));
-    c.chainTable = (uint16_t*)calloc(65536, sizeof(uint16_t));
-    c.nextToUpdate = HC_BASE;
-    const uint8_t* ip = src;
+    const uint8_t* ip = ip0;
     const uint8_t* anchor = ip;
     const uint8_t* const iend = ip + n;
     const uint8_t* const mflimit = iend - HC_MFLIMIT;
@@ -244,14 +236,14 @@ int orc_lz4hc_compress(const uint8_t* src, uint8_t* dst, int n, int cap, int lev
     while (ip <= mflimit) {
         {
             const uint8_t* useless = ip;
-            ml = hc_wider_match(&c, ip, ip, matchlimit, HC_MINMATCH - 1, &ref, &useless, maxNbAttempts,
+            ml = hc_wider_match(c, ip, ip, matchlimit, HC_MINMATCH - 1, &ref, &useless, maxNbAttempts,
                                 patternAnalysis);
         }
         if (ml < HC_MINMATCH) { ip++; continue; }
         start0 = ip; ref0 = ref; ml0 = ml;
     search2:
         if (ip + ml <= mflimit)
-            ml2 = hc_wider_match(&c, ip + ml - 2, ip, matchlimit, ml, &ref2, &start2, maxNbAttempts, patternAnalysis);
+            ml2 = hc_wider_match(c, ip + ml - 2, ip, matchlimit, ml, &ref2, &start2, maxNbAttempts, patternAnalysis);
         else
             ml2 = ml;
         if (ml2 == ml) {   /* no better match: encode ML1 */
@@ -272,7 +264,7 @@ int orc_lz4hc_compress(const uint8_t* src, uint8_t* dst, int n, int cap, int lev
             if (correction > 0) { start2 += correction; ref2 += correction; ml2 -= correction; }
         }
         if (start2 + ml2 <= mflimit)
-            ml3 = hc_wider_match(&c, start2 + ml2 - 3, start2, matchlimit, ml2, &ref3, &start3, maxNbAttempts,
+            ml3 = hc_wider_match(c, start2 + ml2 - 3, start2, matchlimit, ml2, &ref3, &start3, maxNbAttempts,
                                  patternAnalysis);
         else
             ml3 = ml2;
@@ -333,7 +325,76 @@ last_literals:
     }
     result = (int)(op - dst);
 overflow:
+    return result;
+}
+
+static void hc_ctx_init(hc_ctx* c, const uint8_t* s, int n) {
+    c->s = s;
+    c->n = n;
+    memset(c->hashTable, 0, (1u << HC_HASH_LOG) * sizeof(uint32_t));
+    memset(c->chainTable, 0, 65536 * sizeof(uint16_t));
+    c->nextToUpdate = HC_BASE;
+}
+
+int orc_lz4hc_compress(const uint8_t* src, uint8_t* dst, int n, int cap, int level) {
+    static const int kAttempts[10] = {2, 2, 2, 4, 8, 16, 32, 64, 128, 256};   /* clTable[0..9] */
+    if ((unsigned)n > 0x7E000000u) return 0;
+    if (level < 1) level = 9;   /* LZ4HC_CLEVEL_DEFAULT */
+    if (level > 9) return -1;   /* the optimal parser (10..12) is not restated */
+    hc_ctx c;
+    c.hashTable = (uint32_t*)malloc((1u << HC_HASH_LOG) * sizeof(uint32_t));
+    c.chainTable = (uint16_t*)malloc(65536 * sizeof(uint16_t));
+    hc_ctx_init(&c, src, n);
+    const int r = hc_compress_range(&c, src, dst, n, cap, kAttempts[level], kAttempts[level] > 128);
     free(c.hashTable);
     free(c.chainTable);
-    return result;
+    return r;
+}
+
+/* -BD at level >= 3: compressBlockDependency over the legacy HC stream
+ * (reference src/lz4mt.cpp:295-332, 460-538, lz4 1.9.3): the input buffer
+ * of max(blockMax + 64 KiB, 1088 KiB) bytes; LZ4_resetStreamStateHC leaves
+ * the stream at the default level 9; each block is
+ * LZ4_compressHC_limitedOutput_continue (cap = inSize - 1) over the blocks
+ * before it in the buffer; when the next block would not fit,
+ * LZ4_slideInputBufferHC resets the stream (a new segment, no dictionary).
+ * Writes the frame body (records: size word, payload, [block XXH32]) to
+ * out (n + 8 * blocks bytes at most) and returns its size. */
+int64_t orc_bd_hc_body(const uint8_t* src, size_t n, int blockMaxId, int bck, uint8_t* out) {
+    const size_t bm = (size_t)1 << (8 + 2 * blockMaxId);
+    const size_t bufSize = bm + 65536 > (size_t)(1024 + 64) * 1024 ? bm + 65536 : (size_t)(1024 + 64) * 1024;
+    hc_ctx c;
+    c.hashTable = (uint32_t*)malloc((1u << HC_HASH_LOG) * sizeof(uint32_t));
+    c.chainTable = (uint16_t*)malloc(65536 * sizeof(uint16_t));
+    size_t inStart = 0, seg = 0, op = 0;
+    for (size_t pos = 0; pos < n;) {
+        const size_t len = n - pos < bm ? n - pos : bm;
+        if (pos == 0 || inStart + bm > bufSize) {   /* translate(): a fresh stream */
+            inStart = 0;
+            seg = pos;
+            hc_ctx_init(&c, src + seg, 0);
+        }
+        uint8_t* rec = out + op;
+        int cs = hc_compress_range(&c, src + pos, rec + 4, (int)len, (int)len - 1, 256, 1);
+        if (cs <= 0) {
+            memcpy(rec + 4, src + pos, len);
+            cs = (int)len;
+            rec[0] = (uint8_t)len; rec[1] = (uint8_t)(len >> 8); rec[2] = (uint8_t)(len >> 16);
+            rec[3] = (uint8_t)((len >> 24) | 0x80);
+        } else {
+            rec[0] = (uint8_t)cs; rec[1] = (uint8_t)(cs >> 8); rec[2] = (uint8_t)(cs >> 16); rec[3] = (uint8_t)(cs >> 24);
+        }
+        op += 4 + (size_t)cs;
+        if (bck) {
+            const uint32_t h = orc_xxh32(rec + 4, (size_t)cs, 0);
+            out[op] = (uint8_t)h; out[op + 1] = (uint8_t)(h >> 8); out[op + 2] = (uint8_t)(h >> 16);
+            out[op + 3] = (uint8_t)(h >> 24);
+            op += 4;
+        }
+        inStart += len;
+        pos += len;
+    }
+    free(c.hashTable);
+    free(c.chainTable);
+    return (int64_t)op;
 }

@@ -121,6 +121,38 @@ def bd_frame_reference(data, bid, sck, bck):
     return _bd_header(bid, sck, bck) + _bd_records(blocks, bck) + tail
 
 
+def bd_hc_frame_reference(data, bid, sck, bck):
+    """compressBlockDependency at compression level >= 3 (reference
+    src/lz4mt.cpp:295-332, 460-538) replayed on liblz4 1.9.3: the legacy HC
+    stream -- LZ4_resetStreamStateHC(state, inputBuffer) (which sets the
+    stream to lz4hc's default level 9 whatever ctx.compressionLevel says),
+    LZ4_compressHC_limitedOutput_continue (cap = inSize - 1), and
+    LZ4_slideInputBufferHC when the next block would not fit (in 1.9.3 it
+    resets the stream: the next block starts without a dictionary)."""
+    LZ4.LZ4_slideInputBufferHC.restype = ctypes.c_void_p
+    bm = 1 << (8 + 2 * bid)
+    size = max(bm + 65536, (1024 + 64) * 1024)
+    buf = ctypes.create_string_buffer(size)
+    base = ctypes.addressof(buf)
+    dst = ctypes.create_string_buffer(bm + 64)
+    st = ctypes.create_string_buffer(LZ4.LZ4_sizeofStreamStateHC())
+    assert LZ4.LZ4_resetStreamStateHC(st, buf) == 0
+    ins, pos, blocks = base, 0, []
+    while True:
+        if ins + bm > base + size:
+            ins = LZ4.LZ4_slideInputBufferHC(st)
+        chunk = data[pos:pos + bm]
+        if not chunk:
+            break
+        ctypes.memmove(ins, chunk, len(chunk))
+        pos += len(chunk)
+        n = LZ4.LZ4_compressHC_limitedOutput_continue(st, ctypes.c_void_p(ins), dst, len(chunk), len(chunk) - 1)
+        blocks.append((dst.raw[:n], False) if n > 0 else (chunk, True))
+        ins += len(chunk)
+    tail = b"\0\0\0\0" + (struct.pack("<I", xxh(data)) if sck else b"")
+    return _bd_header(bid, sck, bck) + _bd_records(blocks, bck) + tail
+
+
 def bd_frame_contiguous(data, bid, sck, bck):
     """The same stream compressed from one contiguous buffer (every block in
     LZ4 prefix mode after the first), cap = inSize - 1: what the reference's
@@ -189,12 +221,42 @@ BD_CASES = [  # (name, bytes, seed, block id, stream checksum, block checksum[, 
     ("bd_rand", 300_000, 38, 4, True, True, "random"), ("bd_mix4", 1_300_000, 39, 4, False, True, "mixed"),
     ("bd_mix5", 1_300_000, 40, 5, True, True, "mixed"),
 ]
+BD_HC_CASES = [  # -BD at level >= 3 (lz4hc level 9 stream): (name, bytes, seed, id, sck, bck[, kind])
+    ("bdhc_b4_sX", 1_500_000, 51, 4, False, True), ("bdhc_b5_Sx", 1_500_000, 52, 5, True, False),
+    ("bdhc_b6_SX", 2_500_000, 53, 6, True, True), ("bdhc_e13", 13, 54, 4, False, True),
+    ("bdhc_e64k1", 65537, 55, 4, True, True), ("bdhc_mix4", 1_300_000, 56, 4, False, True, "mixed"),
+    ("bdhc_zero", 300_000, 57, 5, False, True, "zeros"), ("bdhc_rand", 200_000, 58, 4, True, True, "random"),
+]
+BD_HC_KNOWN = [  # (name, bytes, seed, id, sck, bck): size + XXH32 only
+    ("bdhc_b7_9m", 9_437_184 + 4321, 61, 7, True, True), ("bdhc_b4_9m", 9_437_184 + 4321, 62, 4, False, True),
+]
 BD_KNOWN = [  # larger -BD frames pinned by size + XXH32 only: (name, bytes, seed, id, sck, bck, writer)
     ("bd_b4_9m", 9_437_184 + 4321, 21, 4, False, True, "reference"),
     ("bd_b5_9m", 9_437_184 + 4321, 22, 5, True, True, "reference"),
     ("bd_b6_9m", 9_437_184 + 4321, 23, 6, False, True, "contiguous"),
     ("bd_b7_9m", 9_437_184 + 4321, 24, 7, True, False, "contiguous"),
 ]
+
+
+def bd_hc_main(manifest):
+    manifest["bd_hc_frames"], manifest["bd_hc_known"] = [], []
+    for name, n, seed, bid, sck, bck, *kind in BD_HC_CASES:
+        entry = {"name": name, "bytes": n, "seed": seed, "bid": bid, "stream_checksum": sck, "block_checksum": bck}
+        if kind:
+            entry["kind"] = kind[0]
+        data = bd_data(entry)
+        f = bd_hc_frame_reference(data, bid, sck, bck)
+        assert bd_decode_reference(f) == data, name
+        open(os.path.join(HERE, "frames", f"{name}.lz4"), "wb").write(f)
+        entry.update({"file": f"frames/{name}.lz4", "size": len(f), "xxh32": xxh(f), "content_xxh32": xxh(data)})
+        manifest["bd_hc_frames"].append(entry)
+    for name, n, seed, bid, sck, bck in BD_HC_KNOWN:
+        data = bd_input(n, seed)
+        f = bd_hc_frame_reference(data, bid, sck, bck)
+        assert bd_decode_reference(f) == data, name
+        manifest["bd_hc_known"].append({"name": name, "bytes": n, "seed": seed, "bid": bid, "stream_checksum": sck,
+                                        "block_checksum": bck, "size": len(f), "xxh32": xxh(f),
+                                        "content_xxh32": xxh(data)})
 
 
 def bd_main(manifest):
@@ -356,6 +418,7 @@ def main():
                 manifest["hc_blocks"].append({"input": name, "n": len(blk), "cap": cap, "level": level, "ret": r,
                                               "sha1": hashlib.sha1(dst.raw[:r]).hexdigest()})
     bd_main(manifest)
+    bd_hc_main(manifest)
     json.dump(manifest, open(os.path.join(HERE, "golden.json"), "w"), indent=0)
     print("frames", len(manifest["frames"]), "blocks", len(manifest["blocks"]), "decode", len(manifest["decode"]),
           "crafted", len(manifest["crafted"]), "cli mismatches",

@@ -223,6 +223,56 @@ def test_reference_bd_compress_defect_at_1mib_blocks():
     assert G.bd_decode_reference(G.bd_frame_contiguous(data, 6, False, True)) == data
 
 
+def test_bd_hc_oracle_vs_golden(golden):
+    """-BD at level >= 3 (the legacy HC stream, src/lz4mt.cpp:295-332,
+    460-538): the oracle's restatement against the frames liblz4 1.9.3 wrote
+    with the reference's call sequence (tests/golden/make_golden.py)."""
+    from conftest import bd_data, bd_input
+    for f in golden["bd_hc_frames"]:
+        data = bd_data(f)
+        got = oracle.bd_hc_frame(data, f["bid"], f["stream_checksum"], f["block_checksum"])
+        assert got == read_golden(f["file"]), f["name"]
+        r, out = oracle.decompress_frame(got, len(data) + (1 << 20))
+        assert r == 0 and out == data, f["name"]
+    for f in golden["bd_hc_known"]:
+        got = oracle.bd_hc_frame(bd_input(f["bytes"], f["seed"]), f["bid"], f["stream_checksum"], f["block_checksum"])
+        assert (len(got), xxhash.xxh32(got).intdigest()) == (f["size"], f["xxh32"]), f["name"]
+
+
+@pytest.mark.skipif(not os.path.exists(LIBLZ4), reason="liblz4 not present")
+def test_bd_hc_differential_vs_liblz4():
+    """The HC stream replayed on liblz4 (make_golden.bd_hc_frame_reference)
+    against the oracle on random sizes around the segment boundaries."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_golden as G
+    from conftest import bd_input
+    rnd = random.Random(11)
+    for i in range(10):
+        bid = rnd.choice([4, 4, 5, 6])
+        bm = 1 << (8 + 2 * bid)
+        n = rnd.choice([bm * 17 + rnd.randrange(bm), bm * 4 + 1, rnd.randrange(1, 3 * bm), 1_200_000])
+        data = _hc_mixed(n, i) if i % 2 else bd_input(n, 100 + i)
+        want = G.bd_hc_frame_reference(data, bid, bool(i & 1), bool(i & 2))
+        assert oracle.bd_hc_frame(data, bid, bool(i & 1), bool(i & 2)) == want, (i, bid, n)
+
+
+def test_bd_hc_large_blocks_are_independent_hc9():
+    """1 and 4 MiB blocks fill the HC stream's buffer alone: every block is a
+    fresh level-9 parse with cap = inSize - 1, whatever the level asked."""
+    from conftest import bd_input
+    data = bd_input(2_500_000, 3)
+    f = oracle.bd_hc_frame(data, 6, False, False)
+    pos = 7
+    for off in range(0, len(data), 1 << 20):
+        blk = data[off:off + (1 << 20)]
+        w = int.from_bytes(f[pos:pos + 4], "little")
+        c = oracle.compress_block_hc(blk, len(blk) - 1, 9)
+        assert (w & 0x7FFFFFFF) == (len(c) if c else len(blk)) and bool(w >> 31) == (not c)
+        assert f[pos + 4:pos + 4 + (w & 0x7FFFFFFF)] == (c or blk)
+        pos += 4 + (w & 0x7FFFFFFF)
+
+
 # ---------------------------------------------------------------------------
 # LZ4-HC 1.9.3 (levels 3..9): the reference's codec for compression levels >= 3
 # ---------------------------------------------------------------------------
