@@ -131,10 +131,15 @@ def cpu_baseline(mib, block_id, sck, level=0, bd=False):
     if bd:
         if not lz:
             return None   # the stream API comes from liblz4 only
-        tc, td, _ = oracle.bd_roundtrip(buf, n, block_id, sck, not sck, lz[2])
+        if level >= 3:
+            mib = min(mib, 64)   # ~30 MB/s: a bounded sample
+        tc, td, _ = oracle.bd_roundtrip(buf, mib << 20, block_id, sck, not sck, lz[2], hc=level >= 3)
+        n = mib << 20
+        how = ("one HC stream at level 9 (LZ4_compress_HC_continue" if level >= 3 else
+               "one LZ4 stream (LZ4_compress_fast_continue")
         line.update({"value": round(n / GiB / (tc + td), 3), "cores": 1, "codec": f"liblz4 {lz[1]}",
-                     "sample": f"{mib} MiB App.F synthetic, B{block_id} {flags}: one LZ4 stream "
-                               f"(LZ4_compress_fast_continue, cap n-1; LZ4_decompress_safe_usingDict), block/stream "
+                     "sample": f"{mib} MiB App.F synthetic, B{block_id} {flags}: {how}, cap n-1; "
+                               f"LZ4_decompress_safe_usingDict), block/stream "
                                f"XXH32, single thread as the reference's -BD path",
                      "compress_GiBps": round(n / GiB / tc, 3), "decompress_GiBps": round(n / GiB / td, 3)})
         return line
@@ -329,7 +334,8 @@ def main():
     body = frame_len - 7 - 4 - (4 if sck else 0)
     alg = n + body                           # algorithmic bytes per launch: in + out
     # the kernels the timing marks bracket in this mode
-    enc_k = ("k_encode_linked_round" if a.block_dependent else "k_encode_hc" if a.level >= 3 else "k_encode")
+    enc_k = ("k_encode_hc_bd" if a.block_dependent and a.level >= 3 else "k_encode_linked_round"
+             if a.block_dependent else "k_encode_hc" if a.level >= 3 else "k_encode")
     dec_k = "k_decode_linked" if a.block_dependent else "k_decode"
     roof = dec_roof = None
     if enc_avg:
@@ -337,7 +343,9 @@ def main():
         tr, why = pmc_traffic(enc_k, n, bm, flg)
         roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBPS, 5), "traffic": round(tr["bytes"]) if tr else None,
-                "kernel": enc_k + (" (+ k_link_settle rounds, serial fallback)" if a.block_dependent else ""),
+                "kernel": enc_k + (" (+ k_hc_prev_seg)" if a.block_dependent and a.level >= 3 else
+                                   " (+ k_link_settle rounds, serial fallback)" if a.block_dependent else
+                                   " (+ k_hc_prev)" if a.level >= 3 else ""),
                 "kernel_ms": round(enc_avg, 3), "algorithmic_bytes": alg,
                 "traffic_detail": tr or why}
     if dec_avg:

@@ -43,6 +43,7 @@ struct LinkState {
     // level >= 3: the HC stream's segments (hc_bd_pack's layout on the device)
     const uint8_t* hcSegs = nullptr;
     uint32_t nSeg = 0;
+    bool hcPerBlock = false;   // every block starts its own segment (1 / 4 MiB blocks)
 };
 
 // Frame-walk summary written by the walk kernel.
@@ -119,9 +120,14 @@ hipError_t launch_decode_stats(const uint8_t* frame, const BlockRec* recs, uint3
 hipError_t launch_gen_synthetic(uint8_t* dst, uint64_t n, uint64_t seed, hipStream_t st);
 // LZ4-HC (lz4mt_hc.hip): level 1..9 (lz4 1.9.3 hash chain); `delta` is
 // scratch of 2 bytes per input byte.  hipErrorInvalidValue for levels > 9.
+// capOverride: 0xFFFFFFFF = n (lz4mt), 0xFFFFFFFE = n - 1 (-BD), else the cap.
+// splitWs (hc_split_bytes, or null): blocks of at least 2 x hc_split_sub()
+// bytes are parsed by several waves and spliced (slotStride >= blockSize).
 hipError_t launch_encode_hc(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                             uint8_t* slots, uint64_t slotStride, uint32_t capOverride, int level, uint16_t* delta,
-                            int32_t* csize, hipStream_t st);
+                            int32_t* csize, hipStream_t st, uint8_t* splitWs = nullptr);
+uint32_t hc_split_sub();
+uint64_t hc_split_bytes(uint64_t nBlocks, uint32_t blockSize);
 uint32_t hc_attempts(int level);   // 0 for levels the library does not run (10..12)
 // -BD at level >= 3: segments [begin[k], end[k]) of src (begin >= -64 KiB),
 // blockSeg[b] = block b's segment; delta0 = chain scratch for src[0], with

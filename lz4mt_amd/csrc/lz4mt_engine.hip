@@ -58,6 +58,7 @@ thread_local Timing g_timing;
 struct CompressWs {
     uint8_t* slots;
     uint16_t* delta;   // LZ4-HC hash chain (level >= 3 only)
+    uint8_t* hcSplit;  // LZ4-HC split-parse records (level >= 3, large blocks)
     int32_t* csize;
     uint32_t* bsum;
     uint64_t* recOff;
@@ -73,6 +74,8 @@ CompressWs carve_compress(uint8_t* base, uint64_t nb, uint64_t bm, int level = 0
     w.slots = take(nb * bm + 64);
     // (-BD: 64 Ki entries more, for a segment that starts in the history before src)
     w.delta = level >= 3 ? reinterpret_cast<uint16_t*>(take((nb * bm + 65536) * 2 + 64)) : nullptr;
+    const uint64_t hs = level >= 3 ? hc_split_bytes(nb, (uint32_t)bm) : 0;
+    w.hcSplit = hs ? take(hs) : nullptr;
     w.csize = reinterpret_cast<int32_t*>(take((nb + 1) * 4));
     w.bsum = reinterpret_cast<uint32_t*>(take((nb + 1) * 4));
     w.recOff = reinterpret_cast<uint64_t*>(take((nb + 1) * 8));
@@ -323,7 +326,9 @@ Lz4MtResult device_compress_body(const uint8_t* src, uint64_t n, uint32_t bm, in
     const uint64_t nb = (n + bm - 1) / bm;
     CompressWs w = carve_compress(ws, nb, bm, level);
     g_timing.mark(0, st);
-    if (link && level >= 3) {   // block-dependent LZ4-HC: the stream's segments, a wave per block
+    if (link && level >= 3 && link->hcPerBlock) {   // -BD LZ4-HC, one segment per block: level 9, cap n - 1
+        HIPCHK(launch_encode_hc(src, n, bm, (uint32_t)nb, w.slots, bm, 0xFFFFFFFEu, 9, w.delta, w.csize, st, w.hcSplit));
+    } else if (link && level >= 3) {   // block-dependent LZ4-HC: the stream's segments, a wave per block
         const uint8_t* g = link->hcSegs;
         const uint32_t ns = link->nSeg;
         HIPCHK(launch_encode_hc_bd(src, n, bm, (uint32_t)nb, w.slots, reinterpret_cast<const int64_t*>(g),
@@ -337,7 +342,8 @@ Lz4MtResult device_compress_body(const uint8_t* src, uint64_t n, uint32_t bm, in
         HIPCHK(launch_encode_linked(src, n, bm, (uint32_t)nb, w.slots, link->plan, link->table, link->fresh, w.csize,
                                     st));
     else if (level >= 3)   // LZ4-HC, a wave per block (lz4mt_hc.hip)
-        HIPCHK(launch_encode_hc(src, n, bm, (uint32_t)nb, w.slots, bm, 0xFFFFFFFFu, level, w.delta, w.csize, st));
+        HIPCHK(launch_encode_hc(src, n, bm, (uint32_t)nb, w.slots, bm, 0xFFFFFFFFu, level, w.delta, w.csize, st,
+                                w.hcSplit));
     else
         HIPCHK(launch_encode(src, n, bm, (uint32_t)nb, w.slots, bm, 0xFFFFFFFFu, w.csize, st));
     g_timing.mark(1, st);
@@ -529,7 +535,7 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
         segAbs.assign(nb, 0);
         HcBdSim sim(sd->bd.blockMaximumSize);
         for (uint64_t b = 0; b < nb; ++b) segAbs[b] = sim.next((uint32_t)std::min<uint64_t>(bm, srcSize - b * bm));
-        ls.nSeg = hc_bd_pack(segAbs.data(), nb, 0, srcSize, 0, packed);
+        ls.nSeg = hc_bd_pack(segAbs.data(), nb, 0, srcSize, 0, packed, bm, &ls.hcPerBlock);
         if (!segBuf.ensure(packed.size() + 64)) return LZ4MT_RESULT_ERROR;
         if (!packed.empty())
             HIPCHK(hipMemcpyAsync(segBuf.p, packed.data(), packed.size(), hipMemcpyHostToDevice, st));

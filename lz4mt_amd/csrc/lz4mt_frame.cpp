@@ -563,7 +563,7 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
             memcpy(S.hIn, hist.data(), 65536);
             segAbs.resize(nb);
             for (uint64_t b = 0; b < nb; ++b) segAbs[b] = hsim.next((uint32_t)std::min<uint64_t>(bm, total - b * bm));
-            ls.nSeg = hc_bd_pack(segAbs.data(), nb, streamPos, total, 65536, packed);
+            ls.nSeg = hc_bd_pack(segAbs.data(), nb, streamPos, total, 65536, packed, bm, &ls.hcPerBlock);
             if (packed.size() + 64 > planCap * sizeof(LinkPlan)) {
                 if (dplan.p) { hipStreamSynchronize(S.st); hipFree(dplan.p); dplan.p = nullptr; }
                 planCap = (packed.size() + 64 + sizeof(LinkPlan) - 1) / sizeof(LinkPlan);

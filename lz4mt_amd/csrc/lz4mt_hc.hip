@@ -23,6 +23,13 @@
 //                candidate, with the candidate's bytes in the same round).
 #include "lz4mt_device.h"
 
+#include <stdlib.h>
+
+#include <stdio.h>
+
+#include <algorithm>
+#include <vector>
+
 namespace lz4mt {
 
 // Lanes of one wavefront hand data to each other through LDS.  LDS
@@ -325,21 +332,60 @@ __device__ bool hc_encode(g_cu8* s, g_u8* d, uint32_t& ip, uint32_t& op, uint32_
     return true;
 }
 
-// LZ4HC_compress_hashChain; 0 = does not fit cap (store raw)
-// The block is [start, B.n) of B.s (start > 0: the rest of a stream segment
-// before it, -BD at level >= 3).
-__device__ int32_t encode_block_hc(const HcBlock& B, g_u8* d, uint32_t cap, uint32_t start = 0) {
+// Loop-top hooks of a split parse (one block parsed by several waves, each
+// from its own start, spliced where two of them meet; see k_hc_heads).  At
+// the top of LZ4HC_compress_hashChain's main loop the whole parse state is
+// (ip, anchor, op): every later match decision depends on ip alone (the
+// searches take ip, never anchor, as their low limit) and anchor only sets
+// the literal run of the next sequence.  Two parses at a loop top with the
+// same ip and anchor == ip write the same bytes from there on.
+enum : uint32_t { kHcRun = 0, kHcEnd = 1, kHcSync = 2, kHcFail = 3 };
+struct HcState {
+    uint32_t ip, anchor, op, status, cnt;   // cnt: loop tops recorded (MODE 1)
+};
+struct HcHooks {
+    // MODE 1: record loop tops with anchor == ip (position, op) into hp / ho,
+    // stop after R of them or at ip >= hlim (a loop top), state saved
+    __attribute__((address_space(1))) uint32_t* hp;
+    __attribute__((address_space(1))) uint32_t* ho;
+    uint32_t R, hlim;
+    // MODE 2: from xlo on, stop at the first loop top with anchor == ip whose
+    // ip is in np[0 .. nR) (ascending); past np[nR - 1], fail
+    const __attribute__((address_space(1))) uint32_t* np;
+    uint32_t nR, xlo;
+};
+
+// LZ4HC_compress_hashChain from the loop-top state st; returns the state it
+// stops in.  MODE 0: to the block end (last literals; status kHcEnd, or
+// kHcFail when the output does not fit cap); 1 / 2: see HcHooks.
+template <int MODE>
+__device__ HcState hc_parse(const HcBlock& B, g_u8* d, uint32_t cap, bool limit, HcState st, const HcHooks& hk,
+                           bool fresh = false) {
     const uint32_t L = laneid();
     const uint32_t n = B.n;
-    const uint32_t blen = n - start;
     g_cu8* s = B.s;
-    const bool limit = (uint64_t)cap < (uint64_t)blen + blen / 255 + 16;
-    uint32_t ip = start, anchor = start, op = 0;
+    uint32_t ip = st.ip, anchor = st.anchor, op = st.op;
     const uint32_t mflimit = n >= 12 ? n - 12 : 0, matchlimit = n >= 5 ? n - 5 : 0;
     int ml0, ml, ml2, ml3;
     uint32_t start0 = 0, ref0 = 0, ref = 0, start2 = 0, ref2 = 0, start3 = 0, ref3 = 0;
-    if (blen < 13) goto last_literals;
+    uint32_t cnt = 0, k = 0, lastHead = 0;
+    if (MODE == 2) lastHead = hk.nR ? hk.np[hk.nR - 1] : 0u;
+    if (MODE == 0 && fresh && n - ip < 13) goto last_literals;   // inputSize < LZ4_minLength
     while (ip <= mflimit) {
+        if (MODE == 1) {
+            if (anchor == ip) {
+                if (L == 0) { hk.hp[cnt] = ip; hk.ho[cnt] = op; }
+                ++cnt;
+            }
+            if (cnt == hk.R || ip >= hk.hlim) return HcState{ip, anchor, op, kHcRun, cnt};
+        }
+        if (MODE == 2 && ip >= hk.xlo) {
+            if (ip > lastHead) return HcState{ip, anchor, op, kHcFail, cnt};
+            if (anchor == ip) {
+                while (hk.np[k] < ip) ++k;
+                if (hk.np[k] == ip) return HcState{ip, anchor, op, kHcSync};
+            }
+        }
         {
             uint32_t useless = ip;
             ml = B.wider(ip, ip, matchlimit, 3, &ref, &useless);
@@ -350,7 +396,7 @@ __device__ int32_t encode_block_hc(const HcBlock& B, g_u8* d, uint32_t cap, uint
         if (ip + (uint32_t)ml <= mflimit) ml2 = B.wider(ip + (uint32_t)ml - 2, ip, matchlimit, ml, &ref2, &start2);
         else ml2 = ml;
         if (ml2 == ml) {
-            if (!hc_encode(s, d, ip, op, anchor, ml, ref, limit, cap)) return 0;
+            if (!hc_encode(s, d, ip, op, anchor, ml, ref, limit, cap)) return HcState{ip, anchor, op, kHcFail, cnt};
             continue;
         }
         if (start0 < ip && start2 < ip + (uint32_t)ml0) { ip = start0; ref = ref0; ml = ml0; }
@@ -370,9 +416,9 @@ __device__ int32_t encode_block_hc(const HcBlock& B, g_u8* d, uint32_t cap, uint
         else ml3 = ml2;
         if (ml3 == ml2) {
             if (start2 < ip + (uint32_t)ml) ml = (int)(start2 - ip);
-            if (!hc_encode(s, d, ip, op, anchor, ml, ref, limit, cap)) return 0;
+            if (!hc_encode(s, d, ip, op, anchor, ml, ref, limit, cap)) return HcState{ip, anchor, op, kHcFail, cnt};
             ip = start2;
-            if (!hc_encode(s, d, ip, op, anchor, ml2, ref2, limit, cap)) return 0;
+            if (!hc_encode(s, d, ip, op, anchor, ml2, ref2, limit, cap)) return HcState{ip, anchor, op, kHcFail, cnt};
             continue;
         }
         if (start3 < ip + (uint32_t)ml + 3) {
@@ -382,7 +428,7 @@ __device__ int32_t encode_block_hc(const HcBlock& B, g_u8* d, uint32_t cap, uint
                     start2 += (uint32_t)corr; ref2 += (uint32_t)corr; ml2 -= corr;
                     if (ml2 < 4) { start2 = start3; ref2 = ref3; ml2 = ml3; }
                 }
-                if (!hc_encode(s, d, ip, op, anchor, ml, ref, limit, cap)) return 0;
+                if (!hc_encode(s, d, ip, op, anchor, ml, ref, limit, cap)) return HcState{ip, anchor, op, kHcFail, cnt};
                 ip = start3; ref = ref3; ml = ml3;
                 start0 = start2; ref0 = ref2; ml0 = ml2;
                 goto search2;
@@ -400,15 +446,17 @@ __device__ int32_t encode_block_hc(const HcBlock& B, g_u8* d, uint32_t cap, uint
                 ml = (int)(start2 - ip);
             }
         }
-        if (!hc_encode(s, d, ip, op, anchor, ml, ref, limit, cap)) return 0;
+        if (!hc_encode(s, d, ip, op, anchor, ml, ref, limit, cap)) return HcState{ip, anchor, op, kHcFail, cnt};
         ip = start2; ref = ref2; ml = ml2;
         start2 = start3; ref2 = ref3; ml2 = ml3;
         goto search3;
     }
+    if (MODE == 1) return HcState{ip, anchor, op, kHcRun, cnt};   // past mflimit: MODE 0 writes the last literals
+    if (MODE == 2) return HcState{ip, anchor, op, kHcFail, cnt};
 last_literals : {
     const uint32_t run = n - anchor;
     const uint32_t llAdd = (run + 255 - 15) / 255;
-    if (limit && (uint64_t)op + 1 + llAdd + run > cap) return 0;
+    if (limit && (uint64_t)op + 1 + llAdd + run > cap) return HcState{ip, anchor, op, kHcFail, cnt};
     uint32_t o = op;
     if (run >= 15) {
         if (L == 0) d[o] = (uint8_t)(15u << 4);
@@ -425,7 +473,23 @@ last_literals : {
         if (c + L < run) d[o + c + L] = s[anchor + c + L];
     op = o + run;
 }
-    return (int32_t)op;
+    return HcState{n, n, op, kHcEnd};
+}
+
+
+// LZ4HC_compress_hashChain over [start, B.n) of B.s (start > 0: the rest of
+// a stream segment before it, -BD at level >= 3); 0 = does not fit cap
+// (store raw)
+__device__ int32_t encode_block_hc(const HcBlock& B, g_u8* d, uint32_t cap, uint32_t start = 0) {
+    const uint32_t blen = B.n - start;
+    const bool limit = (uint64_t)cap < (uint64_t)blen + blen / 255 + 16;
+    const HcState r = hc_parse<0>(B, d, cap, limit, HcState{start, start, 0, 0, 0}, HcHooks{}, true);
+    return r.status == kHcEnd ? (int32_t)r.op : 0;
+}
+
+// cap of a block: capOverride, or n (0xFFFFFFFF, lz4mt) or n - 1 (0xFFFFFFFE, -BD)
+__device__ __forceinline__ uint32_t hc_cap(uint32_t n, uint32_t capOverride) {
+    return capOverride == 0xFFFFFFFFu ? n : capOverride == 0xFFFFFFFEu ? n - 1 : capOverride;
 }
 
 }  // namespace
@@ -434,14 +498,169 @@ __global__ void __launch_bounds__(64) k_encode_hc(const uint8_t* __restrict__ sr
                                                   uint32_t blockSize, uint8_t* __restrict__ slots,
                                                   uint64_t slotStride, uint32_t capOverride,
                                                   const uint16_t* __restrict__ delta, uint32_t maxAttempts,
-                                                  int32_t* __restrict__ csize) {
+                                                  int32_t* __restrict__ csize, const uint32_t* __restrict__ redo) {
     const uint32_t b = blockIdx.x;
+    if (redo && !redo[b]) return;   // done by the split parse
     const uint64_t off = (uint64_t)b * blockSize;
     const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
-    const uint32_t cap = capOverride == 0xFFFFFFFFu ? n : capOverride;   // lz4mt: cap = n
+    const uint32_t cap = hc_cap(n, capOverride);   // lz4mt: cap = n; -BD: n - 1
     HcBlock B{(g_cu8*)src + off, n, (g_cu16*)delta + off, maxAttempts, maxAttempts > 128};
     const int32_t r = encode_block_hc(B, (g_u8*)slots + (uint64_t)b * slotStride, cap);
     if (laneid() == 0) csize[b] = r;
+}
+
+// ---------------------------------------------------------------------------
+// Split parse of large blocks.  A 4 MiB block is one serial hashChain parse
+// (k_encode_hc: 2048 waves for 8 GiB, latency-bound); here stream j of a
+// block starts its own parse at M_j = j * sub (j = 0: the block start) and
+// the streams are spliced where they meet:
+//   k_hc_heads  stream j >= 1 parses from (M_j, M_j) until it has recorded
+//               kHcHeads loop tops with anchor == ip (position, output
+//               offset) or passed M_j + sub / 4; its state is kept.
+//   k_hc_exit   stream j resumes (j = 0 starts at 0) and, past M_{j+1},
+//               stops at its first loop top with anchor == ip at a position
+//               stream j+1 recorded: from there both parses are the same
+//               (hc_parse's note), so the block is stream 0 up to that
+//               point, stream 1 from it, ...  The last stream runs to the
+//               block end.
+//   k_hc_join   per block: checks the chain of meeting points (each at or
+//               after the previous one, where the stream is exact), sums
+//               the pieces (raw iff the total exceeds cap: every
+//               limitedOutput check of lz4hc implies it) and compacts them
+//               in the slot; a block that did not meet is re-run whole by
+//               k_encode_hc (flag).
+// Stream j writes at slot + M_j, capped at its region [M_j, M_{j+1}).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kHcHeads = 64;
+
+struct HcSplitWs {
+    uint32_t* hp;      // streams x kHcHeads
+    uint32_t* ho;
+    HcState* st1;      // after k_hc_heads
+    HcState* st2;      // after k_hc_exit
+    uint32_t* redo;    // per block: 1 = run k_encode_hc on it
+};
+
+__device__ __forceinline__ uint32_t hc_streams(uint32_t n, uint32_t sub) { return n >= 2 * sub ? n / sub : 1u; }
+
+
+__global__ void __launch_bounds__(64) k_hc_heads(const uint8_t* __restrict__ src, uint64_t srcSize, uint32_t blockSize,
+                                                 uint8_t* __restrict__ slots, uint64_t slotStride,
+                                                 const uint16_t* __restrict__ delta, uint32_t maxAttempts,
+                                                 uint32_t sub, uint32_t smax, HcSplitWs w) {
+    const uint32_t id = blockIdx.x, b = id / smax, j = id % smax;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
+    const uint32_t S = hc_streams(n, sub);
+    if (j == 0 || j >= S) return;
+    const uint32_t M = j * sub, end = j + 1 < S ? M + sub : n;
+    HcBlock B{(g_cu8*)src + off, n, (g_cu16*)delta + off, maxAttempts, maxAttempts > 128};
+    HcHooks hk{};
+    hk.hp = (__attribute__((address_space(1))) uint32_t*)w.hp + (uint64_t)id * kHcHeads;
+    hk.ho = (__attribute__((address_space(1))) uint32_t*)w.ho + (uint64_t)id * kHcHeads;
+    hk.R = kHcHeads;
+    hk.hlim = M + sub / 4;
+    const HcState r = hc_parse<1>(B, (g_u8*)slots + (uint64_t)b * slotStride + M, end - M, true,
+                                  HcState{M, M, 0, 0, 0}, hk);
+    if (laneid() == 0) w.st1[id] = r;
+}
+
+__global__ void __launch_bounds__(64) k_hc_exit(const uint8_t* __restrict__ src, uint64_t srcSize, uint32_t blockSize,
+                                                uint8_t* __restrict__ slots, uint64_t slotStride,
+                                                const uint16_t* __restrict__ delta, uint32_t maxAttempts,
+                                                uint32_t sub, uint32_t smax, HcSplitWs w) {
+    const uint32_t id = blockIdx.x, b = id / smax, j = id % smax;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
+    const uint32_t S = hc_streams(n, sub);
+    if (S == 1 || j >= S) return;
+    const uint32_t M = j * sub, end = j + 1 < S ? M + sub : n;
+    HcState st = j ? w.st1[id] : HcState{0, 0, 0, kHcRun, 0};
+    st.ip = uni(st.ip); st.anchor = uni(st.anchor); st.op = uni(st.op); st.status = uni(st.status);
+    HcState r = st;
+    if (st.status == kHcRun) {
+        HcBlock B{(g_cu8*)src + off, n, (g_cu16*)delta + off, maxAttempts, maxAttempts > 128};
+        g_u8* d = (g_u8*)slots + (uint64_t)b * slotStride + M;
+        if (j + 1 < S) {
+            const HcState nx = w.st1[id + 1];
+            HcHooks hk{};
+            hk.np = (const __attribute__((address_space(1))) uint32_t*)w.hp + (uint64_t)(id + 1) * kHcHeads;
+            hk.nR = nx.status == kHcFail ? 0u : uni(nx.cnt);
+            hk.xlo = M + sub;
+            r = hc_parse<2>(B, d, end - M, true, st, hk);
+        } else {
+            r = hc_parse<0>(B, d, end - M, true, st, HcHooks{});
+        }
+    }
+    if (laneid() == 0) w.st2[id] = r;
+}
+
+// one workgroup (256 threads) per block
+__global__ void __launch_bounds__(256) k_hc_join(uint64_t srcSize, uint32_t blockSize, uint8_t* __restrict__ slots,
+                                                 uint64_t slotStride, uint32_t capOverride, uint32_t sub, uint32_t smax,
+                                                 HcSplitWs w, int32_t* __restrict__ csize) {
+    __shared__ uint32_t pieceSrc[64], pieceLen[64];
+    __shared__ uint32_t verdict;   // 0 ok, 1 redo, 2 raw
+    __shared__ uint32_t total;
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
+    const uint32_t S = hc_streams(n, sub);
+    if (S == 1) {   // not split: k_encode_hc parses it
+        if (t == 0) w.redo[b] = 1;
+        return;
+    }
+    if (t == 0) {
+        uint32_t v = S <= 64 ? 0u : 1u, F = 0, prevE = 0;
+        const uint64_t base = (uint64_t)b * smax;
+        for (uint32_t j = 0; j < S && v == 0; ++j) {
+            const HcState x = w.st2[base + j];
+            uint32_t from = 0;
+            if (j) {   // stream j's output offset at prevE, a loop top it recorded
+                const HcState h = w.st1[base + j];
+                const uint32_t* hp = w.hp + (base + j) * kHcHeads;
+                const uint32_t* ho = w.ho + (base + j) * kHcHeads;
+                uint32_t k = 0;
+                while (k < h.cnt && hp[k] < prevE) ++k;
+                if (h.status == kHcFail || k == h.cnt || hp[k] != prevE) { v = 1; break; }
+                from = ho[k];
+            }
+            const bool last = j + 1 == S;
+            if (last ? x.status != kHcEnd : (x.status != kHcSync || x.ip < prevE)) { v = 1; break; }
+            pieceSrc[j] = j * sub + from;
+            pieceLen[j] = x.op - from;
+            F += x.op - from;
+            prevE = x.ip;
+        }
+        if (v == 0 && F > hc_cap(n, capOverride)) v = 2;
+        verdict = v;
+        total = F;
+        w.redo[b] = v == 1;
+    }
+    __syncthreads();
+    if (verdict != 0) {
+        if (verdict == 2 && t == 0) csize[b] = 0;
+        return;
+    }
+    // compact the pieces in order (each destination at or before its source)
+    uint8_t* d = slots + (uint64_t)b * slotStride;
+    uint32_t dst = pieceLen[0];
+    for (uint32_t j = 1; j < S; ++j) {
+        const uint32_t ps = pieceSrc[j], len = pieceLen[j];
+        if (ps != dst) {
+            for (uint32_t c = 0; c < len; c += 256 * 16) {
+                uint8_t v[16];
+                const uint32_t x = c + 16 * t;
+                const uint32_t m = x < len ? min(16u, len - x) : 0u;
+                for (uint32_t q = 0; q < m; ++q) v[q] = d[ps + x + q];
+                __syncthreads();
+                for (uint32_t q = 0; q < m; ++q) d[dst + x + q] = v[q];
+                __syncthreads();
+            }
+        }
+        dst += len;
+    }
+    if (t == 0) csize[b] = (int32_t)total;
 }
 
 // -BD at level >= 3 (compressBlockDependency with the HC stream, reference
@@ -484,15 +703,68 @@ uint32_t hc_attempts(int level) {
     return level > 9 ? 0u : kA[level];
 }
 
+// stream length of the split parse (LZ4MT_AMD_HC_SUB_KIB, default 256; 0 = off)
+uint32_t hc_split_sub() {
+    const char* e = getenv("LZ4MT_AMD_HC_SUB_KIB");
+    const long k = e ? atol(e) : 256;
+    return k > 0 ? (uint32_t)std::max<long>(k, 64) << 10 : 0u;
+}
+
+static uint32_t hc_smax(uint32_t blockSize) {
+    const uint32_t sub = hc_split_sub();
+    return sub && blockSize >= 2 * sub ? blockSize / sub : 0u;
+}
+
+uint64_t hc_split_bytes(uint64_t nBlocks, uint32_t blockSize) {
+    const uint64_t sm = hc_smax(blockSize), streams = nBlocks * sm;
+    if (!sm) return 0;
+    return streams * (2 * kHcHeads * 4 + 2 * sizeof(HcState)) + (nBlocks + 1) * 4 + 256;
+}
+
+static HcSplitWs carve_split(uint8_t* p, uint64_t nBlocks, uint32_t blockSize) {
+    const uint64_t streams = nBlocks * hc_smax(blockSize);
+    HcSplitWs w;
+    w.hp = reinterpret_cast<uint32_t*>(p);
+    w.ho = w.hp + streams * kHcHeads;
+    w.st1 = reinterpret_cast<HcState*>(w.ho + streams * kHcHeads);
+    w.st2 = w.st1 + streams;
+    w.redo = reinterpret_cast<uint32_t*>(w.st2 + streams);
+    return w;
+}
+
 hipError_t launch_encode_hc(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                             uint8_t* slots, uint64_t slotStride, uint32_t capOverride, int level, uint16_t* delta,
-                            int32_t* csize, hipStream_t st) {
+                            int32_t* csize, hipStream_t st, uint8_t* splitWs) {
     const uint32_t att = hc_attempts(level);
     if (att == 0) return hipErrorInvalidValue;
     if (nBlocks == 0) return hipSuccess;
     hipLaunchKernelGGL(k_hc_prev, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, delta);
+    const uint32_t sm = hc_smax(blockSize), sub = hc_split_sub();
+    if (splitWs && sm && slotStride >= blockSize) {   // large blocks: split parse, whole-block re-run where it fails
+        const HcSplitWs w = carve_split(splitWs, nBlocks, blockSize);
+        const uint32_t grid = nBlocks * sm;
+        hipLaunchKernelGGL(k_hc_heads, dim3(grid), dim3(64), 0, st, src, srcSize, blockSize, slots, slotStride,
+                           (const uint16_t*)delta, att, sub, sm, w);
+        hipLaunchKernelGGL(k_hc_exit, dim3(grid), dim3(64), 0, st, src, srcSize, blockSize, slots, slotStride,
+                           (const uint16_t*)delta, att, sub, sm, w);
+        hipLaunchKernelGGL(k_hc_join, dim3(nBlocks), dim3(256), 0, st, srcSize, blockSize, slots, slotStride,
+                           capOverride, sub, sm, w, csize);
+        if (getenv("LZ4MT_AMD_HC_STATS")) {   // diagnostics: blocks the split parse left to k_encode_hc
+            std::vector<uint32_t> r(nBlocks);
+            if (hipMemcpyAsync(r.data(), w.redo, nBlocks * 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
+                hipStreamSynchronize(st) == hipSuccess) {
+                uint32_t c = 0;
+                for (uint32_t x : r) c += x;
+                fprintf(stderr, "[hc split] sub %u KiB, %u streams/block: %u of %u blocks re-run whole\n", sub >> 10,
+                        sm, c, nBlocks);
+            }
+        }
+        hipLaunchKernelGGL(k_encode_hc, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, slotStride,
+                           capOverride, (const uint16_t*)delta, att, csize, (const uint32_t*)w.redo);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_encode_hc, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, slotStride,
-                       capOverride, delta, att, csize);
+                       capOverride, (const uint16_t*)delta, att, csize, (const uint32_t*)nullptr);
     return hipGetLastError();
 }
 

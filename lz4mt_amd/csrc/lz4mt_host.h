@@ -249,7 +249,7 @@ struct HcBdSim {
 // relative to A; a begin before A - hist is clamped there: no match or chain
 // link reaches more than 64 KiB back) and blockSeg[nb] (uint32) into `out`.
 inline uint32_t hc_bd_pack(const uint64_t* segAbs, uint64_t nb, uint64_t A, uint64_t total, uint64_t hist,
-                           std::vector<uint8_t>& out) {
+                           std::vector<uint8_t>& out, uint64_t bm = 0, bool* perBlock = nullptr) {
     std::vector<int64_t> begin, end;
     std::vector<uint32_t> blockSeg(nb);
     for (uint64_t b = 0; b < nb; ++b) {
@@ -262,6 +262,11 @@ inline uint32_t hc_bd_pack(const uint64_t* segAbs, uint64_t nb, uint64_t A, uint
     }
     end.push_back((int64_t)total);
     const uint32_t nSeg = (uint32_t)begin.size();
+    if (perBlock) {   // segment k = block k: the blocks are independent level-9 parses (cap n - 1)
+        bool pb = nSeg == nb;
+        for (uint64_t k = 0; pb && k < nSeg; ++k) pb = begin[k] == (int64_t)(k * bm);
+        *perBlock = pb;
+    }
     out.resize(16 * (size_t)nSeg + 4 * nb);
     memcpy(out.data(), begin.data(), 8 * (size_t)nSeg);
     memcpy(out.data() + 8 * (size_t)nSeg, end.data(), 8 * (size_t)nSeg);

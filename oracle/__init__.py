@@ -55,7 +55,7 @@ def _load():
     lib.orc_bd_hc_body.argtypes = [u8p, sz, ctypes.c_int, ctypes.c_int, u8p]
     lib.orc_hc_codec_set.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.orc_bd_roundtrip.argtypes = [u8p, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
-                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(sz)]
     lib.orc_stream_known_answer.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(FrameParams),
                                             ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(KnownAnswer)]
@@ -199,16 +199,17 @@ def hc_codec(level, lz=None):
     return tramp, dec
 
 
-def bd_roundtrip(data_buf, n, block_max_id, stream_checksum, block_checksum, lz):
+def bd_roundtrip(data_buf, n, block_max_id, stream_checksum, block_checksum, lz, hc=False):
     """Single-thread -BD round trip over liblz4's stream API (the reference's
-    compressBlockDependency / decompressBlockDependency shape):
-    (compress_s, decompress_s, frame_bytes)."""
-    ptr = [ctypes.cast(getattr(lz, f), ctypes.c_void_p).value for f in
-           ("LZ4_createStream", "LZ4_freeStream", "LZ4_compress_fast_continue", "LZ4_decompress_safe_usingDict")]
+    compressBlockDependency / decompressBlockDependency shape; ``hc``: its
+    level >= 3 HC stream): (compress_s, decompress_s, frame_bytes)."""
+    names = (("LZ4_createStreamHC", "LZ4_freeStreamHC", "LZ4_compress_HC_continue") if hc else
+             ("LZ4_createStream", "LZ4_freeStream", "LZ4_compress_fast_continue")) + ("LZ4_decompress_safe_usingDict",)
+    ptr = [ctypes.cast(getattr(lz, f), ctypes.c_void_p).value for f in names]
     secs = (ctypes.c_double * 2)()
     fs = ctypes.c_size_t(0)
-    if lib.orc_bd_roundtrip(data_buf, n, block_max_id, int(stream_checksum), int(block_checksum), *ptr, secs,
-                            ctypes.byref(fs)) != 0:
+    if lib.orc_bd_roundtrip(data_buf, n, block_max_id, int(stream_checksum), int(block_checksum), *ptr, int(hc),
+                            secs, ctypes.byref(fs)) != 0:
         raise RuntimeError("-BD CPU round trip failed")
     return secs[0], secs[1], fs.value
 

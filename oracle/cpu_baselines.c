@@ -16,7 +16,9 @@
  *       -BD frames: compressBlockDependency / decompressBlockDependency
  *       (reference src/lz4mt.cpp:460-538, 737-845) are single-threaded; one
  *       LZ4 stream, LZ4_compress_fast_continue per block (cap = n - 1,
- *       acceleration 1), block / stream XXH32, then the blocks decoded in
+ *       acceleration 1; hc: an HC stream at its default level 9,
+ *       LZ4_compress_HC_continue, the reference's level >= 3 path
+ *       src/lz4mt.cpp:295-332), block / stream XXH32, then the blocks decoded in
  *       order against the 64 KiB before them (LZ4_decompress_safe_usingDict
  *       over the contiguous output).  The reference's 1088 KiB input buffer
  *       and its slides change which bytes the dictionary holds, not the
@@ -46,6 +48,7 @@ typedef void* (*lz_create_fn)(void);
 typedef int (*lz_free_fn)(void*);
 typedef int (*lz_cont_fn)(void* stream, const char* src, char* dst, int n, int cap, int accel);
 typedef int (*lz_dec_dict_fn)(const char* src, char* dst, int csize, int cap, const char* dict, int dictSize);
+typedef int (*lz_hc_cont_fn)(void* stream, const char* src, char* dst, int n, int cap);
 
 static double now_s(void) {
     struct timespec t;
@@ -55,11 +58,12 @@ static double now_s(void) {
 
 /* returns 0 on success (round trip verified), -1 on a decode or checksum error */
 int orc_bd_roundtrip(const uint8_t* src, size_t n, int blockMaxId, int sck, int bck, void* create, void* freefn,
-                     void* cont, void* decdict, double* secs, size_t* frameSize) {
+                     void* cont, void* decdict, int hc, double* secs, size_t* frameSize) {
     const size_t bm = (size_t)1 << (8 + 2 * blockMaxId), nb = (n + bm - 1) / bm;
     lz_create_fn cr = (lz_create_fn)create;
     lz_free_fn fr = (lz_free_fn)freefn;
     lz_cont_fn cf = (lz_cont_fn)cont;
+    lz_hc_cont_fn hf = (lz_hc_cont_fn)cont;
     lz_dec_dict_fn df = (lz_dec_dict_fn)decdict;
     if (!cr || !fr || !cf || !df) return -1;
     uint8_t* body = (uint8_t*)malloc(n + 16 * nb + 64);
@@ -77,7 +81,8 @@ int orc_bd_roundtrip(const uint8_t* src, size_t n, int blockMaxId, int sck, int 
     size_t pos = 0;
     for (size_t b = 0; b < nb; ++b) {
         const size_t off = b * bm, len = n - off < bm ? n - off : bm;
-        const int cs = cf(st, (const char*)src + off, (char*)body + pos, (int)len, (int)len - 1, 1);
+        const int cs = hc ? hf(st, (const char*)src + off, (char*)body + pos, (int)len, (int)len - 1)
+                          : cf(st, (const char*)src + off, (char*)body + pos, (int)len, (int)len - 1, 1);
         braw[b] = cs <= 0;
         blen[b] = cs > 0 ? cs : (int)len;
         if (cs <= 0) memcpy(body + pos, src + off, len);

@@ -114,7 +114,7 @@ int orc_pipeline_roundtrip_codec(const uint8_t* src, size_t n,
 void orc_hc_codec_set(void* fn, int level);
 int orc_hc_compress_tramp(const char* src, char* dst, int n, int cap);
 int orc_bd_roundtrip(const uint8_t* src, size_t n, int blockMaxId, int sck, int bck, void* create, void* freefn,
-                     void* cont, void* decdict, double* secs, size_t* frameSize);
+                     void* cont, void* decdict, int hc, double* secs, size_t* frameSize);
 
 /* ---- streamed known answers for large configs ------------------------- */
 typedef struct {

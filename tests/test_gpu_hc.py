@@ -147,3 +147,36 @@ def test_hc_256mib_properties():
         size = int.from_bytes(host(fr[recs[b]:recs[b] + 4]), "little")
         assert size == len(want) and host(fr[recs[b] + 4:recs[b] + 4 + size]) == want, b
     assert fr.numel() < 0.45 * n   # HC-9 compresses App. F input well below the fast parser's 1/2.025
+
+
+def _split_input(kind, n, seed):
+    if kind == "appf":
+        return oracle.gen_synthetic(n, seed)
+    if kind == "mixed":
+        return _mixed(n, seed)
+    if kind == "runs":   # long zero runs across the streams' starts, random between
+        rnd = random.Random(seed)
+        out = bytearray()
+        while len(out) < n:
+            out += bytes(rnd.randrange(100_000, 900_000)) + oracle.gen_random(rnd.randrange(10, 90_000), seed)
+        return bytes(out[:n])
+    if kind == "random":
+        return oracle.gen_random(n, seed)
+    return bd_input(n, seed)
+
+
+@pytest.mark.parametrize("sub", ["64", "256", "0"])
+@pytest.mark.parametrize("kind", ["appf", "mixed", "runs", "bd", "random"])
+def test_hc_split_parse_vs_oracle(monkeypatch, sub, kind):
+    """Blocks of >= 2 streams are parsed by one wave per stream and spliced
+    where the parses meet (lz4mt_hc.hip k_hc_heads / k_hc_exit / k_hc_join;
+    blocks that do not meet are re-run whole): the same bytes as the serial
+    parse at every stream length (LZ4MT_AMD_HC_SUB_KIB; 0 = no split)."""
+    monkeypatch.setenv("LZ4MT_AMD_HC_SUB_KIB", sub)
+    data = _split_input(kind, (9 << 20) + 4321, 3)
+    for bid, level in ((7, 9), (6, 5)):
+        want = hc_frame(data, bid, False, True, level)
+        fr = L.compress_frame(dev(data), L.make_sd(bid, False, True), level=level)
+        assert host(fr) == want, (sub, kind, bid, level)
+    out, r = L.decompress_frame(fr)
+    assert r == 0 and host(out) == data
