@@ -51,6 +51,7 @@ typedef const __attribute__((address_space(1))) uint16_t g_cu16;
 typedef __attribute__((address_space(1))) uint16_t g_u16;
 typedef __attribute__((address_space(3))) uint8_t l_u8;
 typedef __attribute__((address_space(3))) uint32_t l_u32;
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -76,44 +77,72 @@ __device__ __forceinline__ uint32_t hc_hash(uint32_t v) { return (v * 2654435761
 // k_hc_prev: delta[p] = p - (previous position with the same hash), 0 if
 // none within 65535, for p in [0, n - 4] (positions lz4hc may insert)
 // ---------------------------------------------------------------------------
-// one wave over the n bytes at s: dl[p] for p in [0, n - 4]
-__device__ void hc_prev_range(g_cu8* s, uint32_t n, g_u16* dl, l_u32* last, l_u8* dd) {
+// 16 bytes per lane of the 1 KiB chunk at c0 (0 past n): one dwordx4 load
+// when the source is 16-byte aligned, bytes at the segment's end
+__device__ __forceinline__ v4u hc_chunk_load(g_cu8* s, uint32_t n, uint32_t c0, bool al) {
+    const uint32_t x = c0 + 16 * laneid();
+    if (al && x + 16 <= n) return *(const __attribute__((address_space(1))) v4u*)(s + x);
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (uint32_t i = 0; i < 16; ++i)
+        if (x + i < n) w[i >> 2] |= (uint32_t)s[x + i] << (8 * (i & 3));
+    return (v4u){w[0], w[1], w[2], w[3]};
+}
+
+// one wave over the n bytes at s: dl[p] for p in [0, n - 4].  The source
+// goes through a 2 KiB LDS ring, one 1 KiB chunk (16 steps of 64
+// positions) at a time, the next chunk's load in flight during the current
+// one's steps.
+__device__ void hc_prev_range(g_cu8* s, uint32_t n, g_u16* dl, l_u32* last, l_u8* dd, l_u32* ring) {
     const uint32_t L = laneid();
     for (uint32_t i = L; i < (1u << kHashLog); i += 64) last[i] = 0;
-    WAVE_SYNC();
     if (n < 4) return;
     const uint32_t np = n - 3;   // positions with 4 readable bytes
-    for (uint32_t base = 0; base < np; base += 64) {
-        const uint32_t p = base + L;
-        const bool live = p < np;
-        const uint32_t h = live ? hc_hash(rd32(s + p)) : 0u;
-        // lanes sharing a hash: the group's earlier member is the predecessor
-        if (live) dd[h & 1023] = (uint8_t)L;
-        WAVE_SYNC();
-        const uint32_t sv = live ? dd[h & 1023] : L;
-        uint64_t pending = ballot(live && sv != L);
-        int pred = -1;
-        uint64_t gm = 1ull << L;
-        while (pending) {
-            const uint32_t leader = ffs64(pending);
-            const uint32_t key = rdlane(h, (int)leader);
-            const uint64_t m = ballot(live && h == key);
-            if ((m >> L) & 1) {
-                gm = m;
-                const uint64_t below = m & ((1ull << L) - 1ull);
-                pred = below ? 63 - __clzll((long long)below) : -1;
+    const bool al = ((uintptr_t)s & 15) == 0;
+    ((__attribute__((address_space(3))) v4u*)ring)[L] = hc_chunk_load(s, n, 0, al);
+    v4u nxt = hc_chunk_load(s, n, 1024, al);
+    WAVE_SYNC();
+    for (uint32_t c0 = 0; c0 < np; c0 += 1024) {
+        for (uint32_t k = 0; k < 16; ++k) {
+            const uint32_t base = c0 + 64 * k;
+            if (base >= np) break;
+            if (k == 15) {   // the last step reads 3 bytes of the next chunk
+                ((__attribute__((address_space(3))) v4u*)ring)[(((c0 + 1024) >> 4) + L) & 127] = nxt;
+                WAVE_SYNC();
             }
-            pending &= ~m;
+            const uint32_t p = base + L;
+            const bool live = p < np;
+            const uint32_t w = p >> 2;
+            const uint32_t word = __builtin_amdgcn_alignbyte(ring[(w + 1) & 511], ring[w & 511], p & 3);
+            const uint32_t h = live ? hc_hash(word) : 0u;
+            // lanes sharing a hash: the group's earlier member is the predecessor
+            if (live) dd[h & 1023] = (uint8_t)L;
+            WAVE_SYNC();
+            const uint32_t sv = live ? dd[h & 1023] : L;
+            uint64_t pending = ballot(live && sv != L);
+            int pred = -1;
+            uint64_t gm = 1ull << L;
+            while (pending) {
+                const uint32_t leader = ffs64(pending);
+                const uint32_t key = rdlane(h, (int)leader);
+                const uint64_t m = ballot(live && h == key);
+                if ((m >> L) & 1) {
+                    gm = m;
+                    const uint64_t below = m & ((1ull << L) - 1ull);
+                    pred = below ? 63 - __clzll((long long)below) : -1;
+                }
+                pending &= ~m;
+            }
+            if (live) {
+                uint32_t q1 = pred >= 0 ? base + (uint32_t)pred + 1 : last[h];   // position + 1 of the previous
+                const uint32_t d = (q1 && p + 1 - q1 <= kHcDist) ? p + 1 - q1 : 0u;
+                dl[p] = (uint16_t)d;
+            }
+            WAVE_SYNC();
+            // the group's last member records its position
+            if (live && !(gm & ~((2ull << L) - 1ull))) last[h] = p + 1;
+            WAVE_SYNC();
         }
-        if (live) {
-            uint32_t q1 = pred >= 0 ? base + (uint32_t)pred + 1 : last[h];   // position + 1 of the previous
-            const uint32_t d = (q1 && p + 1 - q1 <= kHcDist) ? p + 1 - q1 : 0u;
-            dl[p] = (uint16_t)d;
-        }
-        WAVE_SYNC();
-        // the group's last member records its position
-        if (live && !(gm & ~((2ull << L) - 1ull))) last[h] = p + 1;
-        WAVE_SYNC();
+        nxt = hc_chunk_load(s, n, c0 + 2048, al);
     }
 }
 
@@ -121,10 +150,11 @@ __global__ void __launch_bounds__(64) k_hc_prev(const uint8_t* __restrict__ src,
                                                 uint16_t* __restrict__ delta) {
     __shared__ uint32_t last[1u << kHashLog];   // position + 1 of the latest occurrence (0 = none)
     __shared__ uint8_t dd[1024];                // duplicate-hash detection inside a step
+    __shared__ __attribute__((aligned(16))) uint32_t ring[512];   // 2 KiB source ring
     const uint32_t b = blockIdx.x;
     const uint64_t off = (uint64_t)b * blockSize;
     const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
-    hc_prev_range((g_cu8*)src + off, n, (g_u16*)delta + off, (l_u32*)last, (l_u8*)dd);
+    hc_prev_range((g_cu8*)src + off, n, (g_u16*)delta + off, (l_u32*)last, (l_u8*)dd, (l_u32*)ring);
 }
 
 // -BD at level >= 3: the chain over each stream segment (the bytes between
@@ -134,9 +164,11 @@ __global__ void __launch_bounds__(64) k_hc_prev_seg(const uint8_t* __restrict__ 
                                                     const int64_t* __restrict__ end, uint16_t* __restrict__ delta0) {
     __shared__ uint32_t last[1u << kHashLog];
     __shared__ uint8_t dd[1024];
+    __shared__ __attribute__((aligned(16))) uint32_t ring[512];
     const uint32_t k = blockIdx.x;
     const int64_t b0 = begin[k];
-    hc_prev_range((g_cu8*)src + b0, (uint32_t)(end[k] - b0), (g_u16*)delta0 + b0, (l_u32*)last, (l_u8*)dd);
+    hc_prev_range((g_cu8*)src + b0, (uint32_t)(end[k] - b0), (g_u16*)delta0 + b0, (l_u32*)last, (l_u8*)dd,
+                  (l_u32*)ring);
 }
 
 // ---------------------------------------------------------------------------
