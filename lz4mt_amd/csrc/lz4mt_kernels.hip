@@ -20,6 +20,8 @@
 // while the parse state lives in wave-uniform registers.  The hash table
 // (16 KiB) and the decoder's history ring (16 KiB) sit in LDS.
 #include "lz4mt_device.h"
+#include <string.h>
+
 #include <algorithm>
 
 // LZ4MT_PART splits this file into two objects so each half gets its own
@@ -681,28 +683,47 @@ __device__ __forceinline__ uint32_t sff1(uint64_t m) { return m ? (uint32_t)__bu
 // SPLIT (byU16 only): positions in a u16 array and 8-bit tags in a u8
 // array (26 KiB of LDS in all: 6 waves per CU instead of 4); the marker
 // readback compares positions only (distinct per live lane).
-template <bool U16, bool SPLIT = false, bool LINK = false> struct V5Geo {
+// P17: the byU32 table in 3 bytes per entry (u16 + u8 arrays, 12 KiB): a
+// 17-bit position (mod 2^17) + a 7-bit tag, kept exact by a sweep every
+// 32 KiB (sweep_p17) so that every live entry lies within 96 KiB of ip.
+template <bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false> struct V5Geo {
     static constexpr uint32_t kTE = U16 ? 8192u : 4096u;
     // LINK: positions in the block-dependent coordinates (64 KiB of history
     // before the block) need one more bit: 23-bit positions, 9-bit tags
-    static constexpr uint32_t PB = U16 ? 16u : (LINK ? kPosBits + 1 : kPosBits);
+    static constexpr uint32_t PB = P17 ? 17u : U16 ? 16u : (LINK ? kPosBits + 1 : kPosBits);
     static constexpr uint32_t PM = (1u << PB) - 1u;
-    static constexpr uint32_t TB = SPLIT ? 8u : 32u - PB;   // tag bits
+    static constexpr bool SP = SPLIT || P17;                  // u16 + u8 storage
+    static constexpr uint32_t TB = P17 ? 7u : SPLIT ? 8u : 32u - PB;   // tag bits
     static __device__ __forceinline__ uint32_t tag(uint32_t w0) { return (w0 * 0x85EBCA77u) >> (32 - TB); }
     l_u32* T;
     __device__ __forceinline__ l_u16* T16() const { return (l_u16*)T; }
     __device__ __forceinline__ l_u8* TG() const { return (l_u8*)T + 2 * (kTE + 64); }
     __device__ __forceinline__ uint32_t ld(uint32_t i) const {
-        return SPLIT ? ((uint32_t)T16()[i] | ((uint32_t)TG()[i] << 16)) : T[i];
+        return SP ? ((uint32_t)T16()[i] | ((uint32_t)TG()[i] << 16)) : T[i];
     }
     __device__ __forceinline__ void st(uint32_t i, uint32_t e) const {
-        if (SPLIT) { T16()[i] = (uint16_t)e; TG()[i] = (uint8_t)(e >> 16); } else T[i] = e;
+        if (SP) { T16()[i] = (uint16_t)e; TG()[i] = (uint8_t)(e >> 16); } else T[i] = e;
     }
-    __device__ __forceinline__ uint32_t rb(uint32_t i) const { return SPLIT ? (uint32_t)T16()[i] : T[i]; }
-    static constexpr uint32_t kRbMask = SPLIT ? 0xFFFFu : 0xFFFFFFFFu;
+    __device__ __forceinline__ uint32_t rb(uint32_t i) const { return SP ? (uint32_t)T16()[i] : T[i]; }
+    static constexpr uint32_t kRbMask = SP ? 0xFFFFu : 0xFFFFFFFFu;
+    // P17: at T (a multiple of 32 KiB, every table write so far below T +
+    // 32 KiB, every live entry at or above T - 96 KiB): entries more than
+    // 64 KiB below T can never be a candidate again -- they become a marker
+    // (T + 64 KiB mod 2^17) that reads as out of range until the next sweep
+    // re-marks it.  Entries at or above T - 64 KiB (and those written ahead,
+    // at or above T) keep their distance (< 2^17) exact.
+    __device__ __forceinline__ void sweep(uint32_t Tp) const {
+        const uint32_t L = laneid();
+        const uint32_t mk = (Tp + 65536u) & PM;
+        for (uint32_t i = L; i < kTE; i += 64) {
+            const uint32_t d = (Tp - ld(i)) & PM;
+            if (d > 65536u && d <= 98304u) st(i, mk);
+        }
+        WAVE_SYNC();
+    }
     __device__ __forceinline__ void init(uint32_t e0) const {
         const uint32_t L = laneid();
-        if (SPLIT) {
+        if (SP) {
             const uint32_t p2 = (e0 & 0xFFFFu) * 0x10001u, t4 = (e0 >> 16) * 0x01010101u;
             for (uint32_t i = L; i < kTE / 8; i += 64) ((l_u4*)T16())[i] = (v4u){p2, p2, p2, p2};
             for (uint32_t i = L; i < kTE / 16; i += 64) ((l_u4*)TG())[i] = (v4u){t4, t4, t4, t4};
@@ -770,11 +791,11 @@ __device__ __forceinline__ void store_pend(const PendSeq& p, const SrcRing& V, g
 // positions in the coordinates of k_encode_linked (block at o0 = 65536, its
 // 64 KiB history below), the table carried in T unless lk.fresh, candidates
 // bounded by lk (see LinkArgs); n = o0 + block length.
-template <bool ST, bool U16, bool SPLIT = false, bool LINK = false>
+template <bool ST, bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false>
 __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
                                    l_u32* __restrict__ T, l_u8* __restrict__ R, uint64_t* acc,
                                    LinkArgs lk = LinkArgs{0, 0, 0, true}) {
-    using G = V5Geo<U16, SPLIT, LINK>;
+    using G = V5Geo<U16, SPLIT, LINK, P17>;
     const G tab{T};
     const uint32_t L = laneid();
     uint64_t ts = STAMP_T();
@@ -807,6 +828,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     // (0 continuation: search only; 1 after a match ending at sBase - 1:
     // INSERT sBase - 3, TEST sBase - 1; 2 first window: INSERT 0)
     uint32_t sBase = o0 + 1, k0 = 0, s0 = 1, j1 = 65, mode = 2;
+    uint32_t nextSweep = 32768;   // P17
     // ONE exit and no continue: the structurizer then needs no flow
     // variables and the loop-carried state stays in place across windows
     bool done = false, fail = false;
@@ -817,6 +839,12 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
       bool wTerm;
       do {
         if (ST) acc[10] += 1;
+        if (P17) {
+            while (sBase >= nextSweep) {   // (long matches cross several)
+                tab.sweep(nextSweep);
+                nextSweep += 32768;
+            }
+        }
         // ---- probe positions.  SEARCH lane L probes k = k0 + j (j = L - 2) at
         // sBase + j*s0 + max(0, j - j1): the step s0 = step(k0) rises by one at
         // most once inside a window (at j = j1; never in the k0 = 0 window)
@@ -848,7 +876,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         }
         const uint32_t w0 = (uint32_t)v8;
         const uint32_t h = lz4_hash<U16>(w0, (uint32_t)(v8 >> 32));
-        const uint32_t mark = p | (G::tag(w0) << G::PB);   // the lane's final table entry
+        const uint32_t mark = (P17 ? p & G::PM : p) | (G::tag(w0) << G::PB);   // the lane's final table entry
         // ---- table probe: read, write the marker, read back (LDS ops of a wave run in order)
         const uint32_t ti = live ? h : dumIdx;
         const uint32_t told = tab.ld(ti);
@@ -856,8 +884,10 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         WAVE_SYNC();
         const uint32_t sv = tab.rb(ti);
         const uint64_t pend = bal(sv != (mark & G::kRbMask));   // same-bucket collision inside the window
-        uint32_t cand = told & G::PM;
-        const bool cok = live && L != 0 && !term && cand + kDistMax >= p && (!LINK || cand >= lk.candLow);
+        const uint32_t dq = (p - told) & G::PM;   // P17: the distance, exact below 2^17
+        uint32_t cand = P17 ? p - dq : told & G::PM;
+        const bool cok = live && L != 0 && !term && (P17 ? dq <= kDistMax : cand + kDistMax >= p) &&
+                         (!LINK || cand >= lk.candLow);
         bool maybe = cok && (told >> G::PB) == (mark >> G::PB);
         const uint64_t tmk = bal(term);
         uint64_t mm = bal(maybe);
@@ -1087,6 +1117,26 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
         r = encode_block_v5<false, false>(s, n, d, cap, Tl, Xl, nullptr);
     else
         r = encode_block<false, false, false>(s, n, d, cap, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
+    if (laneid() == 0) csize[b] = r;
+}
+
+// The v5 encoder with the 3-byte table (V5Geo P17): 14.25 KiB of LDS, 11
+// waves per CU instead of 8.  Blocks of 65 547 B .. 4 MiB; others are left
+// to k_encode (csize untouched here).
+__global__ void __launch_bounds__(64) k_encode_p17(const uint8_t* __restrict__ src, uint64_t srcSize,
+                                                   uint32_t blockSize, uint8_t* __restrict__ slots,
+                                                   uint64_t slotStride, uint32_t capOverride,
+                                                   int32_t* __restrict__ csize) {
+    __shared__ __attribute__((aligned(16))) uint32_t PLDS[(2 * (4096 + 64) + (4096 + 64) + kSR + kSRMirror) / 4];
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
+    if (n < (uint32_t)kLimit64K || n > (1u << kPosBits)) return;
+    const uint32_t cap = (capOverride == 0xFFFFFFFFu) ? n : capOverride;   // lz4mt: cap = n
+    l_u8* Xl = (l_u8*)PLDS + 3 * (4096 + 64);
+    const int32_t r = encode_block_v5<false, false, false, false, true>(gptr(src) + off, n,
+                                                                        gptr(slots) + (uint64_t)b * slotStride, cap,
+                                                                        (l_u32*)PLDS, Xl, nullptr);
     if (laneid() == 0) csize[b] = r;
 }
 
@@ -1399,13 +1449,31 @@ hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32
     return hipGetLastError();
 }
 
+// k_encode_p17 for 256 KiB blocks (11 waves per CU pay for the split table
+// there: 161 -> 151 ms at 8 GiB; at 1 / 4 MiB blocks the 7-bit tags' extra
+// round trips cost more than the occupancy gains, profiles/r02_p17_ab.txt);
+// LZ4MT_AMD_ENC=p17 / base forces one (A/B)
+static bool enc_p17(uint32_t blockSize) {
+    const char* e = getenv("LZ4MT_AMD_ENC");
+    if (e && !strcmp(e, "p17")) return true;
+    if (e && !strcmp(e, "base")) return false;
+    return blockSize <= (256u << 10);
+}
+
 hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks, uint8_t* slots,
                          uint64_t slotStride, uint32_t capOverride, int32_t* csize, hipStream_t st) {
     if (nBlocks == 0) return hipSuccess;
     if (blockSize < (uint32_t)kLimit64K)
         hipLaunchKernelGGL(k_encode16, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, slotStride,
                            capOverride, csize);
-    else
+    else if (enc_p17(blockSize) && blockSize <= (1u << kPosBits)) {   // 3-byte table; a short last block on k_encode
+        hipLaunchKernelGGL(k_encode_p17, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, slotStride,
+                           capOverride, csize);
+        const uint64_t lastOff = (uint64_t)(nBlocks - 1) * blockSize;
+        if (srcSize - lastOff < (uint64_t)kLimit64K)
+            hipLaunchKernelGGL(k_encode, dim3(1), dim3(64), 0, st, src + lastOff, srcSize - lastOff, blockSize,
+                               slots + (nBlocks - 1) * slotStride, slotStride, capOverride, csize + (nBlocks - 1));
+    } else
         hipLaunchKernelGGL(k_encode, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, slotStride,
                            capOverride, csize);
     return hipGetLastError();
