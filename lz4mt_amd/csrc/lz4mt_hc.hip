@@ -77,10 +77,12 @@ __device__ __forceinline__ uint32_t hc_hash(uint32_t v) { return (v * 2654435761
 // k_hc_prev: delta[p] = p - (previous position with the same hash), 0 if
 // none within 65535, for p in [0, n - 4] (positions lz4hc may insert)
 // ---------------------------------------------------------------------------
-// 16 bytes per lane of the 1 KiB chunk at c0 (0 past n): one dwordx4 load
+constexpr uint32_t kPrevThreads = 256;   // 4 waves share one last-position table
+
+// 16 bytes per thread of the 4 KiB chunk at c0 (0 past n): one dwordx4 load
 // when the source is 16-byte aligned, bytes at the segment's end
 __device__ __forceinline__ v4u hc_chunk_load(g_cu8* s, uint32_t n, uint32_t c0, bool al) {
-    const uint32_t x = c0 + 16 * laneid();
+    const uint32_t x = c0 + 16 * threadIdx.x;
     if (al && x + 16 <= n) return *(const __attribute__((address_space(1))) v4u*)(s + x);
     uint32_t w[4] = {0, 0, 0, 0};
     for (uint32_t i = 0; i < 16; ++i)
@@ -88,36 +90,41 @@ __device__ __forceinline__ v4u hc_chunk_load(g_cu8* s, uint32_t n, uint32_t c0, 
     return (v4u){w[0], w[1], w[2], w[3]};
 }
 
-// one wave over the n bytes at s: dl[p] for p in [0, n - 4].  The source
-// goes through a 2 KiB LDS ring, one 1 KiB chunk (16 steps of 64
-// positions) at a time, the next chunk's load in flight during the current
-// one's steps.
+// One workgroup (4 waves) over the n bytes at s: dl[p] for p in [0, n - 4].
+// Steps of 256 positions, wave w taking positions 64w .. 64w + 63 of the
+// step: equal hashes inside a wave are resolved by ballot (the group's
+// earlier member is the predecessor, its last member records its position);
+// the waves then read / update the last-position table in wave order, so a
+// position without a predecessor in its own wave sees the earlier waves'
+// positions.  The source goes through an 8 KiB LDS ring, one 4 KiB chunk
+// (16 steps) at a time, the next chunk's load in flight meanwhile.
 __device__ void hc_prev_range(g_cu8* s, uint32_t n, g_u16* dl, l_u32* last, l_u8* dd, l_u32* ring) {
-    const uint32_t L = laneid();
-    for (uint32_t i = L; i < (1u << kHashLog); i += 64) last[i] = 0;
+    const uint32_t t = threadIdx.x, L = laneid(), wv = t >> 6;
+    for (uint32_t i = t; i < (1u << kHashLog); i += kPrevThreads) last[i] = 0;
     if (n < 4) return;
     const uint32_t np = n - 3;   // positions with 4 readable bytes
     const bool al = ((uintptr_t)s & 15) == 0;
-    ((__attribute__((address_space(3))) v4u*)ring)[L] = hc_chunk_load(s, n, 0, al);
-    v4u nxt = hc_chunk_load(s, n, 1024, al);
-    WAVE_SYNC();
-    for (uint32_t c0 = 0; c0 < np; c0 += 1024) {
+    typedef __attribute__((address_space(3))) v4u l_v4u;
+    ((l_v4u*)ring)[t] = hc_chunk_load(s, n, 0, al);
+    v4u nxt = hc_chunk_load(s, n, 4096, al);
+    l_u8* ddw = dd + 1024 * wv;
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < np; c0 += 4096) {
         for (uint32_t k = 0; k < 16; ++k) {
-            const uint32_t base = c0 + 64 * k;
+            const uint32_t base = c0 + 256 * k;
             if (base >= np) break;
             if (k == 15) {   // the last step reads 3 bytes of the next chunk
-                ((__attribute__((address_space(3))) v4u*)ring)[(((c0 + 1024) >> 4) + L) & 127] = nxt;
-                WAVE_SYNC();
+                ((l_v4u*)ring)[(((c0 + 4096) >> 4) + t) & 511] = nxt;
+                __syncthreads();
             }
-            const uint32_t p = base + L;
+            const uint32_t p = base + t;
             const bool live = p < np;
             const uint32_t w = p >> 2;
-            const uint32_t word = __builtin_amdgcn_alignbyte(ring[(w + 1) & 511], ring[w & 511], p & 3);
+            const uint32_t word = __builtin_amdgcn_alignbyte(ring[(w + 1) & 2047], ring[w & 2047], p & 3);
             const uint32_t h = live ? hc_hash(word) : 0u;
-            // lanes sharing a hash: the group's earlier member is the predecessor
-            if (live) dd[h & 1023] = (uint8_t)L;
+            if (live) ddw[h & 1023] = (uint8_t)L;
             WAVE_SYNC();
-            const uint32_t sv = live ? dd[h & 1023] : L;
+            const uint32_t sv = live ? ddw[h & 1023] : L;
             uint64_t pending = ballot(live && sv != L);
             int pred = -1;
             uint64_t gm = 1ull << L;
@@ -132,25 +139,27 @@ __device__ void hc_prev_range(g_cu8* s, uint32_t n, g_u16* dl, l_u32* last, l_u8
                 }
                 pending &= ~m;
             }
-            if (live) {
-                uint32_t q1 = pred >= 0 ? base + (uint32_t)pred + 1 : last[h];   // position + 1 of the previous
-                const uint32_t d = (q1 && p + 1 - q1 <= kHcDist) ? p + 1 - q1 : 0u;
-                dl[p] = (uint16_t)d;
+            const bool groupLast = live && !(gm & ~((2ull << L) - 1ull));
+            uint32_t q1 = pred >= 0 ? base + 64 * wv + (uint32_t)pred + 1 : 0u;   // position + 1 of the previous
+            for (uint32_t u = 0; u < kPrevThreads / 64; ++u) {
+                if (wv == u) {
+                    if (live && pred < 0) q1 = last[h];
+                    WAVE_SYNC();
+                    if (groupLast) last[h] = p + 1;
+                }
+                __syncthreads();
             }
-            WAVE_SYNC();
-            // the group's last member records its position
-            if (live && !(gm & ~((2ull << L) - 1ull))) last[h] = p + 1;
-            WAVE_SYNC();
+            if (live) dl[p] = (uint16_t)((q1 && p + 1 - q1 <= kHcDist) ? p + 1 - q1 : 0u);
         }
-        nxt = hc_chunk_load(s, n, c0 + 2048, al);
+        nxt = hc_chunk_load(s, n, c0 + 8192, al);
     }
 }
 
-__global__ void __launch_bounds__(64) k_hc_prev(const uint8_t* __restrict__ src, uint64_t srcSize, uint32_t blockSize,
-                                                uint16_t* __restrict__ delta) {
+__global__ void __launch_bounds__(kPrevThreads) k_hc_prev(const uint8_t* __restrict__ src, uint64_t srcSize,
+                                                          uint32_t blockSize, uint16_t* __restrict__ delta) {
     __shared__ uint32_t last[1u << kHashLog];   // position + 1 of the latest occurrence (0 = none)
-    __shared__ uint8_t dd[1024];                // duplicate-hash detection inside a step
-    __shared__ __attribute__((aligned(16))) uint32_t ring[512];   // 2 KiB source ring
+    __shared__ uint8_t dd[4 * 1024];            // duplicate-hash detection inside a wave's step
+    __shared__ __attribute__((aligned(16))) uint32_t ring[2048];   // 8 KiB source ring
     const uint32_t b = blockIdx.x;
     const uint64_t off = (uint64_t)b * blockSize;
     const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
@@ -160,11 +169,13 @@ __global__ void __launch_bounds__(64) k_hc_prev(const uint8_t* __restrict__ src,
 // -BD at level >= 3: the chain over each stream segment (the bytes between
 // two resets of the reference's HC stream), segment k = src[begin, end)
 // (begin may lie up to 64 KiB before src: the previous batch's history)
-__global__ void __launch_bounds__(64) k_hc_prev_seg(const uint8_t* __restrict__ src, const int64_t* __restrict__ begin,
-                                                    const int64_t* __restrict__ end, uint16_t* __restrict__ delta0) {
+__global__ void __launch_bounds__(kPrevThreads) k_hc_prev_seg(const uint8_t* __restrict__ src,
+                                                              const int64_t* __restrict__ begin,
+                                                              const int64_t* __restrict__ end,
+                                                              uint16_t* __restrict__ delta0) {
     __shared__ uint32_t last[1u << kHashLog];
-    __shared__ uint8_t dd[1024];
-    __shared__ __attribute__((aligned(16))) uint32_t ring[512];
+    __shared__ uint8_t dd[4 * 1024];
+    __shared__ __attribute__((aligned(16))) uint32_t ring[2048];
     const uint32_t k = blockIdx.x;
     const int64_t b0 = begin[k];
     hc_prev_range((g_cu8*)src + b0, (uint32_t)(end[k] - b0), (g_u16*)delta0 + b0, (l_u32*)last, (l_u8*)dd,
@@ -722,7 +733,7 @@ hipError_t launch_encode_hc_bd(const uint8_t* src, uint64_t srcSize, uint32_t bl
                                uint8_t* slots, const int64_t* segBegin, const int64_t* segEnd, uint32_t nSeg,
                                const uint32_t* blockSeg, uint16_t* delta0, int32_t* csize, hipStream_t st) {
     if (nBlocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hc_prev_seg, dim3(nSeg), dim3(64), 0, st, src, segBegin, segEnd, delta0);
+    hipLaunchKernelGGL(k_hc_prev_seg, dim3(nSeg), dim3(kPrevThreads), 0, st, src, segBegin, segEnd, delta0);
     hipLaunchKernelGGL(k_encode_hc_bd, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, segBegin,
                        blockSeg, (const uint16_t*)delta0, csize);
     return hipGetLastError();
@@ -770,7 +781,7 @@ hipError_t launch_encode_hc(const uint8_t* src, uint64_t srcSize, uint32_t block
     const uint32_t att = hc_attempts(level);
     if (att == 0) return hipErrorInvalidValue;
     if (nBlocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hc_prev, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, delta);
+    hipLaunchKernelGGL(k_hc_prev, dim3(nBlocks), dim3(kPrevThreads), 0, st, src, srcSize, blockSize, delta);
     const uint32_t sm = hc_smax(blockSize), sub = hc_split_sub();
     if (splitWs && sm && slotStride >= blockSize) {   // large blocks: split parse, whole-block re-run where it fails
         const HcSplitWs w = carve_split(splitWs, nBlocks, blockSize);
