@@ -100,6 +100,15 @@ struct BlockScratch {
     BlockRec* dRec = nullptr;
     uint16_t* dDelta = nullptr;   // LZ4-HC hash chain
     uint64_t capDelta = 0;
+    uint8_t* dSplit = nullptr;    // LZ4-HC split-parse records
+    uint64_t capSplit = 0;
+    bool ensure_split(uint64_t bytes) {
+        if (dSplit && bytes <= capSplit) return true;
+        hipFree(dSplit);
+        capSplit = std::max<uint64_t>(bytes, 64 << 10);
+        if (hipMalloc(&dSplit, capSplit) != hipSuccess) { dSplit = nullptr; capSplit = 0; return false; }
+        return true;
+    }
     int dev = -1;
     bool ensure_delta(uint64_t n) {
         if (dDelta && n <= capDelta) return true;
@@ -110,7 +119,7 @@ struct BlockScratch {
     }
     void release() {
         if (st) hipStreamSynchronize(st);
-        hipFree(dIn); hipFree(dOut); hipFree(dRes); hipFree(dRec); hipFree(dDelta);
+        hipFree(dIn); hipFree(dOut); hipFree(dRes); hipFree(dRec); hipFree(dDelta); hipFree(dSplit);
         if (st) hipStreamDestroy(st);
         *this = BlockScratch();
     }
@@ -414,13 +423,19 @@ extern "C" int lz4mtHipCompressBlock(const char* src, char* dst, int isize, int 
     ScratchLease g_blk;
     if (!g_blk->init()) return -1;
     const int bound = lz4mtHipCompressBound(isize);
-    const uint64_t outMax = (uint64_t)std::min(maxOutputSize, bound) + 16;
+    uint64_t outMax = (uint64_t)std::min(maxOutputSize, bound) + 16;
+    // LZ4-HC on a large block: the split parse (one wave per 256 KiB stream)
+    // writes each stream at its offset in an output of at least isize bytes
+    const uint64_t splitBytes = hc ? hc_split_bytes(1, (uint32_t)std::max(isize, 1)) : 0;
+    if (splitBytes) outMax = std::max<uint64_t>(outMax, (uint64_t)isize + 16);
     if (!g_blk->ensure((uint64_t)isize, outMax)) return -1;
     if (hc && !g_blk->ensure_delta((uint64_t)isize)) return -1;
+    if (splitBytes && !g_blk->ensure_split(splitBytes)) return -1;
     if (isize && hipMemcpyAsync(g_blk->dIn, src, (size_t)isize, hipMemcpyHostToDevice, g_blk->st) != hipSuccess) return -1;
     const hipError_t le = hc ? launch_encode_hc(g_blk->dIn, (uint64_t)isize, (uint32_t)std::max(isize, 1), 1, g_blk->dOut,
-                                                0, (uint32_t)maxOutputSize, compressionLevel, g_blk->dDelta,
-                                                g_blk->dRes, g_blk->st)
+                                                splitBytes ? (uint64_t)isize : 0, (uint32_t)maxOutputSize,
+                                                compressionLevel, g_blk->dDelta, g_blk->dRes, g_blk->st,
+                                                splitBytes ? g_blk->dSplit : nullptr)
                              : launch_encode(g_blk->dIn, (uint64_t)isize, (uint32_t)std::max(isize, 1), 1, g_blk->dOut,
                                              0, (uint32_t)maxOutputSize, g_blk->dRes, g_blk->st);
     if (le != hipSuccess) return -1;

@@ -180,3 +180,16 @@ def test_hc_split_parse_vs_oracle(monkeypatch, sub, kind):
         assert host(fr) == want, (sub, kind, bid, level)
     out, r = L.decompress_frame(fr)
     assert r == 0 and host(out) == data
+
+
+@pytest.mark.parametrize("kind", ["appf", "mixed", "random"])
+def test_hc_block_operator_split(kind):
+    """lz4mtHipCompressBlock on 1-4 MiB blocks runs the split parse too
+    (one wave per 256 KiB stream): the oracle's bytes at caps n, n - 1, a
+    tight cap and a cap past the bound."""
+    rnd = random.Random(len(kind))
+    for n in (4 << 20, (1 << 20) + 12345):
+        d = _split_input(kind, n, rnd.randrange(1000))
+        want_n = oracle.compress_block_hc(d, n, 9)
+        for cap in (n, n - 1, max(len(want_n), 1) - 1 if want_n else n // 2, n + n // 255 + 16):
+            assert L.compress_block(d, cap, level=9) == oracle.compress_block_hc(d, cap, 9), (kind, n, cap)
