@@ -1343,6 +1343,83 @@ __global__ void __launch_bounds__(256) k_link_settle(const uint32_t* __restrict_
     }
 }
 
+// Chained rounds (blocks of 256 KiB and less): one table guess per block
+// needs ~1-1.5 MiB of parse to be forgotten, i.e. 16-24 rounds of 64 KiB
+// blocks.  Instead a wave encodes a chain of G consecutive blocks serially
+// (exactly as k_encode_linked does), so only chain heads start from a guess;
+// a wrong head entry is forgotten inside the chain, whose last exit table is
+// then (almost always) right, and the next round re-runs only the chains
+// whose head entry changed.  Blocks inside a chain are exact given the head,
+// so only chain heads are compared (k_link_settle_chain) and can be the
+// serial kernel's first unsettled block.
+__global__ void __launch_bounds__(64) k_encode_linked_chain(const uint8_t* __restrict__ src, uint64_t srcSize,
+                                                            uint32_t blockSize, uint32_t nBlocks, uint32_t G,
+                                                            uint8_t* __restrict__ slots,
+                                                            const LinkPlan* __restrict__ plan,
+                                                            const uint32_t* __restrict__ first, int fresh,
+                                                            const uint32_t* __restrict__ entry,
+                                                            uint32_t* __restrict__ exitT, int32_t* __restrict__ csize,
+                                                            const uint32_t* __restrict__ gate,
+                                                            const uint32_t* __restrict__ flag,
+                                                            uint32_t* __restrict__ enc, uint32_t round) {
+    const uint32_t h = blockIdx.x * G;
+    if (h >= nBlocks || *gate == 0 || flag[h] != round) return;   // settled / head entry unchanged
+    ENCODE_LDS
+    (void)S;
+    l_u32* Tl = (l_u32*)T;
+    const uint32_t L = laneid();
+    const bool fr = h == 0 && fresh;
+    if (!fr) {
+        const uint32_t* in = h == 0 ? first : entry + (uint64_t)h * 4096;
+        for (uint32_t i = L; i < 4096; i += 64) Tl[i] = in[i];
+        WAVE_SYNC();
+    }
+    const uint32_t e = min(h + G, nBlocks);
+    for (uint32_t b = h; b < e; ++b) {
+        const uint64_t off = (uint64_t)b * blockSize;
+        const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
+        const LinkPlan pl = plan[b];
+        const LinkArgs lk{pl.lowIn, pl.lowDict, pl.candLow, fr && b == 0};
+        const int32_t r = encode_block_v5<false, false, false, true>(gptr(src) + off - kLinkO0, kLinkO0 + n,
+                                                                     gptr(slots) + off, n - 1, Tl, (l_u8*)X, nullptr, lk);
+        if (L == 0) csize[b] = r;
+        WAVE_SYNC();
+        for (uint32_t i = L; i < 4096; i += 64) Tl[i] = link_rebase(Tl[i], n);
+        WAVE_SYNC();
+    }
+    uint32_t* o = exitT + (uint64_t)(e - 1) * 4096;
+    for (uint32_t i = L; i < 4096; i += 64) o[i] = Tl[i];
+    if (L == 0) enc[e - 1] = round;
+}
+
+__global__ void __launch_bounds__(256) k_link_settle_chain(const uint32_t* __restrict__ exitT,
+                                                           uint32_t* __restrict__ entry, uint32_t nBlocks, uint32_t G,
+                                                           const uint32_t* __restrict__ gate,
+                                                           const uint32_t* __restrict__ enc, uint32_t* __restrict__ flag,
+                                                           uint32_t* __restrict__ changedNext,
+                                                           uint32_t* __restrict__ firstNext, uint32_t round) {
+    const uint32_t b = (blockIdx.x + 1) * G;   // chain head: entry[b] <- exit[b-1]
+    if (b >= nBlocks || *gate == 0 || enc[b - 1] != round) return;
+    const uint32_t* x = exitT + (uint64_t)(b - 1) * 4096;
+    uint32_t* e = entry + (uint64_t)b * 4096;
+    __shared__ uint32_t diff;
+    if (threadIdx.x == 0) diff = 0;
+    __syncthreads();
+    uint32_t d = 0;
+    for (uint32_t i = threadIdx.x; i < 4096; i += 256) {
+        const uint32_t v = x[i];
+        d |= (e[i] != v) ? 1u : 0u;
+        e[i] = v;
+    }
+    if (d) atomicOr(&diff, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0 && diff) {
+        flag[b] = round + 1;
+        atomicAdd(changedNext, 1u);
+        atomicMin(firstNext, b);
+    }
+}
+
 __global__ void k_link_final(const uint32_t* __restrict__ exitT, uint32_t nBlocks, const uint32_t* __restrict__ gate,
                              uint32_t* __restrict__ table) {
     if (*gate != 0) return;   // not settled: the serial kernel writes the table
@@ -1402,6 +1479,14 @@ static uint32_t link_warm_bytes(uint32_t blockSize) {
     return w;
 }
 
+// blocks per chain of the chained rounds: ~1.5 MiB of parse (0 = one block
+// per wave, the plain rounds); LZ4MT_AMD_BD_CHAIN overrides (A/B)
+static uint32_t link_chain(uint32_t blockSize) {
+    const char* e = getenv("LZ4MT_AMD_BD_CHAIN");
+    if (e) return (uint32_t)std::max(0, atoi(e));
+    return blockSize <= (256u << 10) ? (1536u << 10) / blockSize : 0u;
+}
+
 uint64_t link_round_bytes(uint64_t nBlocks) {
     return nBlocks * 4096 * 4 * 2 + (2 * (uint64_t)(kLinkRounds + 1) + 2 * nBlocks) * 4;
 }
@@ -1430,7 +1515,18 @@ hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32
         hipLaunchKernelGGL(k_link_warm, dim3(nBlocks - 1), dim3(64), 0, st, src, blockSize, warm, slots, entry);
     const uint32_t nInit = 2 * (kLinkRounds + 1) + nBlocks;
     hipLaunchKernelGGL(k_link_init, dim3((nInit + 255) / 256), dim3(256), 0, st, ctl, nBlocks);
-    for (int r = 0; r < rounds; ++r) {
+    const uint32_t G = link_chain(blockSize);
+    for (int r = 0; r < rounds && G > 1; ++r) {   // chained rounds
+        const uint32_t nc = (nBlocks + G - 1) / G;
+        hipLaunchKernelGGL(k_encode_linked_chain, dim3(nc), dim3(64), 0, st, src, srcSize, blockSize, nBlocks, G, slots,
+                           plan, (const uint32_t*)table, fresh ? 1 : 0, (const uint32_t*)entry, exitT, csize,
+                           (const uint32_t*)(changed + r), (const uint32_t*)flag, enc, (uint32_t)r);
+        if (nc > 1)
+            hipLaunchKernelGGL(k_link_settle_chain, dim3(nc - 1), dim3(256), 0, st, (const uint32_t*)exitT, entry,
+                               nBlocks, G, (const uint32_t*)(changed + r), (const uint32_t*)enc, flag, changed + r + 1,
+                               firstU + r + 1, (uint32_t)r);
+    }
+    for (int r = 0; r < rounds && G <= 1; ++r) {
         hipLaunchKernelGGL(k_encode_linked_round, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, plan,
                            (const uint32_t*)table, fresh ? 1 : 0, (const uint32_t*)entry, exitT, csize,
                            (const uint32_t*)(changed + r), (const uint32_t*)flag, enc, (uint32_t)r);

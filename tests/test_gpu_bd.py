@@ -59,13 +59,21 @@ def test_bd_golden_frames_device(golden):
         assert r == 0 and host(out) == data, f["name"]
 
 
-@pytest.mark.parametrize("rounds", ["1", "2", "serial"])
+@pytest.mark.parametrize("rounds", ["1", "2", "serial", "chain2", "chain3-1", "chain0"])
 def test_bd_rounds_and_serial_finish(golden, monkeypatch, rounds):
     """The parallel rounds capped at 1 or 2 leave blocks unsettled: the serial
     kernel finishes from the first unsettled block (its entry table exact);
-    "serial" runs the one-wave kernel alone.  Same bytes as the reference."""
+    "serial" runs the one-wave kernel alone; "chainG[-R]" runs the chained
+    rounds with G blocks per chain (capped at R rounds), "chain0" the
+    one-block-per-wave rounds at every block size.  Same bytes as the
+    reference."""
     if rounds == "serial":
         monkeypatch.setenv("LZ4MT_AMD_BD_SERIAL", "1")
+    elif rounds.startswith("chain"):
+        g, _, r = rounds[5:].partition("-")
+        monkeypatch.setenv("LZ4MT_AMD_BD_CHAIN", g)
+        if r:
+            monkeypatch.setenv("LZ4MT_AMD_BD_ROUNDS", r)
     else:
         monkeypatch.setenv("LZ4MT_AMD_BD_ROUNDS", rounds)
     for f in golden["bd_frames"]:
