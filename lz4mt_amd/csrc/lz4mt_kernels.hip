@@ -611,6 +611,13 @@ typedef __attribute__((address_space(3))) uint16_t __attribute__((aligned(1))) l
 typedef __attribute__((address_space(3))) uint64_t l_u64;
 
 constexpr uint32_t kSR = 2048;        // source ring bytes
+// forward-count words the v5 round trip loads per side (the first 4 * this
+// many bytes after the minimum match; longer matches take 256-byte rounds)
+#ifndef LZ4MT_COUNT_LANES
+#define LZ4MT_COUNT_LANES 32
+#endif
+constexpr uint32_t kCountLanes = LZ4MT_COUNT_LANES;
+static_assert(kCountLanes >= 1 && kCountLanes <= 63, "count lanes");
 constexpr uint32_t kSRMirror = 64;    // ring[kSR .. kSR+64) mirrors ring[0 .. 64)
 
 __device__ __forceinline__ uint32_t gld4u(g_cu8* p) { return *(g_cu32u*)p; }
@@ -954,8 +961,11 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                         const uint32_t lowL = !LINK ? 0u : (cd >= o0 ? lk.lowIn : lk.lowDict);
                         maxb = w == 1 ? 0u : min(ip - anchor, cd > lowL ? cd - lowL : 0u);
                     }
-                    const uint32_t ci = cd + 4 * L, ii = ip + 4 * L;
-                    cw = gld4u(s + (ci < last4 ? ci : last4));   // lane 0: verify word; lanes >= 1: count words
+                    // lane 0: verify word; lanes 1 .. kCountLanes: count words; the
+                    // rest repeat lane 0's address (no further lines touched)
+                    const bool cOn = L <= kCountLanes;
+                    const uint32_t ci = cOn ? cd + 4 * L : cd, ii = cOn ? ip + 4 * L : ip;
+                    cw = gld4u(s + (ci < last4 ? ci : last4));
                     iw = gld4u(s + (ii < last4 ? ii : last4));
                     const bool bOn = L < maxb;
                     bi = s[bOn ? ip - L - 1 : o0];   // (o0: a byte of the block itself)
@@ -1018,12 +1028,12 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                 const uint32_t x = cw ^ iw;
                 uint32_t e = min(x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u, lim - rel);
                 e = (L != 0 && rel < lim) ? e : 0u;
-                const uint64_t nf = bal(L != 0 && e < 4);
+                const uint64_t nf = bal(L != 0 && e < 4) & mask_le(kCountLanes);
                 if (nf) {
                     const uint32_t f = (uint32_t)__builtin_ctzll(nf);
                     mc = 4 * (f - 1) + rdlane(e, (int)f);
                 } else {
-                    mc = 252;
+                    mc = 4 * kCountLanes;
                     uint64_t nf2 = 0;
                     while (!nf2) {   // long match: 256 bytes per round
                         const uint32_t r2 = mc + 4 * L;
