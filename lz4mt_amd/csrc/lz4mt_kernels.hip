@@ -822,6 +822,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     }
     SrcRing V{s, n, R, 0, 0, 0};
     V.init(o0);
+    const uint32_t capL = limited ? cap : 0xFFFFFFFFu;   // one SGPR for the per-sequence margin test
     const uint32_t mflimitP1 = n - kMfLimit + 1;
     const uint32_t matchlimit = n - kLastLiterals;
     const uint32_t last4 = n - 4;
@@ -865,9 +866,13 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         const bool insOn = mode != 0, testOn = mode == 1;
         const uint32_t insPos = mode == 2 ? o0 : sBase - 3, testPos = sBase - 1;
         p = L == 0 ? insPos : (L == 1 ? testPos : p);
-        const bool srch = L >= 2;
-        const bool live = srch ? p <= mflimitP1 : (L == 0 ? insOn : testOn);
-        const bool term = srch && live && p + step > mflimitP1;
+        // lane predicates as wave masks (SALU), turned back into per-lane
+        // conditions with inverse_ballot (the mask is the select's condition):
+        // no 0/1 materialisation chains
+        const uint64_t liveM = (bal(p <= mflimitP1) & ~3ull) | (insOn ? 1ull : 0ull) | (testOn ? 2ull : 0ull);
+        const uint64_t tmk = bal(p + step > mflimitP1) & liveM & ~3ull;
+        const bool live = __builtin_amdgcn_inverse_ballot_w64(liveM);
+        const bool term = __builtin_amdgcn_inverse_ballot_w64(tmk);
         const uint32_t lo = insOn ? insPos : sBase;
         const uint32_t hi = (sHi < mflimitP1 ? sHi : mflimitP1) + 8;
         uint64_t v8;
@@ -893,11 +898,10 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         const uint64_t pend = bal(sv != (mark & G::kRbMask));   // same-bucket collision inside the window
         const uint32_t dq = (p - told) & G::PM;   // P17: the distance, exact below 2^17
         uint32_t cand = P17 ? p - dq : told & G::PM;
-        const bool cok = live && L != 0 && !term && (P17 ? dq <= kDistMax : cand + kDistMax >= p) &&
-                         (!LINK || cand >= lk.candLow);
-        bool maybe = cok && (told >> G::PB) == (mark >> G::PB);
-        const uint64_t tmk = bal(term);
-        uint64_t mm = bal(maybe);
+        const uint64_t cokM = bal((P17 ? dq <= kDistMax : cand + kDistMax >= p) && (!LINK || cand >= lk.candLow)) &
+                              liveM & ~tmk & ~1ull;
+        uint64_t mm = cokM & bal((told >> G::PB) == (mark >> G::PB));
+        bool maybe = __builtin_amdgcn_inverse_ballot_w64(mm);
         uint64_t sm = mm | tmk;
         STAMP_ADD(0, ts);
         // ---- resolve the first stop.  Exact in-window predecessors are
@@ -1012,7 +1016,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             // bi/bc are consumed on every path, so no load of this window is
             // left pending into the next window's round trip.
             asm volatile("" ::"v"(bi), "v"(bc));
-            uint64_t fm = ~bal(L < maxb && bi == bc);
+            uint64_t fm = ~(bal(L < maxb) & bal(bi == bc));
             uint32_t back = 0;
             while (fm == 0 && back + 64 < maxb) {   // catch-up longer than 64 bytes
                 back += 64;
@@ -1027,8 +1031,8 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                 const uint32_t rel = 4 * L - 4;
                 const uint32_t x = cw ^ iw;
                 uint32_t e = min(x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u, lim - rel);
-                e = (L != 0 && rel < lim) ? e : 0u;
-                const uint64_t nf = bal(L != 0 && e < 4) & mask_le(kCountLanes);
+                e = rel < lim ? e : 0u;   // (lane 0's e is masked out below)
+                const uint64_t nf = bal(e < 4) & (mask_le(kCountLanes) & ~1ull);
                 if (nf) {
                     const uint32_t f = (uint32_t)__builtin_ctzll(nf);
                     mc = 4 * (f - 1) + rdlane(e, (int)f);
@@ -1054,7 +1058,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             const uint32_t litExt = ext_len(lit), mlExt = ext_len(mcf);
             // 1.9.3's limitedOutput margins; both hold whenever
             // op + 2 (lit + mcf) + 16 <= cap, so the exact test runs rarely
-            if (limited && op + 2 * (lit + mcf) + 16 > cap) {
+            if (op + 2 * (lit + mcf) + 16 > capL) {
                 fail = (w != 1 && op + 1 + lit + 8 + lit / 255 > cap) ||
                        (op + 1 + litExt + lit + 2 + 6 + (mcf + 240) / 255 > cap);
             }
