@@ -8,8 +8,10 @@
  * In lz4 1.9.3 that is LZ4_compress_HC on a fresh state: levels 1..9 run
  * LZ4HC_compress_hashChain with maxNbAttempts = 2,2,2,4,8,16,32,64,128,256
  * (clTable), pattern analysis from 256 attempts (level 9), no chain swap,
- * favorCompressionRatio.  Levels 10..12 (the optimal parser) are not
- * restated (lz4mt's CLI stops at 9).
+ * favorCompressionRatio.  Levels 10..12 (and above, clamped to 12: the
+ * CLI's -A asks for 17) run LZ4HC_compress_optimal: nbSearches 96 / 512 /
+ * 16384, target length 64 / 128 / LZ4_OPT_NUM, full update at 12, pattern
+ * analysis and chain swap in every search.
  *
  * Positions are indices from src; lz4hc's own indices are these + 64 KiB
  * (LZ4HC_init_internal: startingOffset = 64 KB), which only matters for the
@@ -90,10 +92,11 @@ static unsigned hc_rcount_run(const uint8_t* ip, const uint8_t* iLow, uint8_t b)
 }
 
 /* LZ4HC_InsertAndGetWiderMatch (noDictCtx, single segment: every candidate
- * is in the prefix, dictLimit = lowLimit = HC_BASE; chainSwap = 0). */
+ * is in the prefix, dictLimit = lowLimit = HC_BASE; chainSwap on for the
+ * optimal parser only). */
 static int hc_wider_match(hc_ctx* c, const uint8_t* ip, const uint8_t* iLowLimit, const uint8_t* iHighLimit,
                           int longest, const uint8_t** matchpos, const uint8_t** startpos, int maxNbAttempts,
-                          int patternAnalysis) {
+                          int patternAnalysis, int chainSwap) {
     const uint32_t ipIndex = (uint32_t)(ip - c->s) + HC_BASE;
     const uint32_t lowestMatchIndex = (HC_BASE + HC_DIST_MAX + 1 > ipIndex) ? HC_BASE : ipIndex - HC_DIST_MAX;
     const uint8_t* const lowPrefixPtr = c->s;
@@ -103,16 +106,18 @@ static int hc_wider_match(hc_ctx* c, const uint8_t* ip, const uint8_t* iLowLimit
     int repeat = 0;   /* 0 untested, 1 confirmed, 2 not */
     size_t srcPatternLength = 0;
 
+    uint32_t matchChainPos = 0;
     hc_insert(c, ipIndex);
     uint32_t matchIndex = c->hashTable[hc_hash(pattern)];
     while (matchIndex >= lowestMatchIndex && nbAttempts > 0) {
+        int matchLength = 0;
         nbAttempts--;
         {
             const uint8_t* const matchPtr = AT(c, matchIndex);
             if (hc_rd16(iLowLimit + longest - 1) == hc_rd16(matchPtr - lookBackLength + longest - 1)) {
                 if (hc_rd32(matchPtr) == pattern) {
                     const int back = lookBackLength ? hc_count_back(ip, matchPtr, iLowLimit, lowPrefixPtr) : 0;
-                    int matchLength = HC_MINMATCH + (int)hc_count(ip + HC_MINMATCH, matchPtr + HC_MINMATCH, iHighLimit);
+                    matchLength = HC_MINMATCH + (int)hc_count(ip + HC_MINMATCH, matchPtr + HC_MINMATCH, iHighLimit);
                     matchLength -= back;
                     if (matchLength > longest) {
                         longest = matchLength;
@@ -122,9 +127,32 @@ static int hc_wider_match(hc_ctx* c, const uint8_t* ip, const uint8_t* iLowLimit
                 }
             }
         }
+        if (chainSwap && matchLength == longest) {   /* better match => select a better chain */
+            if (matchIndex + (uint32_t)longest <= ipIndex) {
+                const int kTrigger = 4;
+                uint32_t distanceToNextMatch = 1;
+                const int end = longest - HC_MINMATCH + 1;
+                int step = 1;
+                int accel = 1 << kTrigger;
+                for (int pos = 0; pos < end; pos += step) {
+                    const uint32_t candidateDist = c->chainTable[(uint16_t)(matchIndex + (uint32_t)pos)];
+                    step = (accel++ >> kTrigger);
+                    if (candidateDist > distanceToNextMatch) {
+                        distanceToNextMatch = candidateDist;
+                        matchChainPos = (uint32_t)pos;
+                        accel = 1 << kTrigger;
+                    }
+                }
+                if (distanceToNextMatch > 1) {
+                    if (distanceToNextMatch > matchIndex) break;   /* avoid overflow */
+                    matchIndex -= distanceToNextMatch;
+                    continue;
+                }
+            }
+        }
         {
             const uint32_t distNextMatch = c->chainTable[(uint16_t)matchIndex];
-            if (patternAnalysis && distNextMatch == 1) {
+            if (patternAnalysis && distNextMatch == 1 && matchChainPos == 0) {
                 const uint32_t matchCandidateIdx = matchIndex - 1;
                 if (repeat == 0) {
                     if (((pattern & 0xFFFF) == (pattern >> 16)) & ((pattern & 0xFF) == (pattern >> 24))) {
@@ -172,7 +200,7 @@ static int hc_wider_match(hc_ctx* c, const uint8_t* ip, const uint8_t* iLowLimit
                 }
             }
         }
-        matchIndex -= c->chainTable[(uint16_t)matchIndex];   /* follow the chain (matchChainPos = 0) */
+        matchIndex -= c->chainTable[(uint16_t)(matchIndex + matchChainPos)];   /* follow the current chain */
     }
     return longest;
 }
@@ -237,13 +265,13 @@ static int hc_compress_range(hc_ctx* c, const uint8_t* ip0, uint8_t* dst, int n,
         {
             const uint8_t* useless = ip;
             ml = hc_wider_match(c, ip, ip, matchlimit, HC_MINMATCH - 1, &ref, &useless, maxNbAttempts,
-                                patternAnalysis);
+                                patternAnalysis, 0);
         }
         if (ml < HC_MINMATCH) { ip++; continue; }
         start0 = ip; ref0 = ref; ml0 = ml;
     search2:
         if (ip + ml <= mflimit)
-            ml2 = hc_wider_match(c, ip + ml - 2, ip, matchlimit, ml, &ref2, &start2, maxNbAttempts, patternAnalysis);
+            ml2 = hc_wider_match(c, ip + ml - 2, ip, matchlimit, ml, &ref2, &start2, maxNbAttempts, patternAnalysis, 0);
         else
             ml2 = ml;
         if (ml2 == ml) {   /* no better match: encode ML1 */
@@ -265,7 +293,7 @@ static int hc_compress_range(hc_ctx* c, const uint8_t* ip0, uint8_t* dst, int n,
         }
         if (start2 + ml2 <= mflimit)
             ml3 = hc_wider_match(c, start2 + ml2 - 3, start2, matchlimit, ml2, &ref3, &start3, maxNbAttempts,
-                                 patternAnalysis);
+                                 patternAnalysis, 0);
         else
             ml3 = ml2;
         if (ml3 == ml2) {   /* no better match: encode ML1 and ML2 */
@@ -328,6 +356,185 @@ overflow:
     return result;
 }
 
+/* ---- the optimal parser (levels 10..12: LZ4HC_compress_optimal 1.9.3) ---- */
+#define HC_OPT_NUM 4096           /* LZ4_OPT_NUM */
+#define HC_TRAILING_LITERALS 3
+
+typedef struct { int price, off, mlen, litlen; } hc_opt_t;
+
+/* LZ4HC_literalsPrice / LZ4HC_sequencePrice: bytes */
+static int hc_lit_price(int litlen) {
+    int price = litlen;
+    if (litlen >= 15) price += 1 + (litlen - 15) / 255;
+    return price;
+}
+static int hc_seq_price(int litlen, int mlen) {
+    int price = 1 + 2 + hc_lit_price(litlen);
+    if (mlen >= 15 + HC_MINMATCH) price += 1 + (mlen - (15 + HC_MINMATCH)) / 255;
+    return price;
+}
+
+/* LZ4HC_FindLongerMatch: a match longer than minLen at ip (no look-back,
+ * pattern analysis and chain swap on); len 0 if none */
+static void hc_longer_match(hc_ctx* c, const uint8_t* ip, const uint8_t* iHighLimit, int minLen, int nbSearches,
+                            int* len, int* off) {
+    const uint8_t* matchPtr = NULL;
+    const uint8_t* start = ip;
+    const int ml = hc_wider_match(c, ip, ip, iHighLimit, minLen, &matchPtr, &start, nbSearches, 1, 1);
+    if (ml <= minLen) { *len = 0; *off = 0; return; }
+    *len = ml;
+    *off = (int)(start - matchPtr);
+}
+
+/* LZ4HC_compress_optimal (favorCompressionRatio, noDictCtx); 0 = does not fit cap */
+static int hc_compress_optimal(hc_ctx* c, const uint8_t* src, uint8_t* dst, int n, int cap, int nbSearches,
+                               int sufficient_len, int fullUpdate, hc_opt_t* opt) {
+    const int limit = cap < orc_lz4_compress_bound(n);
+    const uint8_t* ip = src;
+    const uint8_t* anchor = ip;
+    const uint8_t* const iend = ip + n;
+    const uint8_t* const mflimit = iend - HC_MFLIMIT;
+    const uint8_t* const matchlimit = iend - HC_LASTLITERALS;
+    uint8_t* op = dst;
+    const uint8_t* const oend = dst + cap;
+    if (sufficient_len >= HC_OPT_NUM) sufficient_len = HC_OPT_NUM - 1;
+
+    while (ip <= mflimit) {
+        const int llen = (int)(ip - anchor);
+        int best_mlen, best_off, cur, last_match_pos = 0;
+        int fmLen, fmOff;
+        hc_longer_match(c, ip, matchlimit, HC_MINMATCH - 1, nbSearches, &fmLen, &fmOff);
+        if (fmLen == 0) { ip++; continue; }
+        if (fmLen > sufficient_len) {   /* good enough: immediate encoding */
+            if (hc_encode(&ip, &op, &anchor, fmLen, ip - fmOff, limit, oend)) return 0;
+            continue;
+        }
+        for (int rPos = 0; rPos < HC_MINMATCH; rPos++) {   /* literals at the first positions */
+            opt[rPos].mlen = 1;
+            opt[rPos].off = 0;
+            opt[rPos].litlen = llen + rPos;
+            opt[rPos].price = hc_lit_price(llen + rPos);
+        }
+        for (int mlen = HC_MINMATCH; mlen <= fmLen; mlen++) {   /* the first match */
+            opt[mlen].mlen = mlen;
+            opt[mlen].off = fmOff;
+            opt[mlen].litlen = llen;
+            opt[mlen].price = hc_seq_price(llen, mlen);
+        }
+        last_match_pos = fmLen;
+        for (int addLit = 1; addLit <= HC_TRAILING_LITERALS; addLit++) {
+            opt[last_match_pos + addLit].mlen = 1;
+            opt[last_match_pos + addLit].off = 0;
+            opt[last_match_pos + addLit].litlen = addLit;
+            opt[last_match_pos + addLit].price = opt[last_match_pos].price + hc_lit_price(addLit);
+        }
+        for (cur = 1; cur < last_match_pos; cur++) {
+            const uint8_t* const curPtr = ip + cur;
+            int nmLen, nmOff;
+            if (curPtr > mflimit) break;
+            if (fullUpdate) {
+                if (opt[cur + 1].price <= opt[cur].price && opt[cur + HC_MINMATCH].price < opt[cur].price + 3) continue;
+            } else {
+                if (opt[cur + 1].price <= opt[cur].price) continue;
+            }
+            if (fullUpdate)
+                hc_longer_match(c, curPtr, matchlimit, HC_MINMATCH - 1, nbSearches, &nmLen, &nmOff);
+            else
+                hc_longer_match(c, curPtr, matchlimit, last_match_pos - cur, nbSearches, &nmLen, &nmOff);
+            if (!nmLen) continue;
+            if (nmLen > sufficient_len || nmLen + cur >= HC_OPT_NUM) {   /* immediate encoding */
+                best_mlen = nmLen;
+                best_off = nmOff;
+                last_match_pos = cur + 1;
+                goto encode;
+            }
+            {   /* before the match: literals after the path to cur */
+                const int baseLitlen = opt[cur].litlen;
+                for (int litlen = 1; litlen < HC_MINMATCH; litlen++) {
+                    const int price = opt[cur].price - hc_lit_price(baseLitlen) + hc_lit_price(baseLitlen + litlen);
+                    const int pos = cur + litlen;
+                    if (price < opt[pos].price) {
+                        opt[pos].mlen = 1;
+                        opt[pos].off = 0;
+                        opt[pos].litlen = baseLitlen + litlen;
+                        opt[pos].price = price;
+                    }
+                }
+            }
+            for (int ml = HC_MINMATCH; ml <= nmLen; ml++) {   /* the match at cur */
+                const int pos = cur + ml;
+                int price, ll;
+                if (opt[cur].mlen == 1) {
+                    ll = opt[cur].litlen;
+                    price = ((cur > ll) ? opt[cur - ll].price : 0) + hc_seq_price(ll, ml);
+                } else {
+                    ll = 0;
+                    price = opt[cur].price + hc_seq_price(0, ml);
+                }
+                if (pos > last_match_pos + HC_TRAILING_LITERALS || price <= opt[pos].price) {
+                    if (ml == nmLen && last_match_pos < pos) last_match_pos = pos;
+                    opt[pos].mlen = ml;
+                    opt[pos].off = nmOff;
+                    opt[pos].litlen = ll;
+                    opt[pos].price = price;
+                }
+            }
+            for (int addLit = 1; addLit <= HC_TRAILING_LITERALS; addLit++) {
+                opt[last_match_pos + addLit].mlen = 1;
+                opt[last_match_pos + addLit].off = 0;
+                opt[last_match_pos + addLit].litlen = addLit;
+                opt[last_match_pos + addLit].price = opt[last_match_pos].price + hc_lit_price(addLit);
+            }
+        }
+        best_mlen = opt[last_match_pos].mlen;
+        best_off = opt[last_match_pos].off;
+        cur = last_match_pos - best_mlen;
+    encode:
+        {   /* reverse traversal: the shortest path's sequences */
+            int candidate_pos = cur;
+            int selected_matchLength = best_mlen;
+            int selected_offset = best_off;
+            for (;;) {
+                const int next_matchLength = opt[candidate_pos].mlen;
+                const int next_offset = opt[candidate_pos].off;
+                opt[candidate_pos].mlen = selected_matchLength;
+                opt[candidate_pos].off = selected_offset;
+                selected_matchLength = next_matchLength;
+                selected_offset = next_offset;
+                if (next_matchLength > candidate_pos) break;
+                candidate_pos -= next_matchLength;
+            }
+        }
+        {
+            int rPos = 0;
+            while (rPos < last_match_pos) {
+                const int ml = opt[rPos].mlen;
+                const int offset = opt[rPos].off;
+                if (ml == 1) { ip++; rPos++; continue; }
+                rPos += ml;
+                if (hc_encode(&ip, &op, &anchor, ml, ip - offset, limit, oend)) return 0;
+            }
+        }
+    }
+    {   /* last literals */
+        const size_t lastRunSize = (size_t)(iend - anchor);
+        const size_t llAdd = (lastRunSize + 255 - 15) / 255;
+        const size_t totalSize = 1 + llAdd + lastRunSize;
+        if (limit && op + totalSize > oend) return 0;
+        if (lastRunSize >= 15) {
+            size_t acc = lastRunSize - 15;
+            *op++ = (uint8_t)(15 << 4);
+            for (; acc >= 255; acc -= 255) *op++ = 255;
+            *op++ = (uint8_t)acc;
+        } else {
+            *op++ = (uint8_t)(lastRunSize << 4);
+        }
+        memcpy(op, anchor, lastRunSize);
+        op += lastRunSize;
+    }
+    return (int)(op - dst);
+}
+
 static void hc_ctx_init(hc_ctx* c, const uint8_t* s, int n) {
     c->s = s;
     c->n = n;
@@ -337,15 +544,23 @@ static void hc_ctx_init(hc_ctx* c, const uint8_t* s, int n) {
 }
 
 int orc_lz4hc_compress(const uint8_t* src, uint8_t* dst, int n, int cap, int level) {
-    static const int kAttempts[10] = {2, 2, 2, 4, 8, 16, 32, 64, 128, 256};   /* clTable[0..9] */
+    static const int kAttempts[13] = {2, 2, 2, 4, 8, 16, 32, 64, 128, 256, 96, 512, 16384};   /* clTable */
+    static const int kTarget[13] = {16, 16, 16, 16, 16, 16, 16, 16, 16, 16, 64, 128, HC_OPT_NUM};
     if ((unsigned)n > 0x7E000000u) return 0;
     if (level < 1) level = 9;   /* LZ4HC_CLEVEL_DEFAULT */
-    if (level > 9) return -1;   /* the optimal parser (10..12) is not restated */
+    if (level > 12) level = 12; /* LZ4HC_CLEVEL_MAX */
     hc_ctx c;
     c.hashTable = (uint32_t*)malloc((1u << HC_HASH_LOG) * sizeof(uint32_t));
     c.chainTable = (uint16_t*)malloc(65536 * sizeof(uint16_t));
     hc_ctx_init(&c, src, n);
-    const int r = hc_compress_range(&c, src, dst, n, cap, kAttempts[level], kAttempts[level] > 128);
+    int r;
+    if (level <= 9) {
+        r = hc_compress_range(&c, src, dst, n, cap, kAttempts[level], kAttempts[level] > 128);
+    } else {
+        hc_opt_t* opt = (hc_opt_t*)malloc(sizeof(hc_opt_t) * (HC_OPT_NUM + HC_TRAILING_LITERALS));
+        r = hc_compress_optimal(&c, src, dst, n, cap, kAttempts[level], kTarget[level], level == 12, opt);
+        free(opt);
+    }
     free(c.hashTable);
     free(c.chainTable);
     return r;

@@ -411,7 +411,7 @@ def main():
     hc_inputs["bdmix300k"] = bd_input(300_000, 31)
     for name, data in hc_inputs.items():
         blk = data[:300_000]
-        for level in (3, 4, 6, 8, 9):
+        for level in (3, 4, 6, 8, 9, 10, 11, 12):   # 10..12: the optimal parser (the CLI's -A asks for 17 = 12)
             for cap in sorted({len(blk), max(len(blk) - 1, 0)}):
                 dst = ctypes.create_string_buffer(max(cap, 1) + len(blk) // 255 + 64)
                 r = LZ4.LZ4_compress_HC(blk, dst, len(blk), cap, level)

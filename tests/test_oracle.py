@@ -314,6 +314,22 @@ def _hc_mixed(n, seed):
 
 
 @pytest.mark.skipif(not os.path.exists(LIBLZ4), reason="liblz4 not present")
+def test_hc_optimal_differential_vs_liblz4():
+    """Levels 10..12 (LZ4HC_compress_optimal) and 17 (the reference CLI's -A,
+    src/main.cpp:377, clamped to 12 by lz4hc) against liblz4 1.9.3."""
+    lz = ctypes.CDLL(LIBLZ4)
+    lz.LZ4_compress_HC.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    inputs = [_hc_mixed(n, seed) for seed, n in enumerate([12, 13, 100, 5000, 65547, 200_000, 300_000])]
+    inputs += [oracle.gen_synthetic(1 << 20, 42), bytes(100_000), oracle.gen_random(70_000, 3)]
+    for d in inputs:
+        for level in (10, 11, 12, 17):
+            for cap in (len(d), len(d) - 1, len(d) // 2):
+                dst = ctypes.create_string_buffer(max(cap, 1) + len(d) // 255 + 64)
+                r = lz.LZ4_compress_HC(d, dst, len(d), cap, level)
+                assert oracle.compress_block_hc(d, cap, level) == dst.raw[:r], (len(d), level, cap)
+
+
+@pytest.mark.skipif(not os.path.exists(LIBLZ4), reason="liblz4 not present")
 def test_hc_differential_vs_liblz4():
     lz = ctypes.CDLL(LIBLZ4)
     lz.LZ4_compress_HC.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
