@@ -167,7 +167,8 @@ def compress_workspace(n, sd=None, device=None, level=0):
 
 def compress_frame(src, sd=None, out=None, workspace=None, stream=None, level=0):
     """Compresses a device tensor into one lz4mt frame; returns the frame tensor (a view of ``out``).
-    ``level`` 3..9 selects LZ4-HC (the reference's codec for those levels)."""
+    ``level`` >= 3 selects LZ4-HC (the reference's codec for those levels:
+    3..9 hashChain, 10..12 and above the optimal parser)."""
     _check_dev(src, "src")
     sd = sd if sd is not None else init_stream_descriptor()
     n = src.numel()

@@ -413,8 +413,8 @@ extern "C" int lz4mtHipCompressBound(int isize) {
 }
 
 extern "C" int lz4mtHipCompressBlock(const char* src, char* dst, int isize, int maxOutputSize, int compressionLevel) {
-    // levels >= 3: LZ4-HC (LZ4_compressHC2_limitedOutput); 10..12, lz4's
-    // optimal parser, is not provided: 0 = the caller stores the block raw
+    // levels >= 3: LZ4-HC (LZ4_compressHC2_limitedOutput): 3..9 hashChain,
+    // 10..12 (and above, clamped to 12) the optimal parser
     const bool hc = compressionLevel >= 3;
     if (hc && hc_attempts(compressionLevel) == 0) return 0;
     if (isize < 0 || (unsigned)isize > 0x7E000000u) return 0;
@@ -499,9 +499,9 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
     if (v != LZ4MT_RESULT_OK) return v;
     if (!have_device()) return LZ4MT_RESULT_ERROR;
     if (frameCap < lz4mtHipFrameBound(srcSize, sd)) return LZ4MT_RESULT_BAD_ARG;
-    // LZ4-HC runs for levels 3..9 on independent blocks; levels 10..12 (the
-    // optimal parser) are not provided.  Block-dependent frames at any level
-    // >= 3 are the reference's HC stream, which runs at level 9 (HcBdSim).
+    // LZ4-HC on independent blocks: levels 3..9 the hashChain parser, 10..12
+    // (and above, clamped) the optimal parser.  Block-dependent frames at any
+    // level >= 3 are the reference's HC stream, which runs at level 9 (HcBdSim).
     if (level >= 3 && sd->flg.blockIndependence && hc_attempts(level) == 0) return LZ4MT_RESULT_BAD_ARG;
     if (level < 3) level = 0;
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);

@@ -513,9 +513,9 @@ struct CallBuf {
 
 void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
     if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return; }
-    // LZ4-HC (levels 3..9) on independent blocks; lz4's optimal parser
-    // (10..12) is not provided.  Block-dependent frames at any level >= 3 are
-    // the reference's HC stream, at level 9 (HcBdSim).
+    // LZ4-HC on independent blocks: levels 3..9 the hashChain parser, 10..12
+    // (and above, clamped) the optimal parser.  Block-dependent frames at any
+    // level >= 3 are the reference's HC stream, at level 9 (HcBdSim).
     const int level = s.level() >= 3 ? s.level() : 0;
     if (level && sd->flg.blockIndependence && hc_attempts(level) == 0) { s.quit(LZ4MT_RESULT_BAD_ARG); return; }
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);

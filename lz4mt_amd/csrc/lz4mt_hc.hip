@@ -1,4 +1,4 @@
-// lz4mt_hc.hip — LZ4-HC (compression levels 3..9) for gfx950: the codec
+// lz4mt_hc.hip — LZ4-HC (compression levels 3..12) for gfx950: the codec
 // lz4mt selects for level >= 3, LZ4_compressHC2_limitedOutput(src, dst, n,
 // cap = n, level) (reference src/main.cpp:778-785, src/lz4mt.cpp:391), i.e.
 // lz4 1.9.3's LZ4_compress_HC -> LZ4HC_compress_hashChain.  Bit-exact with
@@ -252,9 +252,10 @@ struct HcBlock {
         }
     }
 
-    // LZ4HC_InsertAndGetWiderMatch (single segment, chainSwap = 0); positions
-    // are block offsets.  Returns longest; *mpos / *spos as lz4hc's
-    // matchpos / startpos.
+    // LZ4HC_InsertAndGetWiderMatch (single segment); positions are block
+    // offsets.  Returns longest; *mpos / *spos as lz4hc's matchpos /
+    // startpos.  CS: chainSwap (the optimal parser's searches; lookBack 0).
+    template <bool CS = false>
     __device__ int wider(uint32_t ip, uint32_t iLow, uint32_t iHigh, int longest, uint32_t* mpos,
                          uint32_t* spos) const {
         const uint32_t lowest = ip > kHcDist ? ip - kHcDist : 0u;
@@ -263,6 +264,7 @@ struct HcBlock {
         const uint32_t pat = rd32(s + ip);
         int repeat = 0;   // 0 untested, 1 confirmed, 2 not
         uint32_t srcPatLen = 0;
+        uint32_t mcp = 0;   // matchChainPos
         const uint32_t d0 = uni(dl[ip]);
         if (d0 == 0) return longest;   // no earlier position with this hash in the window
         uint32_t m = ip - d0;
@@ -272,18 +274,51 @@ struct HcBlock {
             const uint32_t f16 = uni(rd16(s + m - lookBack + (uint32_t)longest - 1));
             const uint32_t m32 = uni(rd32(s + m));
             const uint32_t dnext = uni(dl[m]);
+            int matchLength = 0;
             if (uni(rd16(s + iLow + (uint32_t)longest - 1)) == f16 && m32 == pat) {
                 const int back = lookBack ? count_back(ip, m, iLow, 0) : 0;
                 int ml = 4 + (int)count_fwd(ip + 4, m + 4, iHigh);
                 ml -= back;
+                matchLength = ml;
                 if (ml > longest) {
                     longest = ml;
                     *mpos = m + (uint32_t)back;
                     *spos = ip + (uint32_t)back;
                 }
             }
+            if (CS && matchLength == longest && m + (uint32_t)longest <= ip) {
+                // a better chain: the position of the match whose chain link
+                // reaches furthest back (lz4hc's accelerating scan), 64
+                // links per load round
+                uint32_t dtn = 1;
+                const int end = longest - 4 + 1;
+                int step = 1, accel = 1 << 4;
+                int pos = 0, base = -64;
+                uint32_t lk = 0;
+                while (pos < end) {
+                    if (pos >= base + 64) {   // links of [pos, pos + 64)
+                        base = pos;
+                        const uint32_t q = m + (uint32_t)pos + laneid();
+                        lk = dl[q];
+                        lk = lk ? lk : kHcDist;
+                    }
+                    const uint32_t cdist = rdlane(lk, pos - base);
+                    step = accel++ >> 4;
+                    if (cdist > dtn) {
+                        dtn = cdist;
+                        mcp = (uint32_t)pos;
+                        accel = 1 << 4;
+                    }
+                    pos += step;
+                }
+                if (dtn > 1) {
+                    if (dtn > m) break;   // below the block: under `lowest`
+                    m -= dtn;
+                    continue;
+                }
+            }
             const uint32_t distNext = dnext ? dnext : kHcDist;
-            if (pattern && distNext == 1) {
+            if (pattern && distNext == 1 && (!CS || mcp == 0)) {
                 const uint32_t cand = m - 1;
                 if (repeat == 0) {
                     if (((pat & 0xFFFF) == (pat >> 16)) & ((pat & 0xFF) == (pat >> 24))) {
@@ -322,8 +357,9 @@ struct HcBlock {
                     continue;
                 }
             }
-            if (m < distNext) break;   // would go below the block: under `lowest`
-            m -= distNext;
+            const uint32_t dfol = (CS && mcp) ? chain(m + mcp) : distNext;   // follow the current chain
+            if (m < dfol) break;   // would go below the block: under `lowest`
+            m -= dfol;
         }
         return longest;
     }
@@ -530,6 +566,191 @@ __device__ int32_t encode_block_hc(const HcBlock& B, g_u8* d, uint32_t cap, uint
     return r.status == kHcEnd ? (int32_t)r.op : 0;
 }
 
+// ---------------------------------------------------------------------------
+// Levels 10..12 (and above, clamped to 12: the reference CLI's -A asks for
+// 17, src/main.cpp:377): lz4 1.9.3's LZ4HC_compress_optimal, restated in
+// oracle/lz4hc_oracle.c (hc_compress_optimal).  One wave per block; the
+// parser state is wave-uniform, its price table (LZ4_OPT_NUM + 3 entries)
+// sits in LDS as four arrays, and the lanes run the searches' counts, the
+// price updates of a match (one lane per match length) and the byte writes.
+// ---------------------------------------------------------------------------
+constexpr int kOptNum = 4096;                 // LZ4_OPT_NUM
+constexpr int kOptEntries = kOptNum + 3 + 1;  // + TRAILING_LITERALS (+ pad)
+typedef __attribute__((address_space(3))) int32_t l_i32;
+typedef __attribute__((address_space(3))) uint16_t l_u16;
+
+struct HcOpt {   // opt[] of LZ4HC_compress_optimal, structure of arrays
+    l_i32* price;
+    l_i32* litlen;
+    l_i32* mlen;
+    l_u16* off;
+};
+
+__device__ __forceinline__ int hc_lit_price(int litlen) { return litlen + (litlen >= 15 ? 1 + (litlen - 15) / 255 : 0); }
+__device__ __forceinline__ int hc_seq_price(int litlen, int mlen) {
+    return 3 + hc_lit_price(litlen) + (mlen >= 19 ? 1 + (mlen - 19) / 255 : 0);
+}
+
+// LZ4HC_compress_optimal over the block (fresh state, favorCompressionRatio);
+// 0 = does not fit cap (store raw)
+__device__ int32_t encode_block_hc_opt(const HcBlock& B, g_u8* d, uint32_t cap, const HcOpt& O, int suff,
+                                       bool fullUpdate) {
+    const uint32_t L = laneid();
+    const uint32_t n = B.n;
+    g_cu8* s = B.s;
+    const bool limit = (uint64_t)cap < (uint64_t)n + n / 255 + 16;
+    uint32_t ip = 0, anchor = 0, op = 0;
+    if (suff >= kOptNum) suff = kOptNum - 1;
+    // FindLongerMatch: a match longer than minLen at p (pattern analysis and chain swap on)
+    auto longer = [&](uint32_t p, int minLen, int& len, int& off) {
+        uint32_t mpos = 0, spos = p;
+        const int ml = B.wider<true>(p, p, n - 5, minLen, &mpos, &spos);
+        len = ml > minLen ? ml : 0;
+        off = ml > minLen ? (int)(spos - mpos) : 0;
+    };
+    auto trailing = [&](int last) {   // literals after the last match position
+        WAVE_SYNC();
+        const int p0 = (int)uni((uint32_t)O.price[last]);
+        if (L >= 1 && L <= 3) {
+            O.mlen[last + L] = 1; O.off[last + L] = 0; O.litlen[last + L] = (int)L;
+            O.price[last + L] = p0 + hc_lit_price((int)L);
+        }
+        WAVE_SYNC();
+    };
+    if (n >= 13) {   // (below, the loop finds no match: lz4hc goes straight to the last literals)
+        const uint32_t mflimit = n - 12;
+        while (ip <= mflimit) {
+            const int llen = (int)(ip - anchor);
+            int best_mlen, best_off, cur, last;
+            int fmLen, fmOff;
+            longer(ip, 3, fmLen, fmOff);
+            if (fmLen == 0) { ++ip; continue; }
+            if (fmLen > suff) {   // good enough: immediate encoding
+                if (!hc_encode(s, d, ip, op, anchor, fmLen, ip - (uint32_t)fmOff, limit, cap)) return 0;
+                continue;
+            }
+            WAVE_SYNC();
+            if (L < 4) {   // literals at the first positions
+                O.mlen[L] = 1; O.off[L] = 0; O.litlen[L] = llen + (int)L; O.price[L] = hc_lit_price(llen + (int)L);
+            }
+            for (int b0 = 4; b0 <= fmLen; b0 += 64) {   // the first match
+                const int ml = b0 + (int)L;
+                if (ml <= fmLen) {
+                    O.mlen[ml] = ml; O.off[ml] = (uint16_t)fmOff; O.litlen[ml] = llen; O.price[ml] = hc_seq_price(llen, ml);
+                }
+            }
+            last = fmLen;
+            trailing(last);
+            for (cur = 1; cur < last; cur++) {
+                if (ip + (uint32_t)cur > mflimit) break;
+                const int pc = (int)uni((uint32_t)O.price[cur]);
+                const int pc1 = (int)uni((uint32_t)O.price[cur + 1]);
+                if (fullUpdate) {
+                    if (pc1 <= pc && (int)uni((uint32_t)O.price[cur + 4]) < pc + 3) continue;
+                } else {
+                    if (pc1 <= pc) continue;
+                }
+                int nmLen, nmOff;
+                longer(ip + (uint32_t)cur, fullUpdate ? 3 : last - cur, nmLen, nmOff);
+                if (!nmLen) continue;
+                if (nmLen > suff || nmLen + cur >= kOptNum) {   // immediate encoding
+                    best_mlen = nmLen;
+                    best_off = nmOff;
+                    last = cur + 1;
+                    goto encode;
+                }
+                {   // before the match: literals after the path to cur
+                    const int bl = (int)uni((uint32_t)O.litlen[cur]);
+                    if (L >= 1 && L <= 3) {
+                        const int price = pc - hc_lit_price(bl) + hc_lit_price(bl + (int)L);
+                        const int pos = cur + (int)L;
+                        if (price < O.price[pos]) {
+                            O.mlen[pos] = 1; O.off[pos] = 0; O.litlen[pos] = bl + (int)L; O.price[pos] = price;
+                        }
+                    }
+                    WAVE_SYNC();
+                }
+                {   // the match at cur, one lane per length
+                    const int mlc = (int)uni((uint32_t)O.mlen[cur]);
+                    int ll, basePrice;
+                    if (mlc == 1) {
+                        ll = (int)uni((uint32_t)O.litlen[cur]);
+                        basePrice = cur > ll ? (int)uni((uint32_t)O.price[cur - ll]) : 0;
+                    } else {
+                        ll = 0;
+                        basePrice = pc;
+                    }
+                    const int lastPre = last;
+                    bool lastTaken = false;
+                    for (int b0 = 4; b0 <= nmLen; b0 += 64) {
+                        const int ml = b0 + (int)L;
+                        const int pos = cur + ml;
+                        bool take = false;
+                        if (ml <= nmLen) {
+                            const int price = basePrice + hc_seq_price(ll, ml);
+                            take = pos > lastPre + 3 || price <= O.price[pos];
+                            if (take) {
+                                O.mlen[pos] = ml; O.off[pos] = (uint16_t)nmOff; O.litlen[pos] = ll; O.price[pos] = price;
+                            }
+                        }
+                        if (ballot(take && ml == nmLen)) lastTaken = true;
+                    }
+                    if (lastTaken && lastPre < cur + nmLen) last = cur + nmLen;
+                    trailing(last);
+                }
+            }
+            best_mlen = (int)uni((uint32_t)O.mlen[last]);
+            best_off = (int)uni((uint32_t)O.off[last]);
+            cur = last - best_mlen;
+        encode:
+            {   // reverse traversal: the shortest path's sequences
+                int cp = cur, sml = best_mlen, soff = best_off;
+                for (;;) {
+                    const int nml = (int)uni((uint32_t)O.mlen[cp]);
+                    const int noff = (int)uni((uint32_t)O.off[cp]);
+                    WAVE_SYNC();
+                    if (L == 0) { O.mlen[cp] = sml; O.off[cp] = (uint16_t)soff; }
+                    WAVE_SYNC();
+                    sml = nml;
+                    soff = noff;
+                    if (nml > cp) break;
+                    cp -= nml;
+                }
+            }
+            {
+                int rPos = 0;
+                while (rPos < last) {
+                    const int ml = (int)uni((uint32_t)O.mlen[rPos]);
+                    const int off = (int)uni((uint32_t)O.off[rPos]);
+                    if (ml == 1) { ++ip; ++rPos; continue; }
+                    rPos += ml;
+                    if (!hc_encode(s, d, ip, op, anchor, ml, ip - (uint32_t)off, limit, cap)) return 0;
+                }
+            }
+        }
+    }
+    {   // last literals
+        const uint32_t run = n - anchor;
+        const uint32_t llAdd = (run + 255 - 15) / 255;
+        if (limit && (uint64_t)op + 1 + llAdd + run > cap) return 0;
+        uint32_t o = op;
+        if (run >= 15) {
+            if (L == 0) d[o] = (uint8_t)(15u << 4);
+            ++o;
+            const uint32_t ext = (run - 15) / 255 + 1, rem = (run - 15) % 255;
+            for (uint32_t c = 0; c < ext; c += 64)
+                if (c + L < ext) d[o + c + L] = (uint8_t)(c + L + 1 < ext ? 255u : rem);
+            o += ext;
+        } else {
+            if (L == 0) d[o] = (uint8_t)(run << 4);
+            ++o;
+        }
+        for (uint32_t c = 0; c < run; c += 64)
+            if (c + L < run) d[o + c + L] = s[anchor + c + L];
+        return (int32_t)(o + run);
+    }
+}
+
 // cap of a block: capOverride, or n (0xFFFFFFFF, lz4mt) or n - 1 (0xFFFFFFFE, -BD)
 __device__ __forceinline__ uint32_t hc_cap(uint32_t n, uint32_t capOverride) {
     return capOverride == 0xFFFFFFFFu ? n : capOverride == 0xFFFFFFFEu ? n - 1 : capOverride;
@@ -549,6 +770,26 @@ __global__ void __launch_bounds__(64) k_encode_hc(const uint8_t* __restrict__ sr
     const uint32_t cap = hc_cap(n, capOverride);   // lz4mt: cap = n; -BD: n - 1
     HcBlock B{(g_cu8*)src + off, n, (g_cu16*)delta + off, maxAttempts, maxAttempts > 128};
     const int32_t r = encode_block_hc(B, (g_u8*)slots + (uint64_t)b * slotStride, cap);
+    if (laneid() == 0) csize[b] = r;
+}
+
+// LZ4-HC levels 10..12: one wave per block, the price table in LDS (57 KiB)
+__global__ void __launch_bounds__(64) k_encode_hc_opt(const uint8_t* __restrict__ src, uint64_t srcSize,
+                                                      uint32_t blockSize, uint8_t* __restrict__ slots,
+                                                      uint64_t slotStride, uint32_t capOverride,
+                                                      const uint16_t* __restrict__ delta, uint32_t nbSearches,
+                                                      int32_t sufficientLen, int32_t fullUpdate,
+                                                      int32_t* __restrict__ csize) {
+    __shared__ int32_t sPrice[kOptEntries], sLitlen[kOptEntries], sMlen[kOptEntries];
+    __shared__ uint16_t sOff[kOptEntries];
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
+    const uint32_t cap = hc_cap(n, capOverride);
+    HcBlock B{(g_cu8*)src + off, n, (g_cu16*)delta + off, nbSearches, true};   // pattern analysis always on
+    const HcOpt O{(l_i32*)sPrice, (l_i32*)sLitlen, (l_i32*)sMlen, (l_u16*)sOff};
+    const int32_t r = encode_block_hc_opt(B, (g_u8*)slots + (uint64_t)b * slotStride, cap, O, sufficientLen,
+                                          fullUpdate != 0);
     if (laneid() == 0) csize[b] = r;
 }
 
@@ -739,11 +980,12 @@ hipError_t launch_encode_hc_bd(const uint8_t* src, uint64_t srcSize, uint32_t bl
     return hipGetLastError();
 }
 
-// level -> maxNbAttempts (lz4 1.9.3 clTable, levels 1..9; < 1 = default 9)
+// level -> maxNbAttempts / nbSearches (lz4 1.9.3 clTable; < 1 = default 9,
+// > 12 = LZ4HC_CLEVEL_MAX)
 uint32_t hc_attempts(int level) {
-    static const uint32_t kA[10] = {2, 2, 2, 4, 8, 16, 32, 64, 128, 256};
+    static const uint32_t kA[13] = {2, 2, 2, 4, 8, 16, 32, 64, 128, 256, 96, 512, 16384};
     if (level < 1) level = 9;
-    return level > 9 ? 0u : kA[level];
+    return kA[level > 12 ? 12 : level];
 }
 
 // stream length of the split parse (LZ4MT_AMD_HC_SUB_KIB, default 256; 0 = off)
@@ -782,6 +1024,13 @@ hipError_t launch_encode_hc(const uint8_t* src, uint64_t srcSize, uint32_t block
     if (att == 0) return hipErrorInvalidValue;
     if (nBlocks == 0) return hipSuccess;
     hipLaunchKernelGGL(k_hc_prev, dim3(nBlocks), dim3(kPrevThreads), 0, st, src, srcSize, blockSize, delta);
+    if (level >= 10) {   // the optimal parser: target length 64 / 128 / LZ4_OPT_NUM, full update at 12
+        const int lv = level > 12 ? 12 : level;
+        hipLaunchKernelGGL(k_encode_hc_opt, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots,
+                           slotStride, capOverride, (const uint16_t*)delta, att,
+                           lv == 10 ? 64 : lv == 11 ? 128 : kOptNum, lv == 12 ? 1 : 0, csize);
+        return hipGetLastError();
+    }
     const uint32_t sm = hc_smax(blockSize), sub = hc_split_sub();
     if (splitWs && sm && slotStride >= blockSize) {   // large blocks: split parse, whole-block re-run where it fails
         const HcSplitWs w = carve_split(splitWs, nBlocks, blockSize);

@@ -82,12 +82,11 @@ def compress_block(data, cap=None):
 
 
 def compress_block_hc(data, cap=None, level=9):
-    """LZ4_compressHC2_limitedOutput(src, dst, n, cap, level) restated (levels 1..9); b'' when it does not fit."""
+    """LZ4_compressHC2_limitedOutput(src, dst, n, cap, level) restated (levels 1..9 hashChain,
+    10..12 and above the optimal parser); b'' when it does not fit."""
     cap = len(data) if cap is None else cap
     dst = ctypes.create_string_buffer(max(cap, lib.orc_lz4_compress_bound(len(data))) + 16)
     n = lib.orc_lz4hc_compress(_buf(data), dst, len(data), cap, level)
-    if n < 0:
-        raise ValueError("HC levels above 9 (the optimal parser) are not restated")
     return dst.raw[:n]
 
 

@@ -1,4 +1,4 @@
-"""GPU parity for LZ4-HC (compression levels 3..9), SURVEY.md §8(f) #3.
+"""GPU parity for LZ4-HC (compression levels 3..12), SURVEY.md §8(f) #3.
 
 The reference selects LZ4_compressHC2_limitedOutput(src, dst, n, cap = n,
 level) for ctx.compressionLevel >= 3 (src/main.cpp:778-785) and stores a
@@ -106,8 +106,24 @@ def test_hc_blocks_fuzz_vs_oracle():
                     (seed, len(d), level, cap)
 
 
+def test_hc_opt_blocks_fuzz_vs_oracle():
+    """Levels 10..12 (LZ4HC_compress_optimal: price table, chain swap, full
+    update at 12) and 17 (the reference CLI's -A, clamped to 12)."""
+    for seed in range(10):
+        rnd = random.Random(100 + seed)
+        d = _mixed(rnd.choice([12, 13, 14, 100, 5000, 65547, 200_000]), 100 + seed)
+        for level in (10, 11, 12, 17):
+            for cap in (len(d), len(d) - 1, len(d) // 3):
+                assert L.compress_block(d, cap, level=level) == oracle.compress_block_hc(d, cap, level), \
+                    (seed, len(d), level, cap)
+    for d in (oracle.gen_synthetic(300_000, 5), bytes(100_000), oracle.gen_random(70_000, 4)):
+        for level in (10, 12):
+            assert L.compress_block(d, len(d), level=level) == oracle.compress_block_hc(d, len(d), level), level
+
+
 @pytest.mark.parametrize("bid,sck,bck,level", [(4, True, True, 9), (5, False, True, 3), (7, True, False, 9),
-                                               (6, False, False, 6)])
+                                               (6, False, False, 6), (5, True, True, 12), (6, False, True, 10),
+                                               (5, False, True, 17)])
 def test_hc_frames_device(bid, sck, bck, level):
     data = oracle.gen_synthetic(3 << 20, 7) + bd_input(2 << 20, 8) + bytes(300_000) + oracle.gen_random(70_000, 2)
     want = hc_frame(data, bid, sck, bck, level)
@@ -115,6 +131,19 @@ def test_hc_frames_device(bid, sck, bck, level):
     assert host(fr) == want
     out, r = L.decompress_frame(fr)
     assert r == 0 and host(out) == data
+
+
+@pytest.mark.parametrize("mode", ["DEVICE", "SEQUENTIAL"])
+def test_hc_opt_callback_api(mode):
+    """lz4mtCompress at ctx.compressionLevel = 12 (the optimal parser) through
+    the batch engine and through the GPU block operator per block."""
+    m = {"DEVICE": L.MODE_DEVICE, "SEQUENTIAL": L.MODE_SEQUENTIAL}[mode]
+    data = oracle.gen_synthetic(600_000, 19) + bd_input(300_000, 20)
+    r, frame = L.compress(data, L.make_sd(5, True, True), mode=m, level=12)
+    assert r == 0, L.result_to_string(r)
+    assert frame == hc_frame(data, 5, True, True, 12), mode
+    r, out, _ = L.decompress(frame, len(data) + 64, mode=m)
+    assert r == 0 and out == data
 
 
 @pytest.mark.parametrize("mode", ["DEVICE", "PARALLEL", "SEQUENTIAL"])
