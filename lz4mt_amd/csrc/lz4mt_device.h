@@ -128,6 +128,7 @@ hipError_t launch_encode_hc(const uint8_t* src, uint64_t srcSize, uint32_t block
                             int32_t* csize, hipStream_t st, uint8_t* splitWs = nullptr);
 uint32_t hc_split_sub();
 uint64_t hc_split_bytes(uint64_t nBlocks, uint32_t blockSize);
+uint64_t hc_ws_bytes(uint64_t nBlocks, uint32_t blockSize, int level);   // splitWs size for a level
 uint32_t hc_attempts(int level);   // lz4hc nbSearches of a level (> 12 = 12)
 // -BD at level >= 3: segments [begin[k], end[k]) of src (begin >= -64 KiB),
 // blockSeg[b] = block b's segment; delta0 = chain scratch for src[0], with

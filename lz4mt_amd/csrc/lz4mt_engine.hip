@@ -74,7 +74,7 @@ CompressWs carve_compress(uint8_t* base, uint64_t nb, uint64_t bm, int level = 0
     w.slots = take(nb * bm + 64);
     // (-BD: 64 Ki entries more, for a segment that starts in the history before src)
     w.delta = level >= 3 ? reinterpret_cast<uint16_t*>(take((nb * bm + 65536) * 2 + 64)) : nullptr;
-    const uint64_t hs = level >= 3 ? hc_split_bytes(nb, (uint32_t)bm) : 0;
+    const uint64_t hs = level >= 3 ? hc_ws_bytes(nb, (uint32_t)bm, level) : 0;
     w.hcSplit = hs ? take(hs) : nullptr;
     w.csize = reinterpret_cast<int32_t*>(take((nb + 1) * 4));
     w.bsum = reinterpret_cast<uint32_t*>(take((nb + 1) * 4));
@@ -426,7 +426,7 @@ extern "C" int lz4mtHipCompressBlock(const char* src, char* dst, int isize, int 
     uint64_t outMax = (uint64_t)std::min(maxOutputSize, bound) + 16;
     // LZ4-HC on a large block: the split parse (one wave per 256 KiB stream)
     // writes each stream at its offset in an output of at least isize bytes
-    const uint64_t splitBytes = hc ? hc_split_bytes(1, (uint32_t)std::max(isize, 1)) : 0;
+    const uint64_t splitBytes = hc ? hc_ws_bytes(1, (uint32_t)std::max(isize, 1), compressionLevel) : 0;
     if (splitBytes) outMax = std::max<uint64_t>(outMax, (uint64_t)isize + 16);
     if (!g_blk->ensure((uint64_t)isize, outMax)) return -1;
     if (hc && !g_blk->ensure_delta((uint64_t)isize)) return -1;

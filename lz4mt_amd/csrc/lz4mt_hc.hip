@@ -571,35 +571,50 @@ __device__ int32_t encode_block_hc(const HcBlock& B, g_u8* d, uint32_t cap, uint
 // 17, src/main.cpp:377): lz4 1.9.3's LZ4HC_compress_optimal, restated in
 // oracle/lz4hc_oracle.c (hc_compress_optimal).  One wave per block; the
 // parser state is wave-uniform, its price table (LZ4_OPT_NUM + 3 entries)
-// sits in LDS as four arrays, and the lanes run the searches' counts, the
-// price updates of a match (one lane per match length) and the byte writes.
+// is four arrays in a per-block scratch, and the lanes run the searches'
+// counts, the price updates of a match (one lane per match length) and the
+// byte writes.
 // ---------------------------------------------------------------------------
 constexpr int kOptNum = 4096;                 // LZ4_OPT_NUM
 constexpr int kOptEntries = kOptNum + 3 + 1;  // + TRAILING_LITERALS (+ pad)
-typedef __attribute__((address_space(3))) int32_t l_i32;
-typedef __attribute__((address_space(3))) uint16_t l_u16;
-
-struct HcOpt {   // opt[] of LZ4HC_compress_optimal, structure of arrays
-    l_i32* price;
-    l_i32* litlen;
-    l_i32* mlen;
-    l_u16* off;
+// opt[] of LZ4HC_compress_optimal, structure of arrays, in LDS (AS 3) or in
+// a per-block global scratch (AS 1).  The wave reads back what its lanes
+// wrote: uniform reads are relaxed atomic loads, so they stay vector loads
+// (never the scalar cache, which does not see vector stores).
+template <int AS>
+struct HcOpt {
+    typedef __attribute__((address_space(AS))) int32_t i32;
+    typedef __attribute__((address_space(AS))) uint16_t u16;
+    i32* price;
+    i32* litlen;
+    i32* mlen;
+    u16* off;
+    template <class P>
+    static __device__ __forceinline__ int rd(P p) { return (int)uni((uint32_t)__atomic_load_n(p, __ATOMIC_RELAXED)); }
 };
+constexpr uint64_t kOptBlockBytes = (uint64_t)kOptEntries * 14 + 256;   // one block's scratch (AS 1)
 
 __device__ __forceinline__ int hc_lit_price(int litlen) { return litlen + (litlen >= 15 ? 1 + (litlen - 15) / 255 : 0); }
 __device__ __forceinline__ int hc_seq_price(int litlen, int mlen) {
     return 3 + hc_lit_price(litlen) + (mlen >= 19 ? 1 + (mlen - 19) / 255 : 0);
 }
 
-// LZ4HC_compress_optimal over the block (fresh state, favorCompressionRatio);
-// 0 = does not fit cap (store raw)
-__device__ int32_t encode_block_hc_opt(const HcBlock& B, g_u8* d, uint32_t cap, const HcOpt& O, int suff,
-                                       bool fullUpdate) {
+// LZ4HC_compress_optimal (favorCompressionRatio) from the loop-top state st;
+// MODE 0: to the block end (kHcEnd, or kHcFail when the output does not fit
+// cap); 1 / 2: the split parse's hooks (HcHooks), as in hc_parse.  Its loop
+// top has the same property: with anchor == ip the literal run is empty, the
+// chain is a function of the input and the price table is rebuilt from ip,
+// so two parses there with the same ip write the same bytes from then on.
+template <int MODE, int AS>
+__device__ HcState hc_opt_parse(const HcBlock& B, g_u8* d, uint32_t cap, bool limit, HcState st, const HcHooks& hk,
+                                const HcOpt<AS>& O, int suff, bool fullUpdate, bool fresh = false) {
+    typedef HcOpt<AS> OT;
     const uint32_t L = laneid();
     const uint32_t n = B.n;
     g_cu8* s = B.s;
-    const bool limit = (uint64_t)cap < (uint64_t)n + n / 255 + 16;
-    uint32_t ip = 0, anchor = 0, op = 0;
+    uint32_t ip = st.ip, anchor = st.anchor, op = st.op;
+    uint32_t cnt = 0, k = 0, lastHead = 0;
+    if (MODE == 2) lastHead = hk.nR ? hk.np[hk.nR - 1] : 0u;
     if (suff >= kOptNum) suff = kOptNum - 1;
     // FindLongerMatch: a match longer than minLen at p (pattern analysis and chain swap on)
     auto longer = [&](uint32_t p, int minLen, int& len, int& off) {
@@ -610,23 +625,38 @@ __device__ int32_t encode_block_hc_opt(const HcBlock& B, g_u8* d, uint32_t cap, 
     };
     auto trailing = [&](int last) {   // literals after the last match position
         WAVE_SYNC();
-        const int p0 = (int)uni((uint32_t)O.price[last]);
+        const int p0 = OT::rd(&O.price[last]);
         if (L >= 1 && L <= 3) {
             O.mlen[last + L] = 1; O.off[last + L] = 0; O.litlen[last + L] = (int)L;
             O.price[last + L] = p0 + hc_lit_price((int)L);
         }
         WAVE_SYNC();
     };
-    if (n >= 13) {   // (below, the loop finds no match: lz4hc goes straight to the last literals)
-        const uint32_t mflimit = n - 12;
+    if (!(fresh && n < 13)) {   // (a fresh block below 13 bytes has no match: straight to the last literals)
+        const uint32_t mflimit = n >= 12 ? n - 12 : 0;
         while (ip <= mflimit) {
+            if (MODE == 1) {
+                if (anchor == ip) {
+                    if (L == 0) { hk.hp[cnt] = ip; hk.ho[cnt] = op; }
+                    ++cnt;
+                }
+                if (cnt == hk.R || ip >= hk.hlim) return HcState{ip, anchor, op, kHcRun, cnt};
+            }
+            if (MODE == 2 && ip >= hk.xlo) {
+                if (ip > lastHead) return HcState{ip, anchor, op, kHcFail, cnt};
+                if (anchor == ip) {
+                    while (hk.np[k] < ip) ++k;
+                    if (hk.np[k] == ip) return HcState{ip, anchor, op, kHcSync};
+                }
+            }
             const int llen = (int)(ip - anchor);
             int best_mlen, best_off, cur, last;
             int fmLen, fmOff;
             longer(ip, 3, fmLen, fmOff);
             if (fmLen == 0) { ++ip; continue; }
             if (fmLen > suff) {   // good enough: immediate encoding
-                if (!hc_encode(s, d, ip, op, anchor, fmLen, ip - (uint32_t)fmOff, limit, cap)) return 0;
+                if (!hc_encode(s, d, ip, op, anchor, fmLen, ip - (uint32_t)fmOff, limit, cap))
+                    return HcState{ip, anchor, op, kHcFail, cnt};
                 continue;
             }
             WAVE_SYNC();
@@ -643,10 +673,10 @@ __device__ int32_t encode_block_hc_opt(const HcBlock& B, g_u8* d, uint32_t cap, 
             trailing(last);
             for (cur = 1; cur < last; cur++) {
                 if (ip + (uint32_t)cur > mflimit) break;
-                const int pc = (int)uni((uint32_t)O.price[cur]);
-                const int pc1 = (int)uni((uint32_t)O.price[cur + 1]);
+                const int pc = OT::rd(&O.price[cur]);
+                const int pc1 = OT::rd(&O.price[cur + 1]);
                 if (fullUpdate) {
-                    if (pc1 <= pc && (int)uni((uint32_t)O.price[cur + 4]) < pc + 3) continue;
+                    if (pc1 <= pc && OT::rd(&O.price[cur + 4]) < pc + 3) continue;
                 } else {
                     if (pc1 <= pc) continue;
                 }
@@ -660,7 +690,7 @@ __device__ int32_t encode_block_hc_opt(const HcBlock& B, g_u8* d, uint32_t cap, 
                     goto encode;
                 }
                 {   // before the match: literals after the path to cur
-                    const int bl = (int)uni((uint32_t)O.litlen[cur]);
+                    const int bl = OT::rd(&O.litlen[cur]);
                     if (L >= 1 && L <= 3) {
                         const int price = pc - hc_lit_price(bl) + hc_lit_price(bl + (int)L);
                         const int pos = cur + (int)L;
@@ -671,11 +701,11 @@ __device__ int32_t encode_block_hc_opt(const HcBlock& B, g_u8* d, uint32_t cap, 
                     WAVE_SYNC();
                 }
                 {   // the match at cur, one lane per length
-                    const int mlc = (int)uni((uint32_t)O.mlen[cur]);
+                    const int mlc = OT::rd(&O.mlen[cur]);
                     int ll, basePrice;
                     if (mlc == 1) {
-                        ll = (int)uni((uint32_t)O.litlen[cur]);
-                        basePrice = cur > ll ? (int)uni((uint32_t)O.price[cur - ll]) : 0;
+                        ll = OT::rd(&O.litlen[cur]);
+                        basePrice = cur > ll ? OT::rd(&O.price[cur - ll]) : 0;
                     } else {
                         ll = 0;
                         basePrice = pc;
@@ -699,15 +729,15 @@ __device__ int32_t encode_block_hc_opt(const HcBlock& B, g_u8* d, uint32_t cap, 
                     trailing(last);
                 }
             }
-            best_mlen = (int)uni((uint32_t)O.mlen[last]);
-            best_off = (int)uni((uint32_t)O.off[last]);
+            best_mlen = OT::rd(&O.mlen[last]);
+            best_off = OT::rd(&O.off[last]);
             cur = last - best_mlen;
         encode:
             {   // reverse traversal: the shortest path's sequences
                 int cp = cur, sml = best_mlen, soff = best_off;
                 for (;;) {
-                    const int nml = (int)uni((uint32_t)O.mlen[cp]);
-                    const int noff = (int)uni((uint32_t)O.off[cp]);
+                    const int nml = OT::rd(&O.mlen[cp]);
+                    const int noff = OT::rd(&O.off[cp]);
                     WAVE_SYNC();
                     if (L == 0) { O.mlen[cp] = sml; O.off[cp] = (uint16_t)soff; }
                     WAVE_SYNC();
@@ -720,19 +750,22 @@ __device__ int32_t encode_block_hc_opt(const HcBlock& B, g_u8* d, uint32_t cap, 
             {
                 int rPos = 0;
                 while (rPos < last) {
-                    const int ml = (int)uni((uint32_t)O.mlen[rPos]);
-                    const int off = (int)uni((uint32_t)O.off[rPos]);
+                    const int ml = OT::rd(&O.mlen[rPos]);
+                    const int off = OT::rd(&O.off[rPos]);
                     if (ml == 1) { ++ip; ++rPos; continue; }
                     rPos += ml;
-                    if (!hc_encode(s, d, ip, op, anchor, ml, ip - (uint32_t)off, limit, cap)) return 0;
+                    if (!hc_encode(s, d, ip, op, anchor, ml, ip - (uint32_t)off, limit, cap))
+                        return HcState{ip, anchor, op, kHcFail, cnt};
                 }
             }
         }
     }
+    if (MODE == 1) return HcState{ip, anchor, op, kHcRun, cnt};   // past mflimit: MODE 0 writes the last literals
+    if (MODE == 2) return HcState{ip, anchor, op, kHcFail, cnt};
     {   // last literals
         const uint32_t run = n - anchor;
         const uint32_t llAdd = (run + 255 - 15) / 255;
-        if (limit && (uint64_t)op + 1 + llAdd + run > cap) return 0;
+        if (limit && (uint64_t)op + 1 + llAdd + run > cap) return HcState{ip, anchor, op, kHcFail, cnt};
         uint32_t o = op;
         if (run >= 15) {
             if (L == 0) d[o] = (uint8_t)(15u << 4);
@@ -747,8 +780,17 @@ __device__ int32_t encode_block_hc_opt(const HcBlock& B, g_u8* d, uint32_t cap, 
         }
         for (uint32_t c = 0; c < run; c += 64)
             if (c + L < run) d[o + c + L] = s[anchor + c + L];
-        return (int32_t)(o + run);
+        return HcState{n, n, o + run, kHcEnd};
     }
+}
+
+// the optimal parse of a whole block; 0 = does not fit cap (store raw)
+template <int AS>
+__device__ int32_t encode_block_hc_opt(const HcBlock& B, g_u8* d, uint32_t cap, const HcOpt<AS>& O, int suff,
+                                       bool fullUpdate) {
+    const bool limit = (uint64_t)cap < (uint64_t)B.n + B.n / 255 + 16;
+    const HcState r = hc_opt_parse<0>(B, d, cap, limit, HcState{0, 0, 0, 0, 0}, HcHooks{}, O, suff, fullUpdate, true);
+    return r.status == kHcEnd ? (int32_t)r.op : 0;
 }
 
 // cap of a block: capOverride, or n (0xFFFFFFFF, lz4mt) or n - 1 (0xFFFFFFFE, -BD)
@@ -773,21 +815,31 @@ __global__ void __launch_bounds__(64) k_encode_hc(const uint8_t* __restrict__ sr
     if (laneid() == 0) csize[b] = r;
 }
 
-// LZ4-HC levels 10..12: one wave per block, the price table in LDS (57 KiB)
-__global__ void __launch_bounds__(64) k_encode_hc_opt(const uint8_t* __restrict__ src, uint64_t srcSize,
-                                                      uint32_t blockSize, uint8_t* __restrict__ slots,
-                                                      uint64_t slotStride, uint32_t capOverride,
-                                                      const uint16_t* __restrict__ delta, uint32_t nbSearches,
-                                                      int32_t sufficientLen, int32_t fullUpdate,
-                                                      int32_t* __restrict__ csize) {
-    __shared__ int32_t sPrice[kOptEntries], sLitlen[kOptEntries], sMlen[kOptEntries];
-    __shared__ uint16_t sOff[kOptEntries];
+// price table number t of a scratch of kOptBlockBytes-sized tables
+__device__ __forceinline__ HcOpt<1> hc_opt_at(uint8_t* ws, uint64_t t) {
+    typedef HcOpt<1> OT;
+    uint8_t* w = ws + t * kOptBlockBytes;
+    return OT{(OT::i32*)w, (OT::i32*)(w + 4 * kOptEntries), (OT::i32*)(w + 8 * kOptEntries),
+              (OT::u16*)(w + 12 * kOptEntries)};
+}
+
+// LZ4-HC levels 10..12: one wave per block, the price table in a global
+// scratch of kOptBlockBytes per block (L2-resident; in LDS it would hold a
+// CU to two of these waves)
+__global__ void __launch_bounds__(64) k_encode_hc_opt_g(const uint8_t* __restrict__ src, uint64_t srcSize,
+                                                        uint32_t blockSize, uint8_t* __restrict__ slots,
+                                                        uint64_t slotStride, uint32_t capOverride,
+                                                        const uint16_t* __restrict__ delta, uint32_t nbSearches,
+                                                        int32_t sufficientLen, int32_t fullUpdate, uint8_t* optWs,
+                                                        uint32_t tableStride, const uint32_t* __restrict__ redo,
+                                                        int32_t* __restrict__ csize) {
     const uint32_t b = blockIdx.x;
+    if (redo && !redo[b]) return;   // done by the split parse
     const uint64_t off = (uint64_t)b * blockSize;
     const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
     const uint32_t cap = hc_cap(n, capOverride);
     HcBlock B{(g_cu8*)src + off, n, (g_cu16*)delta + off, nbSearches, true};   // pattern analysis always on
-    const HcOpt O{(l_i32*)sPrice, (l_i32*)sLitlen, (l_i32*)sMlen, (l_u16*)sOff};
+    const HcOpt<1> O = hc_opt_at(optWs, (uint64_t)b * tableStride);
     const int32_t r = encode_block_hc_opt(B, (g_u8*)slots + (uint64_t)b * slotStride, cap, O, sufficientLen,
                                           fullUpdate != 0);
     if (laneid() == 0) csize[b] = r;
@@ -874,6 +926,62 @@ __global__ void __launch_bounds__(64) k_hc_exit(const uint8_t* __restrict__ src,
             r = hc_parse<2>(B, d, end - M, true, st, hk);
         } else {
             r = hc_parse<0>(B, d, end - M, true, st, HcHooks{});
+        }
+    }
+    if (laneid() == 0) w.st2[id] = r;
+}
+
+// The split parse of the optimal parser (levels >= 10): the same streams,
+// meeting points and join as above, each stream with its own price table
+__global__ void __launch_bounds__(64) k_hc_opt_heads(const uint8_t* __restrict__ src, uint64_t srcSize,
+                                                     uint32_t blockSize, uint8_t* __restrict__ slots,
+                                                     uint64_t slotStride, const uint16_t* __restrict__ delta,
+                                                     uint32_t nbSearches, int32_t suff, int32_t full, uint32_t sub,
+                                                     uint32_t smax, HcSplitWs w, uint8_t* optT) {
+    const uint32_t id = blockIdx.x, b = id / smax, j = id % smax;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
+    const uint32_t S = hc_streams(n, sub);
+    if (j == 0 || j >= S) return;
+    const uint32_t M = j * sub, end = j + 1 < S ? M + sub : n;
+    HcBlock B{(g_cu8*)src + off, n, (g_cu16*)delta + off, nbSearches, true};
+    HcHooks hk{};
+    hk.hp = (__attribute__((address_space(1))) uint32_t*)w.hp + (uint64_t)id * kHcHeads;
+    hk.ho = (__attribute__((address_space(1))) uint32_t*)w.ho + (uint64_t)id * kHcHeads;
+    hk.R = kHcHeads;
+    hk.hlim = M + sub / 4;
+    const HcState r = hc_opt_parse<1>(B, (g_u8*)slots + (uint64_t)b * slotStride + M, end - M, true,
+                                      HcState{M, M, 0, 0, 0}, hk, hc_opt_at(optT, id), suff, full != 0);
+    if (laneid() == 0) w.st1[id] = r;
+}
+
+__global__ void __launch_bounds__(64) k_hc_opt_exit(const uint8_t* __restrict__ src, uint64_t srcSize,
+                                                    uint32_t blockSize, uint8_t* __restrict__ slots,
+                                                    uint64_t slotStride, const uint16_t* __restrict__ delta,
+                                                    uint32_t nbSearches, int32_t suff, int32_t full, uint32_t sub,
+                                                    uint32_t smax, HcSplitWs w, uint8_t* optT) {
+    const uint32_t id = blockIdx.x, b = id / smax, j = id % smax;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)min<uint64_t>(blockSize, srcSize - off);
+    const uint32_t S = hc_streams(n, sub);
+    if (S == 1 || j >= S) return;
+    const uint32_t M = j * sub, end = j + 1 < S ? M + sub : n;
+    HcState st = j ? w.st1[id] : HcState{0, 0, 0, kHcRun, 0};
+    st.ip = uni(st.ip); st.anchor = uni(st.anchor); st.op = uni(st.op); st.status = uni(st.status);
+    HcState r = st;
+    if (st.status == kHcRun) {
+        HcBlock B{(g_cu8*)src + off, n, (g_cu16*)delta + off, nbSearches, true};
+        g_u8* d = (g_u8*)slots + (uint64_t)b * slotStride + M;
+        const HcOpt<1> O = hc_opt_at(optT, id);
+        if (j + 1 < S) {
+            const HcState nx = w.st1[id + 1];
+            HcHooks hk{};
+            hk.np = (const __attribute__((address_space(1))) uint32_t*)w.hp + (uint64_t)(id + 1) * kHcHeads;
+            hk.nR = nx.status == kHcFail ? 0u : uni(nx.cnt);
+            hk.xlo = M + sub;
+            r = hc_opt_parse<2>(B, d, end - M, true, st, hk, O, suff, full != 0);
+        } else {
+            r = hc_opt_parse<0>(B, d, end - M, true, st, HcHooks{}, O, suff, full != 0);
         }
     }
     if (laneid() == 0) w.st2[id] = r;
@@ -1006,6 +1114,17 @@ uint64_t hc_split_bytes(uint64_t nBlocks, uint32_t blockSize) {
     return streams * (2 * kHcHeads * 4 + 2 * sizeof(HcState)) + (nBlocks + 1) * 4 + 256;
 }
 
+// HC scratch of a launch: the split parse's records (levels 3..9), or the
+// optimal parser's price tables (levels >= 10)
+static uint64_t hc_opt_tables_at(uint64_t nBlocks, uint32_t blockSize) {   // after the split records
+    return (hc_split_bytes(nBlocks, blockSize) + 255) & ~uint64_t(255);
+}
+uint64_t hc_ws_bytes(uint64_t nBlocks, uint32_t blockSize, int level) {
+    if (level < 10) return hc_split_bytes(nBlocks, blockSize);
+    const uint64_t tables = std::max<uint64_t>(nBlocks, nBlocks * hc_smax(blockSize));   // one per stream (or block)
+    return hc_opt_tables_at(nBlocks, blockSize) + tables * kOptBlockBytes + 256;
+}
+
 static HcSplitWs carve_split(uint8_t* p, uint64_t nBlocks, uint32_t blockSize) {
     const uint64_t streams = nBlocks * hc_smax(blockSize);
     HcSplitWs w;
@@ -1026,9 +1145,27 @@ hipError_t launch_encode_hc(const uint8_t* src, uint64_t srcSize, uint32_t block
     hipLaunchKernelGGL(k_hc_prev, dim3(nBlocks), dim3(kPrevThreads), 0, st, src, srcSize, blockSize, delta);
     if (level >= 10) {   // the optimal parser: target length 64 / 128 / LZ4_OPT_NUM, full update at 12
         const int lv = level > 12 ? 12 : level;
-        hipLaunchKernelGGL(k_encode_hc_opt, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots,
-                           slotStride, capOverride, (const uint16_t*)delta, att,
-                           lv == 10 ? 64 : lv == 11 ? 128 : kOptNum, lv == 12 ? 1 : 0, csize);
+        const int32_t tl = lv == 10 ? 64 : lv == 11 ? 128 : kOptNum, fu = lv == 12 ? 1 : 0;
+        if (!splitWs) return hipErrorInvalidValue;   // hc_ws_bytes(nBlocks, blockSize, level) of price tables
+        uint8_t* optT = splitWs + hc_opt_tables_at(nBlocks, blockSize);
+        const uint32_t sm = hc_smax(blockSize), sub = hc_split_sub();
+        if (sm && slotStride >= blockSize) {   // large blocks: split parse, whole-block re-run where it fails
+            const HcSplitWs w = carve_split(splitWs, nBlocks, blockSize);
+            const uint32_t grid = nBlocks * sm;
+            hipLaunchKernelGGL(k_hc_opt_heads, dim3(grid), dim3(64), 0, st, src, srcSize, blockSize, slots,
+                               slotStride, (const uint16_t*)delta, att, tl, fu, sub, sm, w, optT);
+            hipLaunchKernelGGL(k_hc_opt_exit, dim3(grid), dim3(64), 0, st, src, srcSize, blockSize, slots,
+                               slotStride, (const uint16_t*)delta, att, tl, fu, sub, sm, w, optT);
+            hipLaunchKernelGGL(k_hc_join, dim3(nBlocks), dim3(256), 0, st, srcSize, blockSize, slots, slotStride,
+                               capOverride, sub, sm, w, csize);
+            hipLaunchKernelGGL(k_encode_hc_opt_g, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots,
+                               slotStride, capOverride, (const uint16_t*)delta, att, tl, fu, optT, sm,
+                               (const uint32_t*)w.redo, csize);
+            return hipGetLastError();
+        }
+        hipLaunchKernelGGL(k_encode_hc_opt_g, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots,
+                           slotStride, capOverride, (const uint16_t*)delta, att, tl, fu, optT, 1u,
+                           (const uint32_t*)nullptr, csize);
         return hipGetLastError();
     }
     const uint32_t sm = hc_smax(blockSize), sub = hc_split_sub();

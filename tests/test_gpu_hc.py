@@ -123,7 +123,7 @@ def test_hc_opt_blocks_fuzz_vs_oracle():
 
 @pytest.mark.parametrize("bid,sck,bck,level", [(4, True, True, 9), (5, False, True, 3), (7, True, False, 9),
                                                (6, False, False, 6), (5, True, True, 12), (6, False, True, 10),
-                                               (5, False, True, 17)])
+                                               (5, False, True, 17), (7, True, True, 12)])
 def test_hc_frames_device(bid, sck, bck, level):
     data = oracle.gen_synthetic(3 << 20, 7) + bd_input(2 << 20, 8) + bytes(300_000) + oracle.gen_random(70_000, 2)
     want = hc_frame(data, bid, sck, bck, level)
@@ -209,6 +209,25 @@ def test_hc_split_parse_vs_oracle(monkeypatch, sub, kind):
         assert host(fr) == want, (sub, kind, bid, level)
     out, r = L.decompress_frame(fr)
     assert r == 0 and host(out) == data
+
+
+@pytest.mark.parametrize("sub", ["64", "256", "0"])
+@pytest.mark.parametrize("kind", ["appf", "mixed", "runs", "random"])
+def test_hc_opt_split_parse_vs_oracle(monkeypatch, sub, kind):
+    """The optimal parser (levels >= 10) on the split path: one wave and one
+    price table per stream, spliced where the parses meet at a loop top
+    with anchor == ip (k_hc_opt_heads / k_hc_opt_exit / k_hc_join)."""
+    monkeypatch.setenv("LZ4MT_AMD_HC_SUB_KIB", sub)
+    data = _split_input(kind, (5 << 20) + 4321, 5)
+    for bid, level in ((7, 12), (6, 10)):
+        want = hc_frame(data, bid, False, True, level)
+        fr = L.compress_frame(dev(data), L.make_sd(bid, False, True), level=level)
+        assert host(fr) == want, (sub, kind, bid, level)
+    out, r = L.decompress_frame(fr)
+    assert r == 0 and host(out) == data
+    d = data[:(1 << 20) + 12345]
+    for cap in (len(d), len(d) - 1):
+        assert L.compress_block(d, cap, level=11) == oracle.compress_block_hc(d, cap, 11), (sub, kind, cap)
 
 
 @pytest.mark.parametrize("kind", ["appf", "mixed", "random"])

@@ -1,0 +1,9 @@
+# optimal parser with global price tables: HC parity tests, then benches at levels 10 / 12 (1 GiB and 8 GiB)
+set -euo pipefail
+out=gpurun_out/r02bc
+mkdir -p $out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_gpu_hc.py -m gpu > $out/tests.log 2>&1
+timeout -k 10 400 python3 bench.py --gib 1 --steps 1 --warmup 1 --level 10 --no-cpu-baseline > $out/hc10_1g.json 2>$out/hc10_1g.err
+timeout -k 10 400 python3 bench.py --gib 8 --steps 1 --warmup 1 --level 10 > $out/hc10.json 2>$out/hc10.err
+timeout -k 10 500 python3 bench.py --gib 8 --steps 1 --warmup 1 --level 12 > $out/hc12.json 2>$out/hc12.err
