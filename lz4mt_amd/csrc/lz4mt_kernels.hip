@@ -102,8 +102,8 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, int lane) {
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
-// mask of lanes <= L (L in [0,63])
-__device__ __forceinline__ uint64_t mask_le(uint32_t L) { return (L >= 63) ? ~0ull : ((2ull << L) - 1ull); }
+// mask of lanes <= L (L in [0,63]; at 63 the shift drops the bit: 0 - 1 = all)
+__device__ __forceinline__ uint64_t mask_le(uint32_t L) { return (2ull << L) - 1ull; }
 
 // Little-endian 32-bit read at an arbitrary byte address.  Only the aligned
 // dwords that hold requested bytes are touched, so it never reads a dword
