@@ -1,5 +1,5 @@
 """Time-boxed random differential campaign (run on the GPU box): random
-mixed inputs of random sizes, block sizes, flags and levels through the
+mixed inputs of random sizes, block sizes, flags, levels and block dependence through the
 device frame engine (lz4mtHipCompressFrame / lz4mtHipDecompressFrame), each
 frame compared byte for byte with the oracle's frame and each decode with the
 input.  Complements the fixed-seed tests with many more shapes.
@@ -16,6 +16,9 @@ import xxhash  # noqa: E402
 
 import lz4mt_amd as L  # noqa: E402
 import oracle  # noqa: E402
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden"))
+import make_golden as G  # noqa: E402  (-BD frames from liblz4 1.9.3 with the reference's call sequence)
 
 budget = float(sys.argv[1]) if len(sys.argv) > 1 else 240.0
 seed = int(sys.argv[2]) if len(sys.argv) > 2 else 1
@@ -99,11 +102,17 @@ while time.time() - t0 < budget:
     bid = rnd.randrange(4, 8)
     sck, bck = rnd.random() < 0.5, rnd.random() < 0.5
     level = rnd.choice([0, 0, 0, 1, 2, 3, 4, 6, 8, 9, 9, 10, 11, 12])
-    if level >= 10:
-        data = data[:3 << 20]   # the oracle's optimal parser is slow on the CPU
-    want = (oracle.compress_frame(data, oracle.params(bid, sck, bck)) if level < 3
-            else hc_frame(data, bid, sck, bck, level))
-    fr = L.compress_frame(dev(data), L.make_sd(bid, sck, bck), level=level)
+    bd = rnd.random() < 0.25   # -BD: expected frame from liblz4's stream API
+    if level >= 10 or (bd and level >= 3):
+        data = data[:3 << 20]   # the CPU side of the optimal parser / the HC stream is slow
+    if bd:   # 1 / 4 MiB fast blocks: the decodable contiguous stream (bugs not copied)
+        want = (G.bd_hc_frame_reference(data, bid, sck, bck) if level >= 3
+                else G.bd_frame_contiguous(data, bid, sck, bck) if bid >= 6
+                else G.bd_frame_reference(data, bid, sck, bck))
+    else:
+        want = (oracle.compress_frame(data, oracle.params(bid, sck, bck)) if level < 3
+                else hc_frame(data, bid, sck, bck, level))
+    fr = L.compress_frame(dev(data), L.make_sd(bid, sck, bck, block_dependence=bd), level=level)
     got = host(fr)
     ok = got == want
     if ok:
@@ -111,10 +120,11 @@ while time.time() - t0 < budget:
         ok = r == 0 and host(out) == data
     cases += 1
     nbytes += len(data)
-    by_level[level] = by_level.get(level, 0) + 1
+    key = f"{'BD' if bd else ''}{level}"
+    by_level[key] = by_level.get(key, 0) + 1
     if not ok:
-        fails.append((cases, len(data), bid, sck, bck, level))
-        print(f"MISMATCH case {cases}: n={len(data)} B{bid} sck={sck} bck={bck} level={level}", flush=True)
+        fails.append((cases, len(data), bid, sck, bck, level, bd))
+        print(f"MISMATCH case {cases}: n={len(data)} B{bid} sck={sck} bck={bck} level={level} bd={bd}", flush=True)
     if time.time() - last > 30:
         last = time.time()
         print(f"  {cases} cases, {nbytes / 2**20:.0f} MiB, {len(fails)} mismatches", flush=True)
