@@ -1,4 +1,4 @@
-"""HC encode kernel time (8 GiB App. F, 4 MiB blocks, levels 3 and 9; best of 2) for A/B of
+"""HC encode kernel time (8 GiB App. F, 4 MiB blocks, levels HC_LEVELS = 3,9,10,12; best of 2) for A/B of
 experiment builds: LZ4MT_AMD_LIB=<variant .so> python tools/hctime.py"""
 import ctypes
 import os
@@ -15,7 +15,7 @@ sd = L.make_sd(7, False, True)
 L.lib.lz4mtHipSetTiming(1)
 ms = (ctypes.c_float * 4)()
 res = []
-for level in (3, 9):
+for level in (int(v) for v in os.environ.get("HC_LEVELS", "3,9,10,12").split(",")):
     best, size = 1e9, 0
     for _ in range(2):
         fr = L.compress_frame(src, sd, level=level)
