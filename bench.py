@@ -34,17 +34,18 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import lz4mt_amd as L  # noqa: E402
-from lz4mt_amd import dist as D  # noqa: E402
+# torch, torch.distributed and lz4mt_amd (which loads the HIP library) are
+# imported in main(): with --gpus N > 1 and no WORLD_SIZE, the parent only
+# launches the N ranks and must not touch the GPU first.
+torch = dist = L = D = None
 
 GiB = float(1 << 30)
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -57,7 +58,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--gib", type=float, default=8.0, help="GiB per GPU")
+    p.add_argument("--gib", type=float, default=8.0, help="GiB per GPU (weak scaling, the default)")
+    p.add_argument("--total-gib", type=float, default=None,
+                   help="strong scaling: ONE buffer of this many GiB, block-sharded over the ranks "
+                        "(configs[3]: --total-gib 64 at 1/2/4/8 GPUs)")
     p.add_argument("--block-id", type=int, default=7, help="4..7 = 64 KiB..4 MiB")
     p.add_argument("--stream-checksum", action="store_true",
                    help="default lz4mt flags (FLG.2 content checksum, no block checksum) instead of -Sx -BX")
@@ -88,24 +92,30 @@ def _cpu_model():
 
 
 def usable_cores():
-    """Threads the reference's pool would get here: hardware_concurrency()
+    """Threads for the reference's pool here: hardware_concurrency()
     (src/lz4mt_compat.cpp, nPool = hw + 1, src/lz4mt.cpp:281), bounded by
-    this process's affinity, its cgroup CPU quota and the pool's thread
-    share (OMP_NUM_THREADS / MAX_JOBS on the GPU box) -- threads beyond the
-    CPUs the process may run on only contend."""
+    what this process may actually run on -- its CPU affinity, its cgroup
+    CPU quota and the box's per-job thread share (OMP_NUM_THREADS /
+    MAX_JOBS, set by the GPU pool to the lease's CPU share).  Threads beyond
+    that only contend.  Returns (threads, hardware_concurrency, limits) with
+    every limit seen and the one that set the count."""
     hw = os.cpu_count() or 1
-    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else hw
+    lim = {"hardware_concurrency": hw}
+    if hasattr(os, "sched_getaffinity"):
+        lim["affinity"] = len(os.sched_getaffinity(0))
     try:
         q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-        if q != "max":
-            n = min(n, max(1, int(int(q) / int(per))))
+        lim["cgroup_quota"] = None if q == "max" else max(1, int(int(q) / int(per)))
     except (OSError, ValueError):
         pass
     for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
         v = os.environ.get(var, "")
         if v.isdigit() and int(v) > 0:
-            n = min(n, int(v))
-    return max(1, n), hw
+            lim[var] = int(v)
+    cands = {k: v for k, v in lim.items() if isinstance(v, int)}
+    by = min(cands, key=lambda k: (cands[k], k != "hardware_concurrency"))
+    lim["limited_by"] = by
+    return max(1, cands[by]), hw, lim
 
 
 def cpu_baseline(mib, block_id, sck, level=0, bd=False):
@@ -120,14 +130,15 @@ def cpu_baseline(mib, block_id, sck, level=0, bd=False):
     compressBlockDependency is (src/lz4mt.cpp:460-538, 737-845), one LZ4
     stream over liblz4 (orc_bd_roundtrip).  Rank 0, N = 1, bounded sample."""
     import oracle
-    threads, hw = usable_cores()
+    threads, hw, limits = usable_cores()
     n = mib << 20
     buf = ctypes.create_string_buffer(n)
     oracle.lib.orc_gen_synthetic(buf, n, 42)
     p = oracle.params(block_id, stream_checksum=sck, block_checksum=not sck)
     lz = oracle.liblz4_codec()
     flags = ("default flags" if sck else "-Sx -BX") + (f" level {level}" if level >= 3 else "") + (" -BD" if bd else "")
-    line = {"unit": "GiB/s", "kind": "port", "hardware_concurrency": hw, "cpu_model": _cpu_model()}
+    line = {"unit": "GiB/s", "kind": "port", "hardware_concurrency": hw, "cpu_model": _cpu_model(),
+            "thread_limits": limits}
     if bd:
         if not lz:
             return None   # the stream API comes from liblz4 only
@@ -150,6 +161,12 @@ def cpu_baseline(mib, block_id, sck, level=0, bd=False):
         codec, codec_name = (lz[0], f"liblz4 {lz[1]}") if lz else (None, "oracle restatement")
     n1 = min(n, 256 << 20 if level < 3 else 64 << 20)
     tc1, td1, _ = oracle.pipeline_roundtrip(buf, n1, p, 1, codec)
+    # configs[0] as BASELINE.json states it: 256 MiB, 4 MiB blocks, one
+    # thread, XXH32 on -- the reference's default flags (content checksum)
+    d1 = None
+    if level < 3 and not sck:
+        pd = oracle.params(block_id, stream_checksum=True, block_checksum=False)
+        d1 = oracle.pipeline_roundtrip(buf, n1, pd, 1, codec)[:2]
     best = None
     for _ in range(3 if level < 3 else 1):
         tc, td, _ = oracle.pipeline_roundtrip(buf, n, p, threads, codec)
@@ -164,6 +181,10 @@ def cpu_baseline(mib, block_id, sck, level=0, bd=False):
         "compress_GiBps": round(n / GiB / tcN, 3), "decompress_GiBps": round(n / GiB / tdN, 3),
         "single_thread_compress_GiBps": round(n1 / GiB / tc1, 3),
         "single_thread_decompress_GiBps": round(n1 / GiB / td1, 3)})
+    if d1:
+        line["configs0_single_thread_default_flags"] = {
+            "sample": f"{n1 >> 20} MiB App.F, B{block_id}, default flags (FLG.2 content XXH32), one thread",
+            "compress_GiBps": round(n1 / GiB / d1[0], 3), "decompress_GiBps": round(n1 / GiB / d1[1], 3)}
     return line
 
 
@@ -196,11 +217,37 @@ def pmc_traffic(kernel, n, bm, flg):
             "source": "profiles/pmc_current.json (" + prof.get("tag", "?") + ")"}, None
 
 
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(a):
+    """--gpus N > 1 without a torch.distributed launcher: start one rank per
+    GPU as a CHILD process (python -m torch.distributed.run, rendezvous on
+    127.0.0.1) and exit with its status.  Nothing here has touched the GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
+    global torch, dist, L, D
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world} ranks were launched")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch as _torch
+    import torch.distributed as _dist
+    torch, dist = _torch, _dist
+    import lz4mt_amd as _L
+    from lz4mt_amd import dist as _D
+    L, D = _L, _D
     # LZ4MT_BENCH_BACKEND=gloo rehearses the N > 1 orchestration with several
     # ranks sharing the GPUs there are (gloo moves CUDA tensors through the
     # host); the measured multi-GPU path is RCCL, one rank per GPU
@@ -216,9 +263,13 @@ def main():
     stream = torch.cuda.current_stream()
 
     bm = 1 << (8 + 2 * a.block_id)
-    n = int(a.gib * GiB) // bm * bm
-    segs_per_rank = n // 65536
-    seed = (42 + rank * segs_per_rank * GOLDEN) % (1 << 64)   # rank r = shard r of one global stream
+    if a.total_gib is not None:   # strong scaling: rank r owns shard_blocks' range of ONE buffer
+        n_total = int(a.total_gib * GiB) // bm * bm
+        first_byte, n, _, _ = D.shard_blocks(n_total, bm, world, rank)
+    else:                         # weak scaling: --gib per rank, rank r = shard r of one global stream
+        n = int(a.gib * GiB) // bm * bm
+        first_byte, n_total = rank * n, n * world
+    seed = (42 + (first_byte // 65536) * GOLDEN) % (1 << 64)   # App. F segment index of the shard's start
     src = L.gen_synthetic(n, seed=seed, device=dev)
     sck = a.stream_checksum
     if sck and world > 1:
@@ -324,7 +375,7 @@ def main():
         tc, td, ts, tg, bad = t.tolist()
         ok = bad == 0.0 and stitched_ok
     K = a.steps
-    total = n * world * K
+    total = n_total * K
     comp_gibps = None if a.decompress_only else total / GiB / tc
     decomp_gibps = total / GiB / td
     value = decomp_gibps if a.decompress_only else total / GiB / (tc + td)
@@ -367,14 +418,18 @@ def main():
         line = {
             "metric": "device-resident LZ4 GiB/s (compress, decompress) on 4 MiB blocks at 1/2/4/8 MI355X",
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": K, "warmup": a.warmup,
-            "ms_per_step": round((tc + td) / K * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round((tc + td) / K * 1e3, 3), "higher_is_better": True, "scaling": "strong" if a.total_gib is not None else "weak",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic (SURVEY.md App. F generator, seed 42)",
             "config": {"workload": (f"configs[2]: {a.gib:g} GiB/GPU pre-compressed synthetic stream, "
                                     f"{bm >> 10} KiB blocks, decompress+XXH32 verify only, device-resident")
                                    if a.decompress_only else
+                                   (f"configs[3]: ONE {a.total_gib:g} GiB synthetic buffer block-sharded over "
+                                    f"{world} GPU(s), {bm >> 10} KiB independent blocks, {flags} frame, "
+                                    f"compress+decompress+XXH32, device-resident")
+                                   if a.total_gib is not None else
                                    (f"configs[{1 if world == 1 else 3}]: {a.gib:g} GiB/GPU synthetic, {bm >> 10} KiB "
                                     f"independent blocks, {flags} frame, compress+decompress+XXH32, device-resident"),
-                       "bytes_per_gpu": n, "block_bytes": bm,
+                       "bytes_per_gpu": n, "bytes_total": n_total, "block_bytes": bm,
                        "parallelism": f"block-sharded x{world}" + (", RCCL gather to one frame on rank 0 (in compress)"
                                                                    if world > 1 else "")},
             "compress_GiBps": round(comp_gibps, 3) if comp_gibps else None,

@@ -35,10 +35,11 @@ extern "C" {
 /* ---- 1. block operators (reference plugin signatures) ------------------ */
 /* LZ4_compress_limitedOutput semantics (lz4 1.9.3, acceleration 1):
  * returns the compressed size, or 0 when it does not fit maxOutputSize.
- * compressionLevel 3..9: LZ4_compressHC2_limitedOutput (LZ4-HC 1.9.3 hash
- * chain), the codec the reference wires for those levels
- * (src/main.cpp:778-785).  Levels 10..12 (lz4's optimal parser) are not
- * provided: 0, so the block is stored raw. */
+ * compressionLevel >= 3: LZ4_compressHC2_limitedOutput, the codec the
+ * reference wires for those levels (src/main.cpp:778-785): 3..9 LZ4-HC
+ * 1.9.3's hash-chain parser, 10..12 its optimal parser
+ * (LZ4HC_compress_optimal); levels above 12 are clamped to 12 as lz4hc
+ * does. */
 int lz4mtHipCompressBlock(const char* src, char* dst, int isize, int maxOutputSize, int compressionLevel);
 /* LZ4_compressBound. */
 int lz4mtHipCompressBound(int isize);
@@ -56,7 +57,9 @@ uint64_t lz4mtHipCompressWorkspaceSize(uint64_t srcSize, const Lz4MtStreamDescri
  * stream once at the end to read it.  blockIndependence = 0 writes a
  * block-dependent (-BD) frame: one wavefront encodes the blocks in order,
  * each against the 64 KiB before it (lz4's streaming compressor, as the
- * reference's compressBlockDependency calls it). */
+ * reference's compressBlockDependency calls it).  The plan, table and
+ * round scratch of -BD frames live in the workspace, so size it with
+ * lz4mtHipCompressWorkspaceSize for the same `sd`. */
 Lz4MtResult lz4mtHipCompressFrame(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
                                   uint64_t* frameSize, const Lz4MtStreamDescriptor* sd,
                                   void* d_workspace, uint64_t workspaceSize, void* stream);
@@ -66,11 +69,11 @@ Lz4MtResult lz4mtHipCompressFrameAsync(const void* d_src, uint64_t srcSize, void
                                        uint64_t* d_frameSize, const Lz4MtStreamDescriptor* sd,
                                        void* d_workspace, uint64_t workspaceSize, void* stream);
 
-/* The same with a compression level: 0..2 fast LZ4, 3..9 LZ4-HC (the
+/* The same with a compression level: 0..2 fast LZ4, 3..9 LZ4-HC hash
+ * chain, 10..12 (and above, clamped to 12) LZ4-HC's optimal parser (the
  * workspace then holds 2 more bytes per input byte: use
- * lz4mtHipCompressWorkspaceSizeEx).  BAD_ARG for levels 10..12 on
- * independent blocks; block-dependent frames at any level >= 3 are the
- * reference's HC stream, which runs at lz4hc's level 9. */
+ * lz4mtHipCompressWorkspaceSizeEx).  Block-dependent frames at any level
+ * >= 3 are the reference's HC stream, which runs at lz4hc's level 9. */
 uint64_t lz4mtHipCompressWorkspaceSizeEx(uint64_t srcSize, const Lz4MtStreamDescriptor* sd, int level);
 Lz4MtResult lz4mtHipCompressFrameEx(const void* d_src, uint64_t srcSize, void* d_frame, uint64_t frameCap,
                                     uint64_t* frameSize, const Lz4MtStreamDescriptor* sd, int level,

@@ -64,10 +64,17 @@ struct CompressWs {
     uint64_t* recOff;
     uint32_t* ssum;
     uint64_t* fsize;
+    // block-dependent frames of the asynchronous calls (bd != 0): the host
+    // plan copied in, the carried lz4 table, the parallel rounds' scratch
+    // (bd == 1), or the HC stream's packed segments (bd == 2)
+    uint8_t* bdPlan;
+    uint32_t* bdTable;
+    uint32_t* bdRounds;
     uint64_t bytes;
 };
 
-CompressWs carve_compress(uint8_t* base, uint64_t nb, uint64_t bm, int level = 0) {
+// bd: 0 independent blocks, 1 block-dependent fast LZ4, 2 block-dependent HC
+CompressWs carve_compress(uint8_t* base, uint64_t nb, uint64_t bm, int level = 0, int bd = 0) {
     CompressWs w{};
     uint64_t o = 0;
     auto take = [&](uint64_t n) { uint8_t* p = base ? base + o : nullptr; o = align_up(o + n, 256); return p; };
@@ -81,6 +88,14 @@ CompressWs carve_compress(uint8_t* base, uint64_t nb, uint64_t bm, int level = 0
     w.recOff = reinterpret_cast<uint64_t*>(take((nb + 1) * 8));
     w.ssum = reinterpret_cast<uint32_t*>(take(16));
     w.fsize = reinterpret_cast<uint64_t*>(take(16));
+    const uint64_t nbp = nb > 0 ? nb : 1;
+    if (bd == 1) {
+        w.bdPlan = take(nbp * sizeof(LinkPlan));
+        w.bdTable = reinterpret_cast<uint32_t*>(take(4096 * 4));
+        w.bdRounds = reinterpret_cast<uint32_t*>(take(link_round_bytes(nbp)));
+    } else if (bd == 2) {
+        w.bdPlan = take(20 * nbp + 64);   // hc_bd_pack: 16 B per segment (<= nb) + 4 B per block
+    }
     w.bytes = o;
     return w;
 }
@@ -216,20 +231,20 @@ struct DevBuf {
     }
 };
 
-// A few bytes of device memory per thread (frame-size / digest results),
-// re-made when the thread's device changes: no hipMalloc/hipFree per call
-// (hipFree waits for the whole device).
+// A few bytes of device memory per thread and device (frame-size / digest
+// results): no hipMalloc/hipFree per call (hipFree waits for the whole
+// device).  One buffer per device ordinal, made on first use, so a thread
+// that alternates devices reuses them instead of leaking one per switch.
 uint8_t* small_dev() {
-    thread_local uint8_t* p = nullptr;
-    thread_local int dev = -1;
+    constexpr int kMaxDev = 64;
+    thread_local uint8_t* p[kMaxDev] = {};
     int d = -1;
-    if (hipGetDevice(&d) != hipSuccess) return nullptr;
-    if (!p || d != dev) {
-        p = nullptr;   // a buffer of another device is left to that device
-        if (hipMalloc(reinterpret_cast<void**>(&p), 256) != hipSuccess) { p = nullptr; return nullptr; }
-        dev = d;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kMaxDev) return nullptr;
+    if (!p[d] && hipMalloc(reinterpret_cast<void**>(&p[d]), 256) != hipSuccess) {
+        p[d] = nullptr;
+        return nullptr;
     }
-    return p;
+    return p[d];
 }
 
 // The content checksum (FLG.2) is ONE serial XXH32 chain:
@@ -399,8 +414,13 @@ void AuxStream::release() {
     st = nullptr; evIn = nullptr; evOut = nullptr; dev = -1;
 }
 
-uint64_t compress_ws_bytes(uint64_t n, uint32_t bm, int level) {
-    return carve_compress(nullptr, (n + bm - 1) / bm, bm, level).bytes;
+uint64_t compress_ws_bytes(uint64_t n, uint32_t bm, int level, int bd) {
+    return carve_compress(nullptr, (n + bm - 1) / bm, bm, level, bd).bytes;
+}
+
+// the workspace kind of a descriptor + level (carve_compress's bd)
+static int ws_bd_kind(const Lz4MtStreamDescriptor* sd, int level) {
+    return (sd && !sd->flg.blockIndependence) ? (level >= 3 ? 2 : 1) : 0;
 }
 
 }  // namespace lz4mt
@@ -416,7 +436,6 @@ extern "C" int lz4mtHipCompressBlock(const char* src, char* dst, int isize, int 
     // levels >= 3: LZ4-HC (LZ4_compressHC2_limitedOutput): 3..9 hashChain,
     // 10..12 (and above, clamped to 12) the optimal parser
     const bool hc = compressionLevel >= 3;
-    if (hc && hc_attempts(compressionLevel) == 0) return 0;
     if (isize < 0 || (unsigned)isize > 0x7E000000u) return 0;
     if (maxOutputSize < 0) maxOutputSize = 0;
     if (!have_device()) return -1;
@@ -484,7 +503,7 @@ extern "C" uint64_t lz4mtHipFrameBound(uint64_t srcSize, const Lz4MtStreamDescri
 extern "C" uint64_t lz4mtHipCompressWorkspaceSizeEx(uint64_t srcSize, const Lz4MtStreamDescriptor* sd, int level) {
     const int id = sd ? sd->bd.blockMaximumSize : 7;
     const uint32_t bm = (id >= 4 && id <= 7) ? (uint32_t)block_max_bytes(id) : (4u << 20);
-    return compress_ws_bytes(srcSize, bm, level);
+    return compress_ws_bytes(srcSize, bm, level < 3 ? 0 : level, ws_bd_kind(sd, level));
 }
 
 extern "C" uint64_t lz4mtHipCompressWorkspaceSize(uint64_t srcSize, const Lz4MtStreamDescriptor* sd) {
@@ -502,10 +521,10 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
     // LZ4-HC on independent blocks: levels 3..9 the hashChain parser, 10..12
     // (and above, clamped) the optimal parser.  Block-dependent frames at any
     // level >= 3 are the reference's HC stream, which runs at level 9 (HcBdSim).
-    if (level >= 3 && sd->flg.blockIndependence && hc_attempts(level) == 0) return LZ4MT_RESULT_BAD_ARG;
     if (level < 3) level = 0;
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
-    const uint64_t need = compress_ws_bytes(srcSize, bm, level);
+    const int bdk = ws_bd_kind(sd, level);
+    const uint64_t need = compress_ws_bytes(srcSize, bm, level, bdk);
     uint8_t* ws = static_cast<uint8_t*>(d_ws);
     if (!ws || wsSize < need) {
         if (hipMalloc(reinterpret_cast<void**>(&ws), need) != hipSuccess) return LZ4MT_RESULT_ERROR;
@@ -519,7 +538,7 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
     thread_local AuxStream aux, auxStream;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     const bool capturing = hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone;
-    CompressWs w = carve_compress(ws, (srcSize + bm - 1) / bm, bm, level);
+    CompressWs w = carve_compress(ws, (srcSize + bm - 1) / bm, bm, level, bdk);
     // The content checksum (FLG.2) is one serial XXH32 chain over the input
     // (SURVEY.md §0.5).  It reads only d_src, so it starts at t = 0 on its
     // own stream, beside the encode, and the finalize waits for it.
@@ -538,39 +557,33 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
         HIPCHK(launch_xxh32_stream(static_cast<const uint8_t*>(d_src), srcSize, w.ssum, auxStream.st));
         HIPCHK(hipEventRecord(auxStream.evOut, auxStream.st));
     }
-    // block-dependent frames: the per-block lz4 stream plan (BdSim) and the
-    // table buffer, kept per thread (the kernels of an async call use them)
+    // block-dependent frames: the per-block lz4 stream plan (BdSim), the
+    // carried table and the rounds' scratch live in this call's workspace,
+    // so asynchronous calls on other streams never share them (the host
+    // plan is staged by the copy before hipMemcpyAsync returns: pageable
+    // memory)
     LinkState ls{};
     const LinkState* lsp = nullptr;
-    if (!sd->flg.blockIndependence && level >= 3) {
-        thread_local DevBuf segBuf;
-        thread_local std::vector<uint64_t> segAbs;
-        thread_local std::vector<uint8_t> packed;
+    if (bdk == 2) {
         const uint64_t nb = (srcSize + bm - 1) / bm;
-        segAbs.assign(nb, 0);
+        std::vector<uint64_t> segAbs(nb, 0);
+        std::vector<uint8_t> packed;
         HcBdSim sim(sd->bd.blockMaximumSize);
         for (uint64_t b = 0; b < nb; ++b) segAbs[b] = sim.next((uint32_t)std::min<uint64_t>(bm, srcSize - b * bm));
         ls.nSeg = hc_bd_pack(segAbs.data(), nb, 0, srcSize, 0, packed, bm, &ls.hcPerBlock);
-        if (!segBuf.ensure(packed.size() + 64)) return LZ4MT_RESULT_ERROR;
         if (!packed.empty())
-            HIPCHK(hipMemcpyAsync(segBuf.p, packed.data(), packed.size(), hipMemcpyHostToDevice, st));
-        ls.hcSegs = static_cast<const uint8_t*>(segBuf.p);
+            HIPCHK(hipMemcpyAsync(w.bdPlan, packed.data(), packed.size(), hipMemcpyHostToDevice, st));
+        ls.hcSegs = w.bdPlan;
         lsp = &ls;
-    } else if (!sd->flg.blockIndependence) {
-        thread_local DevBuf planBuf, tableBuf, roundBuf;
-        thread_local std::vector<LinkPlan> hplan;
+    } else if (bdk == 1) {
         const uint64_t nb = (srcSize + bm - 1) / bm;
-        hplan.assign(std::max<uint64_t>(nb, 1), LinkPlan{});
+        std::vector<LinkPlan> hplan(std::max<uint64_t>(nb, 1), LinkPlan{});
         BdSim sim(sd->bd.blockMaximumSize);
         for (uint64_t b = 0; b < nb; ++b)
             sim.next((uint32_t)std::min<uint64_t>(bm, srcSize - b * bm), &hplan[b].lowIn, &hplan[b].lowDict,
                      &hplan[b].candLow);
-        if (!planBuf.ensure(hplan.size() * sizeof(LinkPlan)) || !tableBuf.ensure(4096 * 4) ||
-            !roundBuf.ensure(link_round_bytes(std::max<uint64_t>(nb, 1))))
-            return LZ4MT_RESULT_ERROR;
-        HIPCHK(hipMemcpyAsync(planBuf.p, hplan.data(), hplan.size() * sizeof(LinkPlan), hipMemcpyHostToDevice, st));
-        ls = LinkState{reinterpret_cast<LinkPlan*>(planBuf.p), reinterpret_cast<uint32_t*>(tableBuf.p), true,
-                       reinterpret_cast<uint32_t*>(roundBuf.p)};
+        HIPCHK(hipMemcpyAsync(w.bdPlan, hplan.data(), hplan.size() * sizeof(LinkPlan), hipMemcpyHostToDevice, st));
+        ls = LinkState{reinterpret_cast<LinkPlan*>(w.bdPlan), w.bdTable, true, w.bdRounds};
         lsp = &ls;
     }
     const Lz4MtResult r = device_compress_body(static_cast<const uint8_t*>(d_src), srcSize, bm, sd->flg.blockChecksum,

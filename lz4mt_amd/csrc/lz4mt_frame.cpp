@@ -44,7 +44,7 @@ namespace lz4mt {
 Lz4MtResult device_compress_body(const uint8_t* src, uint64_t n, uint32_t bm, int blockChecksum, uint8_t* ws,
                                  uint8_t* body, uint32_t hdrLen, hipStream_t st, uint64_t** d_recOffOut,
                                  const AuxStream* aux, const LinkState* link, int level);
-uint64_t compress_ws_bytes(uint64_t n, uint32_t bm, int level);
+uint64_t compress_ws_bytes(uint64_t n, uint32_t bm, int level, int bd = 0);
 }  // namespace lz4mt
 
 using namespace lz4mt;
@@ -517,7 +517,6 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
     // (and above, clamped) the optimal parser.  Block-dependent frames at any
     // level >= 3 are the reference's HC stream, at level 9 (HcBdSim).
     const int level = s.level() >= 3 ? s.level() : 0;
-    if (level && sd->flg.blockIndependence && hc_attempts(level) == 0) { s.quit(LZ4MT_RESULT_BAD_ARG); return; }
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
     // Block-dependent frames (compressBlockDependency, src/lz4mt.cpp:460-538)

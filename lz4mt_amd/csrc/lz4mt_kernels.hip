@@ -1481,7 +1481,7 @@ __global__ void __launch_bounds__(64) k_link_warm(const uint8_t* __restrict__ sr
 // LZ4MT_AMD_BD_WARM_KIB overrides (A/B)
 static uint32_t link_warm_bytes(uint32_t blockSize) {
     const char* e = getenv("LZ4MT_AMD_BD_WARM_KIB");
-    // measured on App. F (LZ4MT_AMD_BD_STATS=1; tools/r02ab.sh, r02ae.sh): two
+    // measured on App. F (LZ4MT_AMD_BD_STATS=1; profiles/r02_bd_warm_sweep*): two
     // parses agree only after ~0.5-1.5 MiB -- 4 MiB blocks with W = 256 / 512
     // / 1024 KiB leave 212 / 47 / 0 of 255 entries wrong at 1 GiB, W = 1024 /
     // 1536 KiB leave 15 / 0 of 2047 at 8 GiB (19.6 / 29.0 GiB/s compress);

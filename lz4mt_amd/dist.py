@@ -108,12 +108,20 @@ def gather_frame(frame, frame_len, dst=0, group=None, async_op=False):
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    hdr, rec = frame_records(frame, frame_len)
+    err = None
+    try:
+        hdr, rec = frame_records(frame, frame_len)
+    except ValueError as e:   # still join the all_gather: every rank raises together below
+        err, hdr, rec = e, 0, -1
     dev = frame.device
     sizes = torch.tensor([rec], dtype=torch.int64, device=dev)
     all_sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(all_sizes, sizes, group=group)
     lens = [int(s.item()) for s in all_sizes]
+    if min(lens) < 0:
+        if err is not None:
+            raise err
+        raise ValueError(f"gather_frame: rank {lens.index(min(lens))} holds no valid -Sx shard frame")
     peer = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
     if rank == dst:
         out = torch.empty(hdr + sum(lens) + 4, dtype=torch.uint8, device=dev)
@@ -230,20 +238,26 @@ def scatter_frame(frame, frame_len, src=0, group=None, records=None, async_op=Fa
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     peer = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+    err = None
     if rank == src:
         dev = frame.device
-        recs_fn = records or (device_records if frame.is_cuda else host_records)
-        hdr, starts = recs_fn(frame, frame_len)
-        _frame_layout(bytes(frame[:hdr].cpu().numpy().tobytes()) + b"\0" * 8)
-        nb = len(starts) - 1
         table = torch.zeros(4 + 2 * world, dtype=torch.int64)
-        table[0] = hdr
-        table[1:4] = torch.frombuffer(bytearray(frame[:hdr].cpu().numpy().tobytes().ljust(24, b"\0")),
-                                      dtype=torch.int64)
-        for r in range(world):
-            first, count = rank_blocks(nb, world, r)
-            table[4 + 2 * r] = starts[first]
-            table[5 + 2 * r] = starts[first + count] - starts[first]
+        try:
+            recs_fn = records or (device_records if frame.is_cuda else host_records)
+            hdr, starts = recs_fn(frame, frame_len)
+            _frame_layout(bytes(frame[:hdr].cpu().numpy().tobytes()) + b"\0" * 8)
+            nb = len(starts) - 1
+            table[0] = hdr
+            table[1:4] = torch.frombuffer(bytearray(frame[:hdr].cpu().numpy().tobytes().ljust(24, b"\0")),
+                                          dtype=torch.int64)
+            for r in range(world):
+                first, count = rank_blocks(nb, world, r)
+                table[4 + 2 * r] = starts[first]
+                table[5 + 2 * r] = starts[first + count] - starts[first]
+        except Exception as e:   # every rank must leave the broadcast below: flag the error in the table
+            err = e
+            table.zero_()
+            table[0] = -1
         table = table.to(dev)
     else:
         if device is not None:   # where this rank decodes (gloo can carry CUDA tensors too)
@@ -253,6 +267,10 @@ def scatter_frame(frame, frame_len, src=0, group=None, records=None, async_op=Fa
                 else torch.device("cpu")
         table = torch.zeros(4 + 2 * world, dtype=torch.int64, device=dev)
     dist.broadcast(table, peer(src), group=group)
+    if int(table[0].item()) < 0:   # the source rank could not cut the frame: all ranks raise together
+        if err is not None:
+            raise err
+        raise ValueError(f"scatter_frame: rank {src} could not walk the frame")
     t = table.cpu().tolist()
     hdr = int(t[0])
     head = torch.tensor(t[1:4], dtype=torch.int64).numpy().tobytes()[:hdr]
@@ -307,18 +325,28 @@ def verify_stitched(full, shard_src, decode, digests, dst=0, group=None):
     sizes = _all_gather_var(torch.tensor([shard_src.numel()], dtype=torch.int64, device=mine.device), group)
     allsum = _all_gather_var(mine, group)
     ok = torch.ones(1, dtype=torch.int64, device=mine.device)
+    err = None
     if rank == dst:
-        out = decode(full)
-        pos = 0
-        good = True
-        for r in range(world):
-            n = int(sizes[r].item())
-            piece = out[pos:pos + n]
-            if piece.numel() != n or not torch.equal(digests(piece).to(torch.int64).cpu(), allsum[r].cpu()):
-                good = False
-            pos += n
-        good = good and pos == out.numel()
-        ok[0] = 1 if good else 0
+        try:
+            out = decode(full)
+            pos = 0
+            good = True
+            for r in range(world):
+                n = int(sizes[r].item())
+                piece = out[pos:pos + n]
+                if piece.numel() != n or not torch.equal(digests(piece).to(torch.int64).cpu(), allsum[r].cpu()):
+                    good = False
+                pos += n
+            good = good and pos == out.numel()
+            ok[0] = 1 if good else 0
+        except Exception as e:   # still reach the broadcast, so no rank waits forever
+            err = e
+            ok[0] = -1
     peer = dist.get_global_rank(group, dst) if group is not None else dst
     dist.broadcast(ok, peer, group=group)
-    return bool(ok.item())
+    v = int(ok.item())
+    if v < 0:
+        if err is not None:
+            raise err
+        raise RuntimeError(f"verify_stitched: rank {dst} could not decode the stitched frame")
+    return v == 1

@@ -210,6 +210,100 @@ def bd_decode_reference(frame):
             dptr = dbase + 65536
 
 
+def bd_decompress_reference(frame):
+    """lz4mtDecompress on a -BD frame, step for step (src/lz4mt.cpp:938-1011
+    frame loop, decompressBlockDependency 737-845) over liblz4 1.9.3's
+    LZ4_decompress_safe_withPrefix64k: per block the size word (0 = EOS;
+    > blockMax = INVALID_BLOCK_SIZE), the payload, the checksum word and its
+    check (BLOCK_CHECKSUM_MISMATCH), then a raw copy or the decode into the
+    64 KiB-prefixed buffer (< 0 = DECOMPRESS_FAIL), each block written as it
+    is done; after the EOS the content checksum (STREAM_CHECKSUM_MISMATCH).
+    Returns (result name, the bytes written)."""
+    flg, bid = frame[4], (frame[5] >> 4) & 7
+    sck, bck = bool(flg & 0x04), bool(flg & 0x10)
+    bm = 1 << (8 + 2 * bid)
+    d = ctypes.create_string_buffer(65536 + bm)
+    dbase = ctypes.addressof(d)
+    dptr, pos, out = dbase + 65536, 7, []
+
+    def u32(at):
+        return struct.unpack_from("<I", frame, at)[0] if at + 4 <= len(frame) else None
+    while True:
+        w = u32(pos)
+        if w is None:
+            return "CANNOT_READ_BLOCK_SIZE", b"".join(out)
+        pos += 4
+        if w == 0:
+            break
+        n = w & 0x7FFFFFFF
+        if n > bm:
+            return "INVALID_BLOCK_SIZE", b"".join(out)
+        if pos + n > len(frame):
+            return "CANNOT_READ_BLOCK_DATA", b"".join(out)
+        payload = frame[pos:pos + n]
+        pos += n
+        if bck:
+            c = u32(pos)
+            if c is None:
+                return "CANNOT_READ_BLOCK_CHECKSUM", b"".join(out)
+            pos += 4
+            if c != xxh(payload):
+                return "BLOCK_CHECKSUM_MISMATCH", b"".join(out)
+        if w & 0x80000000:
+            out.append(payload)
+            if n >= 65536:
+                ctypes.memmove(dbase, payload[-65536:], 65536)
+                dptr = dbase + 65536
+                continue
+            ctypes.memmove(dptr, payload, n)
+            k = n
+        else:
+            k = LZ4.LZ4_decompress_safe_withPrefix64k(payload, ctypes.c_void_p(dptr), n, bm)
+            if k < 0:
+                return "DECOMPRESS_FAIL", b"".join(out)
+            out.append(ctypes.string_at(dptr, k))
+        dptr += k
+        if dbase + 65536 + bm - dptr < bm:
+            ctypes.memmove(dbase, dptr - 65536, 65536)
+            dptr = dbase + 65536
+    content = b"".join(out)
+    if sck:
+        c = u32(pos)
+        if c is None:
+            return "CANNOT_READ_STREAM_CHECKSUM", content
+        if c != xxh(content):
+            return "STREAM_CHECKSUM_MISMATCH", content
+    return "OK", content
+
+
+# Frames the reference itself writes with 1 and 4 MiB blocks (bd_frame_reference:
+# every block after the first is read over its own dictionary, see
+# DESIGN.md), and what lz4mtDecompress does with them: users with such -BD
+# archives feed exactly these bytes in.  (name, bytes, seed, id, sck, bck)
+BD_REF_DECODE = [  # (name, bytes, seed, id, sck, bck, input: "bd" = bd_input, "appf" = App. F)
+    ("bdref_b6_SX", (2 << 20) + 100_000, 71, 6, True, True, "bd"),          # decodes back, other bytes than ours
+    ("bdref_b6_appf_SX", (2 << 20) + 100_000, 42, 6, True, True, "appf"),   # STREAM_CHECKSUM_MISMATCH
+    ("bdref_b6_appf_sX", (2 << 20) + 100_000, 42, 6, False, True, "appf"),  # OK, but not the input
+    ("bdref_b7_Sx", (4 << 20) + 200_000, 73, 7, True, False, "bd"),
+    ("bdref_b7_sx", (4 << 20) + 150_000, 74, 7, False, False, "bd"),
+]
+
+
+def bd_ref_decode_main(manifest):
+    from oracle import gen_synthetic
+    manifest["bd_ref_decode"] = []
+    for name, n, seed, bid, sck, bck, kind in BD_REF_DECODE:
+        data = bd_input(n, seed) if kind == "bd" else gen_synthetic(n, seed)
+        f = bd_frame_reference(data, bid, sck, bck)
+        res, out = bd_decompress_reference(f)
+        open(os.path.join(HERE, "frames", f"{name}.lz4"), "wb").write(f)
+        manifest["bd_ref_decode"].append({
+            "name": name, "bytes": n, "seed": seed, "kind": kind, "bid": bid, "stream_checksum": sck,
+            "block_checksum": bck, "file": f"frames/{name}.lz4", "size": len(f), "xxh32": xxh(f),
+            "content_xxh32": xxh(data), "result": res, "out_bytes": len(out), "out_xxh32": xxh(out),
+            "roundtrips": out == data, "contiguous_identical": f == bd_frame_contiguous(data, bid, sck, bck)})
+
+
 BD_CASES = [  # (name, bytes, seed, block id, stream checksum, block checksum[, input kind])
     ("bd_b4_sX", 1_500_000, 11, 4, False, True), ("bd_b4_SX", 1_500_000, 11, 4, True, True),
     ("bd_b5_Sx", 1_500_000, 12, 5, True, False),
@@ -419,6 +513,7 @@ def main():
                                               "sha1": hashlib.sha1(dst.raw[:r]).hexdigest()})
     bd_main(manifest)
     bd_hc_main(manifest)
+    bd_ref_decode_main(manifest)
     json.dump(manifest, open(os.path.join(HERE, "golden.json"), "w"), indent=0)
     print("frames", len(manifest["frames"]), "blocks", len(manifest["blocks"]), "decode", len(manifest["decode"]),
           "crafted", len(manifest["crafted"]), "cli mismatches",
@@ -426,4 +521,11 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--bd-ref-decode" in sys.argv:   # add / refresh only that section of golden.json
+        path = os.path.join(HERE, "golden.json")
+        m = json.load(open(path))
+        bd_ref_decode_main(m)
+        json.dump(m, open(path, "w"), indent=0)
+        print(json.dumps(m["bd_ref_decode"], indent=1))
+    else:
+        main()

@@ -204,3 +204,49 @@ def test_stream_size_frames_refuse_to_shard():
     frame = oracle.compress_frame(oracle.gen_synthetic(70000, 1), oracle.params(4, False, True, stream_size=70000))
     with pytest.raises(ValueError, match="FLG.3"):
         D.split_frame(frame, 2)
+
+
+def _error_worker(rank, world, port, kind, q):
+    """A frame the source rank cannot cut (-BD, or damaged so the walk runs
+    off its end) must make EVERY rank raise, not leave the others waiting in
+    the broadcast (scatter) or the all_gather (gather)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data = oracle.gen_synthetic(5 * 65536, 3)
+        good = oracle.compress_frame(data, oracle.params(4, False, True))
+        if kind == "bd":   # FLG.5 clear: a block-dependent frame does not shard
+            bad = bytearray(good)
+            bad[4] &= ~0x20
+            bad = bytes(bad)
+        else:   # a size word pointing past the frame end
+            bad = bytearray(good)
+            bad[7:11] = (0x7FFFFF00).to_bytes(4, "little")
+            bad = bytes(bad)
+        try:
+            if kind == "gather":   # rank 1 holds a shard frame with a damaged magic word
+                f = (b"\x05" + good[1:]) if rank == 1 else good
+                D.gather_frame(torch.frombuffer(bytearray(f), dtype=torch.uint8), len(f))
+            else:
+                t = torch.frombuffer(bytearray(bad), dtype=torch.uint8)
+                D.scatter_frame(t if rank == 0 else None, len(bad) if rank == 0 else 0)
+            q.put((rank, "returned"))
+        except (ValueError, RuntimeError) as e:
+            q.put((rank, "raised: " + str(e)[:60]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["bd", "damaged", "gather"])
+def test_bad_frame_raises_on_every_rank(kind):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_error_worker, args=(r, 2, port, kind, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[1].startswith("raised") for r in res), res

@@ -194,3 +194,31 @@ def test_bd_parallel_equals_serial_64mib(monkeypatch, bid):
     assert fr.numel() == fr_ser.numel() and torch.equal(fr, fr_ser)
     out, r = L.decompress_frame(fr)
     assert r == 0 and r_ser == 0 and torch.equal(out, src) and torch.equal(out_ser, src)
+
+
+@pytest.mark.parametrize("api", ["device", "DEVICE", "PARALLEL"])
+def test_bd_reference_written_b6_b7_frames(golden, api):
+    """-BD frames the reference itself writes with 1 and 4 MiB blocks
+    (compressBlockDependency on liblz4 1.9.3, src/lz4mt.cpp:460-538: after
+    LZ4_slideInputBuffer each block is read over its own dictionary, so the
+    bytes differ from this library's contiguous stream and on App. F input
+    they do not decode back).  Decoding them is what a user with existing
+    -BD archives does: lz4mtDecompress must give decompressBlockDependency's
+    bytes and result (src/lz4mt.cpp:737-845, 997-1007), here pinned by
+    liblz4's LZ4_decompress_safe_withPrefix64k (make_golden.py
+    bd_decompress_reference) and the oracle."""
+    from lz4mt_amd import RESULT_NAMES
+    for f in golden["bd_ref_decode"]:
+        frame = read_golden(f["file"])
+        assert (len(frame), xxhash.xxh32(frame).intdigest()) == (f["size"], f["xxh32"]), f["name"]
+        cap = f["bytes"] + (1 << (8 + 2 * f["bid"])) + (1 << 20)   # room for a whole block past the end
+        if api == "device":
+            out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+            o, r = L.decompress_frame(dev(frame), out=out, check=False)
+            got = host(o)
+        else:
+            r, got, _ = L.decompress(frame, cap, mode=L.MODE_DEVICE if api == "DEVICE" else L.MODE_PARALLEL)
+        assert RESULT_NAMES[r] == f["result"], (f["name"], api, RESULT_NAMES[r])
+        assert (len(got), xxhash.xxh32(got).intdigest()) == (f["out_bytes"], f["out_xxh32"]), (f["name"], api)
+        rw, ow = oracle.decompress_frame(frame, cap)
+        assert (r, got) == (rw, ow), (f["name"], api)

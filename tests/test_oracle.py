@@ -341,3 +341,16 @@ def test_hc_differential_vs_liblz4():
                 dst = ctypes.create_string_buffer(max(cap, 1) + len(d) // 255 + 64)
                 r = lz.LZ4_compress_HC(d, dst, len(d), cap, level)
                 assert oracle.compress_block_hc(d, cap, level) == dst.raw[:r], (seed, len(d), level, cap)
+
+
+def test_oracle_decodes_reference_bd_frames(golden):
+    """The reference's own -BD frames at 1 and 4 MiB blocks (read over their
+    own dictionary; tests/golden/make_golden.py BD_REF_DECODE): the oracle's
+    decompressBlockDependency gives liblz4's result and bytes, including a
+    STREAM_CHECKSUM_MISMATCH and an OK frame whose content is not the input."""
+    from lz4mt_amd._abi import RESULT_NAMES
+    for f in golden["bd_ref_decode"]:
+        frame = read_golden(f["file"])
+        r, out = oracle.decompress_frame(frame, f["bytes"] + (1 << (8 + 2 * f["bid"])) + (1 << 20))
+        assert RESULT_NAMES[r] == f["result"], (f["name"], RESULT_NAMES[r])
+        assert (len(out), xxhash.xxh32(out).intdigest()) == (f["out_bytes"], f["out_xxh32"]), f["name"]
