@@ -222,3 +222,34 @@ def test_bd_reference_written_b6_b7_frames(golden, api):
         assert (len(got), xxhash.xxh32(got).intdigest()) == (f["out_bytes"], f["out_xxh32"]), (f["name"], api)
         rw, ow = oracle.decompress_frame(frame, cap)
         assert (r, got) == (rw, ow), (f["name"], api)
+
+
+def test_bd_async_calls_on_two_streams(golden):
+    """Two asynchronous -BD compress calls from one thread on two streams,
+    nothing synchronised in between (lz4mtHipCompressFrameAsyncEx): each
+    call's plan, carried table and round scratch live in its own workspace,
+    so both frames are the reference's (the golden -BD frames)."""
+    import ctypes
+    fs = [f for f in golden["bd_frames"] if f["bytes"] >= 1_000_000][:2]
+    assert len(fs) == 2
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    jobs = []
+    for f, st in zip(fs, streams):
+        data = dev(bd_data(f))
+        sd = _sd(f)
+        cap = L.frame_bound(data.numel(), sd)
+        out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+        ws = L.compress_workspace(data.numel(), sd)
+        fsz = torch.zeros(1, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()   # inputs ready before the side streams read them
+        jobs.append((f, data, sd, out, ws, fsz, st))
+    for f, data, sd, out, ws, fsz, st in jobs * 2:   # A, B, A, B back to back
+        r = L.lib.lz4mtHipCompressFrameAsyncEx(ctypes.c_void_p(data.data_ptr()), data.numel(),
+                                               ctypes.c_void_p(out.data_ptr()), out.numel(),
+                                               ctypes.c_void_p(fsz.data_ptr()), ctypes.byref(sd), 0,
+                                               ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                                               ctypes.c_void_p(st.cuda_stream))
+        assert r == 0
+    torch.cuda.synchronize()
+    for f, data, sd, out, ws, fsz, st in jobs:
+        assert host(out[:int(fsz[0].item())]) == read_golden(f["file"]), f["name"]

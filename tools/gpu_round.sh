@@ -1,0 +1,56 @@
+#!/bin/bash
+# One GPU-box pass for a round: any of the steps below, in the order given,
+# each under its own time limit; the first failure ends the pass.
+# usage (from the repo root on the box): bash tools/gpu_round.sh <tag> <step>...
+#   tests   pytest -m gpu (every GPU test file)
+#   bench   the default 1-GPU bench line (driver shape: --steps 20 --warmup 5)
+#   trace   rocprofv3 kernel-trace stats of a 5-step bench run
+#   sq      SQ counters of the encoder / decoder (tools/kprof.py 2) + the window count (tools/kstats.py 2)
+#   pmc     FETCH_SIZE / WRITE_SIZE passes (tools/prof.sh without its trace)
+#   dist2   bench.py --gpus 2 over gloo on this one GPU (rehearsal of the N > 1 path)
+#   ab      kernel times of every exp_libs/*.so (tools/mkvariants.sh), two passes
+set -euo pipefail
+tag=$1; shift
+out=gpurun_out/$tag
+mkdir -p "$out"
+export TMPDIR=/tmp
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+    tests)
+      timeout -k 10 1100 python3 -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread tests \
+          > "$out/pytest.log" 2>&1 || { tail -30 "$out/pytest.log"; exit 1; }
+      tail -2 "$out/pytest.log" ;;
+    bench)
+      timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > "$out/bench.json" 2> "$out/bench.err"
+      cat "$out/bench.json" ;;
+    trace)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -f csv -d "$out/trace" -o trace -- \
+          python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 > "$out/trace_bench.json" 2> "$out/trace.err"
+      cat "$out/trace_bench.json" ;;
+    sq)
+      timeout -k 10 200 python3 tools/kstats.py 2 > "$out/kstats.txt" 2>&1
+      head -3 "$out/kstats.txt"
+      timeout -s KILL 200 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM \
+          SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -T -f csv -d "$out/sq" -o sq -- \
+          python3 tools/kprof.py 2 > "$out/sq.log" 2>&1
+      python3 tools/sqsum.py "$out/sq" "$out/kstats.txt" | tee "$out/sq_summary.txt" ;;
+    pmc)
+      for input in appf random; do
+        flag=""; [ "$input" = random ] && flag="--random"
+        timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -T -f csv -d "$out/fetch_$input" -o fetch -- \
+            python3 tools/kprof.py 8 $flag > "$out/fetch_$input.log" 2>&1
+        timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -T -f csv -d "$out/write_$input" -o write -- \
+            python3 tools/kprof.py 8 $flag > "$out/write_$input.log" 2>&1
+      done ;;
+    dist2)
+      LZ4MT_BENCH_BACKEND=gloo timeout -k 10 400 python3 bench.py --gpus 2 --gib 0.5 --steps 2 --warmup 1 \
+          --no-cpu-baseline > "$out/dist2.json" 2> "$out/dist2.err"
+      cat "$out/dist2.json" ;;
+    ab)
+      bash tools/ab.sh > "$out/ab.txt" 2>&1 && bash tools/ab.sh >> "$out/ab.txt" 2>&1
+      cat "$out/ab.txt" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
