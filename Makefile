@@ -7,7 +7,7 @@ BUILD  := build
 CSRC   := lz4mt_amd/csrc
 LIB    := lz4mt_amd/liblz4mt_amd.so
 OBJS   := $(BUILD)/lz4mt_kernels_enc.o $(BUILD)/lz4mt_kernels_dec.o $(BUILD)/lz4mt_hc.o $(BUILD)/lz4mt_engine.o \
-          $(BUILD)/lz4mt_frame.o $(BUILD)/lz4mt_io.o
+          $(BUILD)/lz4mt_frame.o $(BUILD)/lz4mt_io.o $(BUILD)/lz4mt_shard.o
 HDRS   := $(CSRC)/lz4mt_device.h $(CSRC)/lz4mt_host.h include/lz4mt.h include/lz4mt_hip.h include/lz4mt_io.h
 
 all: $(LIB) oracle

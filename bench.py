@@ -69,6 +69,12 @@ def parse():
     p.add_argument("--block-dependent", action="store_true", help="-BD frames (serial; not the headline)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-mib", type=int, default=1024, help="CPU baseline sample (MiB, all threads)")
+    p.add_argument("--gather", choices=["streamed", "after"], default="streamed",
+                   help="N > 1: stream the shards' records to rank 0 while they encode (dist.compress_gather_streamed), "
+                        "or gather each finished shard frame after its encode (dist.gather_frame)")
+    p.add_argument("--transport", choices=["ipc", "rccl"], default="ipc",
+                   help="streamed gather: packs pushed by copy engines into IPC-shared root buffers (default; RCCL "
+                        "kernels need LDS that the running encodes hold), or RCCL point-to-point")
     p.add_argument("--decompress-only", action="store_true",
                    help="configs[2]: time only the decompression of a pre-compressed stream (use --gib 32)")
     return p.parse_args()
@@ -318,25 +324,58 @@ def main():
     if a.decompress_only:   # compress once, untimed
         compress()
         torch.cuda.synchronize()
+    streamed = world > 1 and a.gather == "streamed" and not a.decompress_only
+    own_body = 0
+    if streamed:   # the shard engine's streams and workspace, the control group and transport, made once
+        eng = D.HipShardEngine(dev)
+        shard_ws = L.shard_workspace(n, sd, device=dev)
+        del ws
+        ctrl = dist.new_group(backend="gloo") if backend == "nccl" else None
+        transport = D.IpcPushTransport(dev) if a.transport == "ipc" else D.RcclTransport()
+        transport_name = a.transport
     L.lib.lz4mtHipSetTiming(1)
     tc = td = ts = tg = 0.0
-    enc_ms, dec_ms, frame_len = [], [], 0
+    enc_ms, dec_ms, frame_len, exposed_ms, rounds = [], [], 0, [], []
     full = piece = None
     for it in range(a.warmup + a.steps):
         timed = it >= a.warmup
         t0 = sync_all()
         tm = None
-        if not a.decompress_only:
-            compress()
-        frame_len = int(fsz[0].item())          # synchronises the stream
-        if not a.decompress_only:
-            tm = timings()
-        tl = time.perf_counter()
-        if world > 1:   # the gather belongs to compress
-            full = D.gather_frame(frame_buf, frame_len, dst=0)
+        tgr = 0.0
+        if streamed:   # encode + streamed gather: ONE frame on rank 0
+            st_ = {}
+            try:
+                full = D.compress_gather_streamed(src, sd, dst=0, engine=eng, ws=shard_ws, stats=st_,
+                                                  transport=transport, ctrl=ctrl)
+            except RuntimeError as e:   # the IPC setup failed on some rank (collectively): RCCL instead
+                if transport_name != "ipc":
+                    raise
+                print(f"bench.py: IPC push unavailable ({e}); streamed gather over RCCL", file=sys.stderr)
+                transport, transport_name = D.RcclTransport(), "rccl (IPC setup failed)"
+                full = D.compress_gather_streamed(src, sd, dst=0, engine=eng, ws=shard_ws, stats=st_,
+                                                  transport=transport, ctrl=ctrl)
+            end_ev = torch.cuda.Event(enable_timing=True)
+            end_ev.record()
             torch.cuda.synchronize()
-        t1 = sync_all()
-        tgr = time.perf_counter() - tl if world > 1 else 0.0
+            t1 = sync_all()
+            tm = [eng.enc_start.elapsed_time(eng.enc_done)]
+            exposed_ms.append(eng.enc_done.elapsed_time(end_ev) if rank == 0 else 0.0)
+            tgr = exposed_ms[-1] * 1e-3
+            rounds.append(st_.get("rounds", 0))
+            frame_len = full.numel() if rank == 0 else 0
+            own_body = st_.get("own_body_bytes", 0)
+        else:
+            if not a.decompress_only:
+                compress()
+            frame_len = int(fsz[0].item())          # synchronises the stream
+            if not a.decompress_only:
+                tm = timings()
+            tl = time.perf_counter()
+            if world > 1:   # the gather belongs to compress
+                full = D.gather_frame(frame_buf, frame_len, dst=0)
+                torch.cuda.synchronize()
+            t1 = sync_all()
+            tgr = time.perf_counter() - tl if world > 1 else 0.0
         if world > 1:
             piece = D.scatter_frame(full if rank == 0 else None, full.numel() if rank == 0 else 0, src=0,
                                     device=dev)
@@ -382,11 +421,13 @@ def main():
 
     enc_avg = sum(enc_ms) / len(enc_ms) if enc_ms else None
     dec_avg = sum(dec_ms) / len(dec_ms) if dec_ms else None
-    body = frame_len - 7 - 4 - (4 if sck else 0)
-    alg = n + body                           # algorithmic bytes per launch: in + out
+    # algorithmic bytes per launch: in + out of this rank's encode
+    body = own_body if streamed else frame_len - 7 - 4 - (4 if sck else 0)
+    alg = n + body
     # the kernels the timing marks bracket in this mode
     enc_k = ("k_encode_hc_bd" if a.block_dependent and a.level >= 3 else "k_encode_linked_round"
-             if a.block_dependent else "k_encode_hc" if a.level >= 3 else "k_encode")
+             if a.block_dependent else "k_encode_hc" if a.level >= 3 else
+             "k_encode_pub (+ k_xxh32_stored)" if streamed else "k_encode")
     dec_k = "k_decode_linked" if a.block_dependent else "k_decode"
     roof = dec_roof = None
     if enc_avg:
@@ -434,14 +475,22 @@ def main():
                                                                    if world > 1 else "")},
             "compress_GiBps": round(comp_gibps, 3) if comp_gibps else None,
             "decompress_GiBps": round(decomp_gibps, 3),
-            "ratio": round(n / frame_len, 4), "frame_bytes": frame_len,
+            "ratio": round((n_total / frame_len) if streamed else (n / frame_len), 4), "frame_bytes": frame_len,
             "roundtrip_ok": ok, "roofline": roof, "decode_roofline": dec_roof, "cpu_baseline": cpu,
         }
+        if streamed:   # root's GPU time from its own encode's end to the assembled frame
+            line.update({"gather": f"streamed beside the encode (dist.compress_gather_streamed, {transport_name})",
+                         "gather_exposed_ms": round(sum(exposed_ms[a.warmup:]) / max(1, K), 3),
+                         "gather_rounds": round(sum(rounds[a.warmup:]) / max(1, K), 1)})
+        elif world > 1:
+            line.update({"gather": "after the encode (dist.gather_frame)"})
         if world > 1:
             line.update({"gather_ms": round(tg / K * 1e3, 3), "scatter_ms": round(ts / K * 1e3, 3),
                          "stitched_frame_bytes": full.numel(), "stitched_frame_ok": stitched_ok,
                          "roundtrip_with_scatter_GiBps": round(total / GiB / (tc + ts + td), 3)})
         print(json.dumps(line), flush=True)
+    if streamed:
+        transport.close()
     if world > 1:
         dist.destroy_process_group()
     if not ok:

@@ -134,7 +134,64 @@ void lz4mtHipReleaseCaches(void);
 void lz4mtHipSetTiming(int enable);
 int lz4mtHipGetTimings(float* ms4);
 
-/* ---- 4. diagnostics ----------------------------------------------------- */
+/* ---- 4. block-sharded multi-GPU compress, gather streamed beside the encode
+ * (lz4mt_amd/dist.py drives it over RCCL).  A shard is a
+ * contiguous block range of one -Sx stream (FLG.2 and FLG.3 off: they do not
+ * shard).  The sending rank launches its encode once, then packs rounds of
+ * whatever the encoder has published so far (each round one contiguous
+ * buffer: header, a descriptor per block, payload) and sends them while the
+ * encode runs; the root unpacks them into a mirror of that shard's slots and,
+ * once every shard is complete, assembles each shard's records into the one
+ * frame.  Replaces nothing in the reference (it has no multi-device path);
+ * the frame is the one lz4mtCompress writes for the whole stream
+ * (src/lz4mt.cpp:898-935). ------------------------------------------------ */
+/* Bytes of a shard workspace, and of the root's mirror of a shard (same
+ * layout); 0 for a descriptor that cannot shard. */
+uint64_t lz4mtHipShardWorkspaceSize(uint64_t n, const Lz4MtStreamDescriptor* sd);
+/* Largest pack one round can produce with at most perBlockCap bytes per block. */
+uint64_t lz4mtHipShardPackBound(uint64_t n, const Lz4MtStreamDescriptor* sd, uint32_t perBlockCap);
+/* The frame header lz4mtCompress writes for `sd` (magic .. header checksum)
+ * into out[19]; returns its length, -1 on a bad descriptor. */
+int lz4mtHipFrameHeader(const Lz4MtStreamDescriptor* sd, uint8_t* out);
+/* Launches the shard's encode (+ block checksums) on `stream`; 1 and 4 MiB
+ * blocks publish their progress as they go.  Asynchronous. */
+Lz4MtResult lz4mtHipShardEncode(const void* d_src, uint64_t n, const Lz4MtStreamDescriptor* sd, void* d_ws,
+                                uint64_t wsSize, void* stream);
+/* One round into d_pack (capacity >= lz4mtHipShardPackBound): final = 0 while
+ * the encode may still run (stream-ordered anywhere), final = 1 once it is
+ * done (stream-ordered after it; repeat until the header's flags bit 0 is
+ * set).  Header (64 B, little-endian): u64 magic, u64 payload bytes, u64
+ * bytes still to send, u64 bytes of this pack, u32 blocks, u32 flags
+ * (1 = shard complete), u64 the shard's record bytes (when complete). */
+Lz4MtResult lz4mtHipShardPack(const void* d_src, uint64_t n, const Lz4MtStreamDescriptor* sd, void* d_ws,
+                              uint64_t wsSize, void* d_pack, uint64_t packCap, uint32_t perBlockCap, int final,
+                              void* stream);
+/* Root: one received pack of an n-byte shard into its mirror (a buffer of
+ * lz4mtHipShardWorkspaceSize bytes). */
+Lz4MtResult lz4mtHipShardUnpack(const void* d_pack, uint64_t n, const Lz4MtStreamDescriptor* sd, void* d_mirror,
+                                uint64_t mirrorSize, void* stream);
+/* The shard's records (size word, payload, [checksum]) into d_body, as they
+ * stand in the frame of the whole stream.  d_ws: a complete mirror, or the
+ * shard workspace itself after its encode; d_src: the shard's source for the
+ * latter (incompressible blocks), NULL for a mirror.  Body bytes = the
+ * complete pack's record bytes. */
+Lz4MtResult lz4mtHipShardAssemble(const void* d_src, uint64_t n, const Lz4MtStreamDescriptor* sd, void* d_ws,
+                                  uint64_t wsSize, void* d_body, uint64_t bodyCap, void* stream);
+/* The root's receive buffers for the copy-engine push of packs: allocate
+ * (hipMalloc) and export an IPC handle (64 bytes); open / close another
+ * process's buffer (mapped for the calling thread's device); free; and an
+ * asynchronous device-to-device copy (a mapped peer buffer included).
+ * 0 on success, -1 otherwise. */
+int lz4mtHipIpcAlloc(uint64_t bytes, void** d_ptr, void* handle64);
+int lz4mtHipIpcOpen(const void* handle64, void** d_ptr);
+int lz4mtHipIpcClose(void* d_ptr);
+int lz4mtHipFree(void* d_ptr);
+int lz4mtHipCopyAsync(void* d_dst, const void* d_src, uint64_t n, void* stream);
+/* Record bytes of a complete shard workspace (or mirror): synchronises the
+ * stream; UINT64_MAX on bad arguments or a device error. */
+uint64_t lz4mtHipShardBodyBytes(uint64_t n, const Lz4MtStreamDescriptor* sd, void* d_ws, uint64_t wsSize, void* stream);
+
+/* ---- 5. diagnostics ----------------------------------------------------- */
 /* Runs s_memtime-stamped twins of the encode / decode kernels (never the
  * product launch) and sums per-phase shader cycles over all blocks.
  * encode (16 slots): [hash, table+dedup, candidate check, round issue,

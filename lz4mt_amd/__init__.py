@@ -24,7 +24,8 @@ __all__ = [
     "init_context", "init_stream_descriptor", "result_to_string", "result_to_exit_code", "make_sd",
     "compress", "decompress", "compress_block", "decompress_block", "compress_bound",
     "compress_frame", "decompress_frame", "frame_info", "frame_bound", "gen_synthetic", "xxh32",
-    "device_count", "stream_bound", "frame_records", "xxh32_chunks",
+    "device_count", "stream_bound", "frame_records", "xxh32_chunks", "frame_header", "shard_workspace",
+    "shard_pack_bound", "shard_encode", "shard_pack", "shard_unpack", "shard_assemble", "shard_body_bytes",
 ]
 
 lib = _abi.load()
@@ -263,3 +264,77 @@ def xxh32(t, stream=None):
     """XXH32 (seed 0) of a device tensor, computed on the device."""
     _check_dev(t, "tensor")
     return int(lib.lz4mtHipXxh32(ctypes.c_void_p(t.data_ptr()), t.numel(), _stream(stream)))
+
+
+# ---- block-sharded streamed gather (include/lz4mt_hip.h section 4; driven by dist.py)
+PACK_HEADER_BYTES = 64
+
+
+def frame_header(sd):
+    """The frame header lz4mtCompress writes for ``sd`` (bytes)."""
+    buf = (ctypes.c_uint8 * 20)()
+    k = lib.lz4mtHipFrameHeader(ctypes.byref(sd), buf)
+    if k < 0:
+        raise Lz4MtError(Result.BAD_ARG, "lz4mtHipFrameHeader")
+    return bytes(buf[:k])
+
+
+def shard_workspace(n, sd, device=None):
+    """Workspace of an n-byte shard encode (also the root's mirror of such a shard)."""
+    nbytes = int(lib.lz4mtHipShardWorkspaceSize(int(n), ctypes.byref(sd)))
+    if nbytes == 0:
+        raise Lz4MtError(Result.BAD_ARG, "lz4mtHipShardWorkspaceSize (the descriptor does not shard)")
+    return torch.empty(nbytes, dtype=torch.uint8, device=device or "cuda")
+
+
+def shard_pack_bound(n, sd, per_block_cap):
+    return int(lib.lz4mtHipShardPackBound(int(n), ctypes.byref(sd), int(per_block_cap)))
+
+
+def shard_encode(src, sd, ws, stream=None):
+    """Launches the shard's encode (+ block checksums); asynchronous on ``stream``."""
+    _check_dev(src, "src")
+    r = lib.lz4mtHipShardEncode(ctypes.c_void_p(src.data_ptr() if src.numel() else ws.data_ptr()), src.numel(),
+                                ctypes.byref(sd), ctypes.c_void_p(ws.data_ptr()), ws.numel(), _stream(stream))
+    if r != Result.OK:
+        raise Lz4MtError(r, "lz4mtHipShardEncode")
+
+
+def shard_pack(src, sd, ws, pack, per_block_cap, final, stream=None):
+    """One round into ``pack``; asynchronous.  The 64-byte header at pack[:64]
+    says how many bytes to send (u64 at 24) and whether the shard is complete
+    (u32 at 36, bit 0)."""
+    r = lib.lz4mtHipShardPack(ctypes.c_void_p(src.data_ptr() if src.numel() else ws.data_ptr()), src.numel(),
+                              ctypes.byref(sd), ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                              ctypes.c_void_p(pack.data_ptr()), pack.numel(), int(per_block_cap), int(bool(final)),
+                              _stream(stream))
+    if r != Result.OK:
+        raise Lz4MtError(r, "lz4mtHipShardPack")
+
+
+def shard_unpack(pack, n, sd, mirror, stream=None):
+    """A received pack (a tensor, or the device address of one) into ``mirror``."""
+    ptr = pack if isinstance(pack, int) else pack.data_ptr()
+    r = lib.lz4mtHipShardUnpack(ctypes.c_void_p(ptr), int(n), ctypes.byref(sd),
+                                ctypes.c_void_p(mirror.data_ptr()), mirror.numel(), _stream(stream))
+    if r != Result.OK:
+        raise Lz4MtError(r, "lz4mtHipShardUnpack")
+
+
+def shard_assemble(src, n, sd, ws, body, stream=None):
+    """The shard's records into ``body`` (src: the shard's own source, or None for a mirror)."""
+    r = lib.lz4mtHipShardAssemble(ctypes.c_void_p(src.data_ptr() if src is not None and src.numel() else None),
+                                  int(n), ctypes.byref(sd), ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                                  ctypes.c_void_p(body.data_ptr() if body.numel() else None), body.numel(),
+                                  _stream(stream))
+    if r != Result.OK:
+        raise Lz4MtError(r, "lz4mtHipShardAssemble")
+
+
+def shard_body_bytes(n, sd, ws, stream=None):
+    """Record bytes of a complete shard workspace (synchronises ``stream``)."""
+    v = int(lib.lz4mtHipShardBodyBytes(int(n), ctypes.byref(sd), ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                                       _stream(stream)))
+    if v == (1 << 64) - 1:
+        raise Lz4MtError(Result.ERROR, "lz4mtHipShardBodyBytes")
+    return v

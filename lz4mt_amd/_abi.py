@@ -114,6 +114,20 @@ PROTOTYPES = {
     "lz4mtHipReleaseCaches": (None, []),
     "lz4mtHipSetTiming": (None, [c_int]),
     "lz4mtHipGetTimings": (c_int, [ctypes.POINTER(c_float)]),
+    "lz4mtHipShardWorkspaceSize": (c_uint64, [c_uint64, SD_P]),
+    "lz4mtHipShardPackBound": (c_uint64, [c_uint64, SD_P, c_uint32]),
+    "lz4mtHipFrameHeader": (c_int, [SD_P, c_void_p]),
+    "lz4mtHipShardEncode": (c_int, [c_void_p, c_uint64, SD_P, c_void_p, c_uint64, c_void_p]),
+    "lz4mtHipShardPack": (c_int, [c_void_p, c_uint64, SD_P, c_void_p, c_uint64, c_void_p, c_uint64, c_uint32, c_int,
+                                  c_void_p]),
+    "lz4mtHipShardUnpack": (c_int, [c_void_p, c_uint64, SD_P, c_void_p, c_uint64, c_void_p]),
+    "lz4mtHipShardAssemble": (c_int, [c_void_p, c_uint64, SD_P, c_void_p, c_uint64, c_void_p, c_uint64, c_void_p]),
+    "lz4mtHipIpcAlloc": (c_int, [c_uint64, ctypes.POINTER(c_void_p), c_void_p]),
+    "lz4mtHipIpcOpen": (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
+    "lz4mtHipIpcClose": (c_int, [c_void_p]),
+    "lz4mtHipFree": (c_int, [c_void_p]),
+    "lz4mtHipCopyAsync": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
+    "lz4mtHipShardBodyBytes": (c_uint64, [c_uint64, SD_P, c_void_p, c_uint64, c_void_p]),
     "lz4mtHipDebugEncodeStats": (c_int, [c_void_p, c_uint64, c_uint32, ctypes.POINTER(c_uint64), c_void_p]),
     "lz4mtHipDebugDecodeStats": (c_int, [c_void_p, c_uint64, ctypes.POINTER(c_uint64), c_void_p]),
     # lz4mt_io.h

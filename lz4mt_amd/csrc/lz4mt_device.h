@@ -80,6 +80,10 @@ struct AuxStream {
 hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                          uint8_t* slots, uint64_t slotStride, uint32_t capOverride, int32_t* csize,
                          hipStream_t st);
+// k_encode with per-block progress publishing (pub[b]: bytes of slot b final;
+// slot stride = blockSize), for the block-sharded streamed gather
+hipError_t launch_encode_pub(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                             uint8_t* slots, int32_t* csize, uint32_t* pub, hipStream_t st);
 hipError_t launch_decode(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax,
                          uint8_t* out, uint64_t outCap, int32_t* dsize, hipStream_t st);
 hipError_t launch_xxh32_stored(const uint8_t* src, const uint8_t* slots, uint64_t srcSize, uint32_t blockSize,

@@ -798,10 +798,25 @@ __device__ __forceinline__ void store_pend(const PendSeq& p, const SrcRing& V, g
 // positions in the coordinates of k_encode_linked (block at o0 = 65536, its
 // 64 KiB history below), the table carried in T unless lk.fresh, candidates
 // bounded by lk (see LinkArgs); n = o0 + block length.
-template <bool ST, bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false>
+// PUB (the block-sharded streamed gather, lz4mt_shard.hip): every time the
+// output crosses a multiple of kPubBytes, the bytes written so far are
+// published -- the wave drains its stores, writes its XCD's L2 back (agent
+// release) and stores the byte count to *pub (relaxed, agent scope): a
+// concurrent kernel that reads *pub and then (after its own agent acquire,
+// e.g. a new launch) the slot's bytes below it sees them final
+// (MI355X_MICROARCH.md, valid hand-off forms).
+constexpr uint32_t kPubShift = 16;   // publish every 64 KiB of output
+__device__ __forceinline__ void publish_progress(uint32_t* pub, uint32_t v) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (laneid() == 0) __hip_atomic_store(pub, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool ST, bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false, bool PUB = false>
 __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
                                    l_u32* __restrict__ T, l_u8* __restrict__ R, uint64_t* acc,
-                                   LinkArgs lk = LinkArgs{0, 0, 0, true}) {
+                                   LinkArgs lk = LinkArgs{0, 0, 0, true}, uint32_t* pub = nullptr) {
     using G = V5Geo<U16, SPLIT, LINK, P17>;
     const G tab{T};
     const uint32_t L = laneid();
@@ -1068,6 +1083,9 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             pe.off = ip - cd;
             pe.anchor = anchor;
             havePe = !fail;
+            if constexpr (PUB) {   // every sequence before this one has been stored: [0, op) is final
+                if ((op ^ (op + 1 + litExt + lit + 2 + mlExt)) >> kPubShift) publish_progress(pub, op);
+            }
             op += 1 + litExt + lit + 2 + mlExt;
             const uint32_t ipe = ip + kMinMatch + mc;
             anchor = ipe;
@@ -1132,6 +1150,42 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
     else
         r = encode_block<false, false, false>(s, n, d, cap, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
     if (laneid() == 0) csize[b] = r;
+}
+
+// k_encode with progress publishing (block-sharded streamed gather): the
+// same parse and bytes; pub[b] = bytes of slot b already final.  Only the
+// v5 path (65 547 B .. 4 MiB blocks) publishes; other blocks are sent whole
+// once the launch is done.
+__global__ void __launch_bounds__(64) k_encode_pub(const uint8_t* __restrict__ src, uint64_t srcSize,
+                                                   uint32_t blockSize, uint8_t* __restrict__ slots,
+                                                   uint64_t slotStride, int32_t* __restrict__ csize,
+                                                   uint32_t* __restrict__ pub) {
+    ENCODE_LDS
+    const uint32_t b = blockIdx.x;
+    const uint64_t off = (uint64_t)b * blockSize;
+    const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
+    g_cu8* s = gptr(src) + off;
+    g_u8* d = gptr(slots) + (uint64_t)b * slotStride;
+    l_u32* Tl = (l_u32*)T;
+    l_u8* Sl = (l_u8*)S;
+    l_u8* Xl = (l_u8*)X;
+    int32_t r;
+    if (n < (uint32_t)kLimit64K)
+        r = encode_block<true, false, false>(s, n, d, n, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
+    else if (n <= (1u << kPosBits))
+        r = encode_block_v5<false, false, false, false, false, true>(s, n, d, n, Tl, Xl, nullptr,
+                                                                     LinkArgs{0, 0, 0, true}, pub + b);
+    else
+        r = encode_block<false, false, false>(s, n, d, n, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
+    if (laneid() == 0) csize[b] = r;
+}
+
+hipError_t launch_encode_pub(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                             uint8_t* slots, int32_t* csize, uint32_t* pub, hipStream_t st) {
+    if (nBlocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_encode_pub, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots,
+                       (uint64_t)blockSize, csize, pub);
+    return hipGetLastError();
 }
 
 // The v5 encoder with the 3-byte table (V5Geo P17): 14.25 KiB of LDS, 11

@@ -21,6 +21,7 @@ grouped point-to-point transfers; each rank decodes header + records + EOS
 locally.  ``verify_stitched`` checks a stitched frame against every rank's
 source (root decode, per-shard chunk digests).
 """
+import ctypes
 import struct
 
 import torch
@@ -350,3 +351,297 @@ def verify_stitched(full, shard_src, decode, digests, dst=0, group=None):
             raise err
         raise RuntimeError(f"verify_stitched: rank {dst} could not decode the stitched frame")
     return v == 1
+
+
+# ---------------------------------------------------------------------------
+# Streamed gather: the compress-side exchange overlapped with the encode
+# ---------------------------------------------------------------------------
+PACK_HDR = 64   # lz4mtHipShardPack's header: u64 magic, payload, remaining, pack bytes; u32 nb, flags; u64 body
+
+
+def parse_pack_header(b):
+    """(pack bytes, payload bytes, shard complete, the shard's record bytes) from a pack header (64 bytes)."""
+    magic, payload, _remaining, packed, _nb, flags, body = struct.unpack_from("<QQQQIIQ", bytes(b), 0)
+    if magic != 0x44485354344D5A4C:
+        raise ValueError("not a shard pack")
+    return packed, payload, bool(flags & 1), body
+
+
+class HipShardEngine:
+    """The device side of compress_gather_streamed on this rank's GPU
+    (include/lz4mt_hip.h section 4).  The encode runs on its own stream and
+    the rounds' packs on another, so that neither the encode nor the RCCL
+    transfers (which torch orders after the CURRENT stream) wait for each
+    other."""
+
+    def __init__(self, device=None):
+        import lz4mt_amd as L
+        self.L = L
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.enc_stream = torch.cuda.Stream(self.device)
+        self.pack_stream = torch.cuda.Stream(self.device)
+        self.enc_done = torch.cuda.Event()
+
+    def header(self, sd):
+        return self.L.frame_header(sd)
+
+    def workspace(self, n, sd):
+        return self.L.shard_workspace(n, sd, device=self.device)
+
+    def pack_buffer(self, n, sd, cap):
+        return torch.empty(self.L.shard_pack_bound(n, sd, cap), dtype=torch.uint8, device=self.device)
+
+    def encode(self, src, sd, ws):
+        self.enc_stream.wait_stream(torch.cuda.current_stream(self.device))   # src / ws ready
+        self.enc_start = torch.cuda.Event(enable_timing=True)
+        self.enc_done = torch.cuda.Event(enable_timing=True)
+        self.enc_start.record(self.enc_stream)
+        self.L.shard_encode(src, sd, ws, stream=self.enc_stream)
+        self.enc_done.record(self.enc_stream)
+
+    def encode_finished(self):
+        return self.enc_done.query()
+
+    def pack(self, src, sd, ws, buf, cap, final):
+        """One round; returns parse_pack_header's fields -- waits for the pack."""
+        ps = self.pack_stream
+        ps.wait_stream(torch.cuda.current_stream(self.device))   # the previous send of `buf` is done
+        if final:
+            ps.wait_event(self.enc_done)
+        self.L.shard_pack(src, sd, ws, buf, cap, final, stream=ps)
+        with torch.cuda.stream(ps):
+            h = buf[:PACK_HDR].cpu()   # synchronises the pack stream
+        return parse_pack_header(h.numpy().tobytes())
+
+    def unpack(self, buf, n, sd, mirror):
+        self.L.shard_unpack(buf, n, sd, mirror)
+
+    def body_bytes(self, n, sd, ws):
+        torch.cuda.current_stream(self.device).wait_event(self.enc_done)
+        return self.L.shard_body_bytes(n, sd, ws)
+
+    def assemble(self, src, n, sd, ws, body):
+        torch.cuda.current_stream(self.device).wait_event(self.enc_done)
+        self.L.shard_assemble(src, n, sd, ws, body)
+
+
+class RcclTransport:
+    """Packs travel as point-to-point transfers of a torch.distributed group
+    (RCCL under the nccl backend) after each round's exchange of sizes.  On
+    MI355X an RCCL transfer is a kernel needing ~37 KiB of LDS per
+    workgroup, which no CU has free while its 8 encoder waves hold all 160
+    KiB: the transfers then wait for the encodes to end.  Used by the CPU
+    tests (gloo) and as the fallback of IpcPushTransport."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def setup(self, E, sizes, sd, cap, rank, dst, ctrl):
+        self.rank, self.dst = rank, dst
+        self.recv = {r: E.pack_buffer(sizes[r], sd, cap) for r in range(len(sizes)) if r != dst} \
+            if rank == dst else {}
+
+    def push(self, k, buf, nbytes):
+        pass
+
+    def exchange(self, k, buf, rows):
+        peer = (lambda r: dist.get_global_rank(self.group, r)) if self.group is not None else (lambda r: r)
+        ops = []
+        if self.rank == self.dst:
+            for r, row in enumerate(rows):
+                if r != self.dst and row[0]:
+                    ops.append(dist.P2POp(dist.irecv, self.recv[r][:row[0]], peer(r), self.group))
+        elif rows[self.rank][0]:
+            ops.append(dist.P2POp(dist.isend, buf[:rows[self.rank][0]], peer(self.dst), self.group))
+        for w in (dist.batch_isend_irecv(ops) if ops else []):
+            w.wait()
+
+    def received(self, r, k):
+        return self.recv[r]
+
+    def close(self):
+        self.recv = {}
+
+
+class IpcPushTransport:
+    """Each sender's pack goes straight into a receive buffer in the root's
+    HBM, exported once by IPC handle (lz4mtHipIpcAlloc / lz4mtHipIpcOpen),
+    with an asynchronous device-to-device copy (lz4mtHipCopyAsync: a copy
+    engine over xGMI, no kernel and no LDS) before the round's exchange; two
+    buffers per sender alternate, and the root finishes unpacking round k
+    before it joins round k + 1's exchange, so a sender never overwrites a
+    pack the root still reads.  Only the round's sizes go over the (gloo)
+    control group."""
+
+    def __init__(self, device):
+        self.device = device
+        self.bufs, self.remote, self.copy_stream = {}, [], None
+
+    def setup(self, E, sizes, sd, cap, rank, dst, ctrl):
+        """Collective over ``ctrl``: every rank either sets up or raises."""
+        import lz4mt_amd as L
+        self.L, self.rank, self.dst = L, rank, dst
+        if self.bufs or self.remote:   # buffers of an earlier call with the same shapes
+            return
+        handles, err = {}, None
+        if rank == dst:
+            try:
+                for r in range(len(sizes)):
+                    if r == dst:
+                        continue
+                    nbytes = L.shard_pack_bound(sizes[r], sd, cap)
+                    pair = []
+                    for _ in range(2):
+                        ptr, h = ctypes.c_void_p(), (ctypes.c_uint8 * 64)()
+                        if L.lib.lz4mtHipIpcAlloc(nbytes, ctypes.byref(ptr), h) != 0:
+                            raise RuntimeError("lz4mtHipIpcAlloc failed")
+                        pair.append(ptr.value)
+                        handles.setdefault(r, []).append(bytes(h))
+                    self.bufs[r] = pair
+            except RuntimeError as e:
+                err, handles = e, None
+        obj = [handles]
+        dist.broadcast_object_list(obj, src=dst if ctrl is None else dist.get_global_rank(ctrl, dst), group=ctrl)
+        ok = obj[0] is not None
+        if ok and rank != dst:
+            try:
+                for h in obj[0][rank]:
+                    ptr = ctypes.c_void_p()
+                    hb = (ctypes.c_uint8 * 64).from_buffer_copy(h)
+                    if L.lib.lz4mtHipIpcOpen(hb, ctypes.byref(ptr)) != 0:
+                        raise RuntimeError("lz4mtHipIpcOpen failed")
+                    self.remote.append(ptr.value)
+                self.copy_stream = torch.cuda.Stream(self.device)
+            except RuntimeError as e:
+                err, ok = e, False
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=ctrl)
+        if int(flag.item()) == 0:
+            self.close()
+            raise err or RuntimeError("IpcPushTransport: another rank could not set up its buffers")
+
+    def push(self, k, buf, nbytes):
+        if self.rank == self.dst or not nbytes:
+            if self.rank == self.dst:   # round k - 1's unpacks are done before round k's exchange
+                torch.cuda.current_stream(self.device).synchronize()
+            return
+        st = self.copy_stream
+        if self.L.lib.lz4mtHipCopyAsync(ctypes.c_void_p(self.remote[k % 2]), ctypes.c_void_p(buf.data_ptr()), nbytes,
+                                        ctypes.c_void_p(st.cuda_stream)) != 0:
+            raise RuntimeError("lz4mtHipCopyAsync failed")
+        st.synchronize()
+
+    def exchange(self, k, buf, rows):
+        pass
+
+    def received(self, r, k):
+        return self.bufs[r][k % 2]
+
+    def close(self):
+        for p in self.remote:
+            self.L.lib.lz4mtHipIpcClose(ctypes.c_void_p(p))
+        for pair in self.bufs.values():
+            for p in pair:
+                self.L.lib.lz4mtHipFree(ctypes.c_void_p(p))
+        self.bufs, self.remote = {}, []
+
+
+def compress_gather_streamed(src, sd, dst=0, group=None, engine=None, per_block_cap=128 << 10, ws=None, stats=None,
+                             min_round_s=0.002, transport=None, ctrl=None):
+    """Compresses this rank's shard and gathers every shard's records into ONE
+    frame on ``dst`` WHILE the shards encode.
+
+    Each rank holds a contiguous block range of one stream (ranks in stream
+    order, ``shard_blocks``), ``src`` its bytes.  Every rank launches its
+    encode (lz4mtHipShardEncode: 1 and 4 MiB blocks publish their progress
+    every 64 KiB of output), then the ranks run rounds together until every
+    shard is complete: a sender packs what its encoder has published since
+    the last round (at most ``per_block_cap`` bytes per block; after its
+    encode: the tails, incompressible blocks' source bytes, stored sizes and
+    block checksums) and hands it to the ``transport`` (IpcPushTransport: a
+    copy-engine write into the root's buffer; RcclTransport, the default:
+    point-to-point after the exchange); one all_gather over ``ctrl`` (a gloo
+    group: no GPU kernel) of (pack bytes, complete, record bytes) per rank;
+    the root unpacks each pack into its mirror of that shard.  At the end the
+    root assembles each shard's records at its place in the frame (header,
+    records in rank order, EOS): byte for byte the frame one process writes
+    for the whole stream (src/lz4mt.cpp:898-935; blocks are independent,
+    914-918).  Returns the frame on ``dst`` (None elsewhere).  ``stats``
+    (dict), if given, receives the round count and the bytes per round.
+    While the encodes run, rounds start at least ``min_round_s`` apart.
+    """
+    import time
+    ctrl = ctrl if ctrl is not None else group
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    E = engine or HipShardEngine(src.device)
+    T = transport or RcclTransport(group)
+    dev = src.device
+    n = src.numel()
+    alln = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(alln, torch.tensor([n], dtype=torch.int64), group=ctrl)
+    sizes = [int(x.item()) for x in alln]
+    ws = ws if ws is not None else E.workspace(n, sd)
+    T.setup(E, sizes, sd, per_block_cap, rank, dst, ctrl)
+    E.encode(src, sd, ws)
+    mirrors = {r: E.workspace(sizes[r], sd) for r in range(world) if r != rank} if rank == dst else {}
+    bufs = [] if rank == dst else [E.pack_buffer(n, sd, per_block_cap), E.pack_buffer(n, sd, per_block_cap)]
+    complete = rank == dst          # the root sends nothing; it assembles its own shard from its workspace
+    body = {}
+    rounds, sent_log = 0, []
+    t_last = 0.0
+    while True:
+        nbytes, body_now, now_complete = 0, 0, complete
+        buf = None
+        if not complete:
+            final = E.encode_finished()
+            if not final:
+                wait = t_last + min_round_s - time.perf_counter()
+                if wait > 0:
+                    time.sleep(wait)
+            t_last = time.perf_counter()
+            buf = bufs[rounds % 2]
+            nbytes, payload, done, b = E.pack(src, sd, ws, buf, per_block_cap, final)
+            if final and done:
+                now_complete, body_now = True, b
+            elif not payload:
+                nbytes = 0   # nothing published since the last round: send nothing
+        T.push(rounds, buf, nbytes)
+        info = torch.tensor([nbytes, 1 if now_complete else 0, body_now], dtype=torch.int64)
+        alli = [torch.zeros(3, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(alli, info, group=ctrl)
+        rows = [[int(v) for v in x.tolist()] for x in alli]
+        T.exchange(rounds, buf, rows)
+        if rank == dst:
+            for r in range(world):
+                if r != rank and rows[r][0]:
+                    E.unpack(T.received(r, rounds), sizes[r], sd, mirrors[r])
+        for r in range(world):
+            if rows[r][1] and r not in body:
+                body[r] = rows[r][2]
+        complete = now_complete
+        rounds += 1
+        sent_log.append(sum(row[0] for row in rows))
+        if all(row[1] for row in rows):
+            break
+    if stats is not None:
+        stats.update(rounds=rounds, bytes_per_round=sent_log)
+    if rank != dst:
+        return None
+    body[rank] = E.body_bytes(n, sd, ws)
+    if stats is not None:
+        stats["own_body_bytes"] = body[rank]
+    head = E.header(sd)
+    total = len(head) + sum(body[r] for r in range(world)) + 4
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    out[:len(head)] = torch.frombuffer(bytearray(head), dtype=torch.uint8).to(dev)
+    pos = len(head)
+    for r in range(world):
+        piece = out[pos:pos + body[r]]
+        if r == rank:
+            E.assemble(src, n, sd, ws, piece)
+        else:
+            E.assemble(None, sizes[r], sd, mirrors[r], piece)
+        pos += body[r]
+    out[pos:pos + 4] = 0
+    return out

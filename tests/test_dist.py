@@ -250,3 +250,192 @@ def test_bad_frame_raises_on_every_rank(kind):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(r[1].startswith("raised") for r in res), res
+
+
+# ---------------------------------------------------------------------------
+# compress_gather_streamed: the round protocol on the CPU with a mock engine
+# ---------------------------------------------------------------------------
+class MockShardEngine:
+    """CPU stand-in for dist.HipShardEngine (test infrastructure): the same
+    pack wire format (lz4mt_shard.hip: 64-byte header, 16-byte descriptor
+    per block, stored sizes, block checksums, payload at a 256-byte
+    boundary), the encoder's output taken from the oracle (the checker) and
+    published a little more every round, at a per-block pace, so blocks
+    finish out of step; the encode of rank r ends after `2 + r` rounds.
+    Blocks that end incompressible first publish bytes that are NOT their
+    stored bytes (the device encoder publishes a prefix before it gives
+    up), so the last round's switch to the source bytes is exercised."""
+
+    def __init__(self, rank, bid, rounds_to_finish):
+        self.bm = 1 << (8 + 2 * bid)
+        self.rounds_to_finish = rounds_to_finish
+        self.calls = 0
+
+    def header(self, sd):
+        import lz4mt_amd as L   # host-only code of the library: no device needed
+        return L.frame_header(sd)
+
+    def workspace(self, n, sd):
+        nb = (n + self.bm - 1) // self.bm
+        return {"n": n, "nb": nb, "slots": [bytearray(self.bm) for _ in range(nb)], "csize": [0] * nb,
+                "bsum": [0] * nb, "sent": [0] * nb}
+
+    def pack_buffer(self, n, sd, cap):
+        nb = (n + self.bm - 1) // self.bm
+        return torch.zeros(self._data_off(nb) + nb * min(cap, self.bm) + 64, dtype=torch.uint8)
+
+    @staticmethod
+    def _data_off(nb):
+        return (64 + 24 * nb + 255) & ~255
+
+    def encode(self, src, sd, ws):
+        import xxhash
+        data = bytes(src.numpy().tobytes())
+        self.src, self.final, self.pace = data, [], []
+        for b in range(ws["nb"]):
+            blk = data[b * self.bm:(b + 1) * self.bm]
+            c = oracle.compress_block(blk, len(blk))   # cap = n (src/lz4mt.cpp:391)
+            cs = len(c) if c else 0
+            ws["csize"][b] = cs
+            ws["bsum"][b] = xxhash.xxh32(c if cs else blk).intdigest()
+            self.final.append(c if cs else b"\xEE" * (len(blk) // 3))   # a raw block's abandoned prefix
+            self.pace.append(1 + (b * 7919) % 5)
+
+    def encode_finished(self):
+        return self.calls >= self.rounds_to_finish
+
+    def _published(self, b):
+        f = self.final[b]
+        return min(len(f), len(f) * self.calls * self.pace[b] // (4 * self.rounds_to_finish))
+
+    def pack(self, src, sd, ws, buf, cap, final):
+        import struct
+        nb, raw_bit = ws["nb"], 0x80000000
+        cap = min(cap, self.bm)
+        b0 = bytearray(buf.numel())
+        doff, off, rem, body = self._data_off(nb), 0, 0, 0
+        for b in range(nb):
+            n_b = min(self.bm, ws["n"] - b * self.bm)
+            s = ws["sent"][b]
+            raw = False
+            if final:
+                cs = ws["csize"][b]
+                if cs > 0:
+                    hi, srcb = cs, self.final[b]
+                else:
+                    if not s & raw_bit:
+                        s = raw_bit
+                    raw, hi, srcb = True, n_b, self.src[b * self.bm:b * self.bm + n_b]
+                body += 4 + (cs if cs > 0 else n_b) + (4 if sd.flg.blockChecksum else 0)
+                struct.pack_into("<i", b0, 64 + 16 * nb + 4 * b, cs)
+                struct.pack_into("<I", b0, 64 + 20 * nb + 4 * b, ws["bsum"][b] if sd.flg.blockChecksum else 0)
+            else:
+                hi, srcb = self._published(b), self.final[b]
+            lo = s & ~raw_bit
+            avail = max(hi - lo, 0)
+            ln = min(avail, cap)
+            struct.pack_into("<IIQ", b0, 64 + 16 * b, lo | (raw_bit if raw else 0), ln, off)
+            b0[doff + off:doff + off + ln] = srcb[lo:lo + ln]
+            ws["sent"][b] = (raw_bit if raw else 0) | (lo + ln)
+            off += ln
+            rem += avail - ln
+        flags = 1 if final and rem == 0 else 0
+        struct.pack_into("<QQQQIIQ", b0, 0, 0x44485354344D5A4C, off, rem, doff + off, nb, flags, body if final else 0)
+        buf.copy_(torch.frombuffer(b0, dtype=torch.uint8))
+        self.calls += 1
+        return D.parse_pack_header(bytes(b0[:64]))
+
+    def unpack(self, buf, n, sd, mirror):
+        import struct
+        b0 = bytes(buf.numpy().tobytes())
+        nb = mirror["nb"]
+        flags = struct.unpack_from("<I", b0, 36)[0]
+        doff = self._data_off(nb)
+        for b in range(nb):
+            lo, ln, off = struct.unpack_from("<IIQ", b0, 64 + 16 * b)
+            lo &= 0x7FFFFFFF
+            mirror["slots"][b][lo:lo + ln] = b0[doff + off:doff + off + ln]
+            if flags & 1:
+                mirror["csize"][b] = struct.unpack_from("<i", b0, 64 + 16 * nb + 4 * b)[0]
+                mirror["bsum"][b] = struct.unpack_from("<I", b0, 64 + 20 * nb + 4 * b)[0]
+
+    def _records(self, src, ws, sd):
+        import struct
+        out = bytearray()
+        for b in range(ws["nb"]):
+            n_b = min(self.bm, ws["n"] - b * self.bm)
+            cs = ws["csize"][b]
+            if src is not None:   # the rank's own shard: its encoder output / source
+                pay = self.final[b] if cs > 0 else self.src[b * self.bm:b * self.bm + n_b]
+            else:
+                pay = bytes(ws["slots"][b][:cs if cs > 0 else n_b])
+            out += struct.pack("<I", cs if cs > 0 else (n_b | 0x80000000)) + pay
+            if sd.flg.blockChecksum:
+                out += struct.pack("<I", ws["bsum"][b])
+        return bytes(out)
+
+    def body_bytes(self, n, sd, ws):
+        return len(self._records(self.src, ws, sd))
+
+    def assemble(self, src, n, sd, ws, body):
+        rec = self._records(src if src is None else self.src, ws, sd)
+        assert len(rec) == body.numel()
+        body.copy_(torch.frombuffer(bytearray(rec), dtype=torch.uint8) if rec else body)
+
+
+def _streamed_worker(rank, world, port, n, block_id, bck, kind, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import lz4mt_amd as L
+        data = _stream_input(n, kind)
+        bm = D.block_bytes(block_id)
+        off, ln, _, _ = D.shard_blocks(n, bm, world, rank)
+        sd = L.make_sd(block_id, stream_checksum=False, block_checksum=bck)
+        eng = MockShardEngine(rank, block_id, 2 + rank)
+        stats = {}
+        full = D.compress_gather_streamed(torch.frombuffer(bytearray(data[off:off + ln]) or bytearray(1),
+                                                           dtype=torch.uint8)[:ln], sd, engine=eng,
+                                          per_block_cap=max(bm // 8, 4096), stats=stats, min_round_s=0.0)
+        if rank == 0:
+            q.put((bytes(full.numpy().tobytes()), stats["rounds"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _stream_input(n, kind):
+    if kind == "mixed":   # compressible text with incompressible stretches: some blocks stored raw
+        a = bytearray(oracle.gen_synthetic(n, 42))
+        r = oracle.gen_random(n, 9)
+        for s in range(0, n, 3 * 65536 + 1000):
+            a[s:s + 70000] = r[s:s + 70000]
+        return bytes(a)
+    return oracle.gen_synthetic(n, 42)
+
+
+@pytest.mark.parametrize("world,n,block_id,bck,kind", [
+    (2, 9 * 65536 + 4321, 4, True, "appf"),
+    (3, 23 * 65536 + 77, 4, False, "mixed"),
+    (3, 2 * 262144, 5, True, "mixed"),          # 2 blocks, 3 ranks: one shard is empty
+    (2, 3 * (1 << 20) + 5, 6, True, "mixed"),
+])
+def test_streamed_gather_stitches_whole_stream_frame(world, n, block_id, bck, kind):
+    """compress_gather_streamed over gloo: ranks finish their encodes in
+    different rounds, blocks publish at different paces, payloads are capped
+    per block per round (several final rounds), incompressible blocks switch
+    to source bytes -- and the root's frame is byte for byte the oracle's
+    frame of the whole stream."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_streamed_worker, args=(r, world, port, n, block_id, bck, kind, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got, rounds = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = oracle.compress_frame(_stream_input(n, kind), oracle.params(block_id, False, bck))
+    assert rounds > world + 1
+    assert got == want

@@ -16,6 +16,7 @@ import subprocess
 import sys
 
 import pytest
+import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -49,3 +50,69 @@ def test_bench_gpus2_strong_scaling_one_buffer():
     assert line["n_gpus"] == 2 and line["scaling"] == "strong"
     assert line["config"]["bytes_total"] == 1 << 29
     assert line["stitched_frame_ok"] is True and line["roundtrip_ok"] is True
+
+
+def _streamed_rank(rank, world, port, n, bid, cap, kind, q):
+    """One rank of a streamed gather on the shared test GPU (gloo): its shard
+    of a mixed input (App. F text with incompressible stretches, so some
+    blocks are stored raw and their source bytes travel in the last round)."""
+    import torch.distributed as dist
+
+    import oracle
+    from lz4mt_amd import dist as D
+    import lz4mt_amd as L
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data = bytearray(oracle.gen_synthetic(n, 42))
+        rnd = oracle.gen_random(n, 5)
+        for s in range(0, n, 5 << 20):
+            data[s:s + 1_200_000] = rnd[s:s + 1_200_000]
+        bm = 1 << (8 + 2 * bid)
+        off, ln, _, _ = D.shard_blocks(n, bm, world, rank)
+        src = torch.frombuffer(bytearray(data[off:off + ln]), dtype=torch.uint8).cuda()
+        sd = L.make_sd(bid, stream_checksum=False, block_checksum=True)
+        st = {}
+        tr = D.IpcPushTransport(torch.device("cuda", 0)) if kind == "ipc" else D.RcclTransport()
+        full = None
+        for _ in range(2):   # twice: the IPC buffers are set up once and reused
+            full = D.compress_gather_streamed(src, sd, per_block_cap=cap, stats=st, min_round_s=0.0005,
+                                              transport=tr)
+        tr.close()
+        if rank == 0:
+            want = L.compress_frame(torch.frombuffer(data, dtype=torch.uint8).cuda(), sd)
+            q.put((full.numel() == want.numel() and bool(torch.equal(full, want)), st["rounds"], full.numel()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["ipc", "rccl"])
+@pytest.mark.parametrize("n,bid,cap", [((48 << 20) + 12345, 7, 128 << 10), ((40 << 20) + 7, 6, 16 << 10),
+                                       ((12 << 20) + 99, 5, 64 << 10)])
+def test_streamed_gather_on_device(n, bid, cap, kind):
+    """dist.compress_gather_streamed with the HIP engine, 2 ranks on one GPU:
+    k_encode_pub publishes while it encodes (1 and 4 MiB blocks), rounds of
+    k_shard_plan / k_shard_pack travel to rank 0 and k_shard_unpack places
+    them, the root assembles -- the stitched frame must be byte for byte the
+    single-process frame of the whole input (lz4mtHipCompressFrame).  "ipc":
+    packs pushed by device copies into the root's IPC-shared buffers (the
+    multi-GPU default); "rccl": point-to-point over the group (gloo here)."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_streamed_rank, args=(r, 2, port, n, bid, cap, kind, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    same, rounds, size = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert same, (rounds, size)
+    assert rounds >= 2
