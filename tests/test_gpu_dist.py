@@ -38,7 +38,20 @@ def test_bench_gpus2_launches_two_ranks_weak():
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
     assert line["stitched_frame_ok"] is True and line["roundtrip_ok"] is True
     assert line["config"]["bytes_total"] == 2 * line["config"]["bytes_per_gpu"]
-    # the stitched frame is ONE frame of the whole 2 x 0.25 GiB stream: header + records + EOS
+    # streamed gather (the default): the frame on rank 0 is ONE frame of the
+    # whole 2 x 0.25 GiB stream, gathered in rounds beside the encodes
+    assert line["gather"].startswith("streamed") and line["gather_rounds"] >= 1
+    assert line["stitched_frame_bytes"] == line["frame_bytes"]
+    assert 1.9 < line["ratio"] < 2.2
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_gather_after_encode():
+    line = _bench("--gpus", "2", "--gib", "0.25", "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
+                  "--gather", "after")
+    assert line["n_gpus"] == 2 and line["gather"].startswith("after")
+    assert line["stitched_frame_ok"] is True and line["roundtrip_ok"] is True
+    # frame_bytes: rank 0's own shard frame; the stitched frame holds both shards' records
     assert line["stitched_frame_bytes"] > line["frame_bytes"]
 
 

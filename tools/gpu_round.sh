@@ -3,6 +3,7 @@
 # each under its own time limit; the first failure ends the pass.
 # usage (from the repo root on the box): bash tools/gpu_round.sh <tag> <step>...
 #   tests   pytest -m gpu (every GPU test file)
+#   tdist   pytest -m gpu tests/test_gpu_dist.py (the multi-rank paths) only
 #   bench   the default 1-GPU bench line (driver shape: --steps 20 --warmup 5)
 #   trace   rocprofv3 kernel-trace stats of a 5-step bench run
 #   sq      SQ counters of the encoder / decoder (tools/kprof.py 2) + the window count (tools/kstats.py 2)
@@ -21,6 +22,10 @@ for step in "$@"; do
       timeout -k 10 1100 python3 -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread tests \
           > "$out/pytest.log" 2>&1 || { tail -30 "$out/pytest.log"; exit 1; }
       tail -2 "$out/pytest.log" ;;
+    tdist)
+      timeout -k 10 600 python3 -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread tests/test_gpu_dist.py \
+          > "$out/pytest_dist.log" 2>&1 || { tail -40 "$out/pytest_dist.log"; exit 1; }
+      tail -2 "$out/pytest_dist.log" ;;
     bench)
       timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > "$out/bench.json" 2> "$out/bench.err"
       cat "$out/bench.json" ;;
