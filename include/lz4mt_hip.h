@@ -202,6 +202,10 @@ uint64_t lz4mtHipShardBodyBytes(uint64_t n, const Lz4MtStreamDescriptor* sd, voi
  * matches, far matches, batch sequences, serial-path sequences, -...]. */
 int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* stats16, void* stream);
 int lz4mtHipDebugDecodeStats(const void* d_frame, uint64_t frameSize, uint64_t* stats16, void* stream);
+/* FETCH_SIZE calibration (tools/fetch_cal.py): reads n bytes of d_buf exactly
+ * once with `width`-byte loads per lane (1, 4, 8 or 16); d_out4: 4 bytes of
+ * device scratch.  Asynchronous; 0, or -1 on a bad width. */
+int lz4mtHipDebugFetchCal(const void* d_buf, uint64_t n, int width, void* d_out4, void* stream);
 
 #ifdef __cplusplus
 }

@@ -429,3 +429,52 @@ extern "C" int lz4mtHipCopyAsync(void* d_dst, const void* d_src, uint64_t n, voi
     return hipMemcpyAsync(d_dst, d_src, n, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)) == hipSuccess
                ? 0 : -1;
 }
+
+// ---------------------------------------------------------------------------
+// Diagnostics: FETCH_SIZE calibration (tools/fetch_cal.py).  Reads n bytes
+// exactly once, every lane `width` bytes per load (1, 4, 8 or 16: the
+// encoder's byte, gld4u, gld8u loads and a dwordx4 stream), 64 x width
+// contiguous bytes per wave instruction, consecutive loads of one lane
+// 64 x width apart (so they stay separate instructions).  The XOR of every
+// word is folded into out[0] only if it equals a value no input produces
+// here, which keeps the loads without a store per load.
+// ---------------------------------------------------------------------------
+namespace lz4mt { namespace shard {
+template <int W>
+__global__ void __launch_bounds__(256) k_fetch_cal(const uint8_t* __restrict__ p, uint64_t n,
+                                                   uint32_t* __restrict__ out) {
+    const uint64_t waves = (uint64_t)gridDim.x * 4;
+    const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t L = threadIdx.x & 63;
+    const uint64_t step = 64ull * W;
+    uint32_t acc = 0;
+    for (uint64_t c = wave * step; c + step <= n; c += waves * step) {
+        g_cu8* q = gp(p) + c + (uint64_t)L * W;
+        if constexpr (W == 1) acc ^= *q;
+        else if constexpr (W == 4) acc ^= *(g_cu32*)q;
+        else if constexpr (W == 8) {
+            const uint64_t v = *(const __attribute__((address_space(1))) uint64_t*)q;
+            acc ^= (uint32_t)v ^ (uint32_t)(v >> 32);
+        } else {
+            const v4u v = *(const __attribute__((address_space(1))) v4u*)q;
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+    }
+    if (acc == 0x9E3779B9u) out[0] = acc;
+}
+}}  // namespace lz4mt::shard
+
+extern "C" int lz4mtHipDebugFetchCal(const void* d_buf, uint64_t n, int width, void* d_out4, void* stream) {
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    const dim3 g(256 * 16), b(256);
+    const uint8_t* p = static_cast<const uint8_t*>(d_buf);
+    uint32_t* o = static_cast<uint32_t*>(d_out4);
+    switch (width) {
+        case 1: hipLaunchKernelGGL(k_fetch_cal<1>, g, b, 0, st, p, n, o); break;
+        case 4: hipLaunchKernelGGL(k_fetch_cal<4>, g, b, 0, st, p, n, o); break;
+        case 8: hipLaunchKernelGGL(k_fetch_cal<8>, g, b, 0, st, p, n, o); break;
+        case 16: hipLaunchKernelGGL(k_fetch_cal<16>, g, b, 0, st, p, n, o); break;
+        default: return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -9,6 +9,8 @@
 #   sq      SQ counters of the encoder / decoder (tools/kprof.py 2) + the window count (tools/kstats.py 2)
 #   pmc     FETCH_SIZE / WRITE_SIZE passes (tools/prof.sh without its trace)
 #   dist2   bench.py --gpus 2 over gloo on this one GPU (rehearsal of the N > 1 path)
+#   fcal    FETCH_SIZE calibration on a known byte count (tools/fetch_cal.py + fetchcal_sum.py)
+#   tail    the streamed gather's exposed tail on one GPU (tools/tail_model.py)
 #   ab      kernel times of every exp_libs/*.so (tools/mkvariants.sh), two passes
 set -euo pipefail
 tag=$1; shift
@@ -52,6 +54,13 @@ for step in "$@"; do
       LZ4MT_BENCH_BACKEND=gloo timeout -k 10 400 python3 bench.py --gpus 2 --gib 0.5 --steps 2 --warmup 1 \
           --no-cpu-baseline > "$out/dist2.json" 2> "$out/dist2.err"
       cat "$out/dist2.json" ;;
+    fcal)
+      timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -T -f csv -d "$out/fcal" -o fcal -- \
+          python3 tools/fetch_cal.py 8 > "$out/fcal.log" 2>&1
+      python3 tools/fetchcal_sum.py "$out/fcal" 8 | tee "$out/fcal_summary.json" ;;
+    tail)
+      timeout -k 10 300 python3 tools/tail_model.py 8 8 > "$out/tail_model.txt" 2>&1
+      cat "$out/tail_model.txt" ;;
     ab)
       bash tools/ab.sh > "$out/ab.txt" 2>&1 && bash tools/ab.sh >> "$out/ab.txt" 2>&1
       cat "$out/ab.txt" ;;
