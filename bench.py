@@ -218,7 +218,8 @@ def pmc_traffic(kernel, n, bm, flg):
         fetch = sb + max(0.0, fr - cal["stream_factor"] * sb) / cal["other_factor"]
     else:
         fetch = fr / cal.get("fetch_factor", 0.5)
-    return {"bytes": fetch + k["write_bytes"], "fetch_raw": fr, "fetch_calibrated": round(fetch),
+    return {"bytes": fetch + k["write_bytes"], "raw_bytes": fr + k["write_bytes"], "fetch_raw": fr,
+            "fetch_calibrated": round(fetch),
             "write": k["write_bytes"], "calibration": cal.get("how", "guide x2 (uncalibrated)"),
             "source": "profiles/pmc_current.json (" + prof.get("tag", "?") + ")"}, None
 

@@ -1668,7 +1668,11 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 // ---------------------------------------------------------------------------
 // Decoder
 // ---------------------------------------------------------------------------
-constexpr int32_t kRing = 16384;   // LDS history ring (bytes)
+#ifndef LZ4MT_DEC_RING
+#define LZ4MT_DEC_RING 16384
+#endif
+constexpr int32_t kRing = LZ4MT_DEC_RING;   // LDS history ring (bytes; A/B: -DLZ4MT_DEC_RING=8192 / 32768)
+static_assert((kRing & (kRing - 1)) == 0 && kRing >= 4096, "history ring: a power of two");
 constexpr int32_t kInWin = 2048;   // LDS input window (bytes)
 constexpr int32_t kFlush = 1024;   // ring -> HBM flush granule (64 lanes x 16 B)
 // next-sequence table of a batch: u16 per candidate token position (512),

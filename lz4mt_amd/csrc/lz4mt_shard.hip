@@ -436,13 +436,13 @@ extern "C" int lz4mtHipCopyAsync(void* d_dst, const void* d_src, uint64_t n, voi
 // encoder's byte, gld4u, gld8u loads and a dwordx4 stream), 64 x width
 // contiguous bytes per wave instruction, consecutive loads of one lane
 // 64 x width apart (so they stay separate instructions).  The XOR of every
-// word is folded into out[0] only if it equals a value no input produces
-// here, which keeps the loads without a store per load.
+// word is stored only if it equals `never` (a run-time argument the host
+// picks so that it cannot match): the loads stay, with no store per load.
 // ---------------------------------------------------------------------------
 namespace lz4mt { namespace shard {
 template <int W>
 __global__ void __launch_bounds__(256) k_fetch_cal(const uint8_t* __restrict__ p, uint64_t n,
-                                                   uint32_t* __restrict__ out) {
+                                                   uint32_t* __restrict__ out, uint32_t never) {
     const uint64_t waves = (uint64_t)gridDim.x * 4;
     const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const uint32_t L = threadIdx.x & 63;
@@ -460,7 +460,7 @@ __global__ void __launch_bounds__(256) k_fetch_cal(const uint8_t* __restrict__ p
             acc ^= v.x ^ v.y ^ v.z ^ v.w;
         }
     }
-    if (acc == 0x9E3779B9u) out[0] = acc;
+    if (acc == never) out[0] = acc;
 }
 }}  // namespace lz4mt::shard
 
@@ -470,10 +470,10 @@ extern "C" int lz4mtHipDebugFetchCal(const void* d_buf, uint64_t n, int width, v
     const uint8_t* p = static_cast<const uint8_t*>(d_buf);
     uint32_t* o = static_cast<uint32_t*>(d_out4);
     switch (width) {
-        case 1: hipLaunchKernelGGL(k_fetch_cal<1>, g, b, 0, st, p, n, o); break;
-        case 4: hipLaunchKernelGGL(k_fetch_cal<4>, g, b, 0, st, p, n, o); break;
-        case 8: hipLaunchKernelGGL(k_fetch_cal<8>, g, b, 0, st, p, n, o); break;
-        case 16: hipLaunchKernelGGL(k_fetch_cal<16>, g, b, 0, st, p, n, o); break;
+        case 1: hipLaunchKernelGGL(k_fetch_cal<1>, g, b, 0, st, p, n, o, 0xFFFFFFFFu); break;
+        case 4: hipLaunchKernelGGL(k_fetch_cal<4>, g, b, 0, st, p, n, o, 0xFFFFFFFFu); break;
+        case 8: hipLaunchKernelGGL(k_fetch_cal<8>, g, b, 0, st, p, n, o, 0xFFFFFFFFu); break;
+        case 16: hipLaunchKernelGGL(k_fetch_cal<16>, g, b, 0, st, p, n, o, 0xFFFFFFFFu); break;
         default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;

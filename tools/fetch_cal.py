@@ -25,7 +25,7 @@ flush = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
 out = torch.zeros(1, dtype=torch.int32, device="cuda")
 for width in (1, 4, 8, 16):
     for _ in range(2):
-        buf.fill_(width)       # rewrite: nothing of it stays in L2 / MALL from a read
+        buf.fill_(0x11 * width % 256)   # rewrite: nothing of it stays in L2 / MALL from a read
         flush.fill_(0)         # and push the tail of that write out of the caches
         torch.cuda.synchronize()
         assert L.lib.lz4mtHipDebugFetchCal(ctypes.c_void_p(buf.data_ptr()), n, width,

@@ -12,12 +12,12 @@ import sys
 N = int(float(sys.argv[2] if len(sys.argv) > 2 else 8) * (1 << 30))
 ACHIEVABLE = 6.3e12   # MI355X_MICROARCH.md: achievable HBM read rate
 f = glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)[0]
+ORDER = [1, 1, 4, 4, 8, 8, 16, 16]   # tools/fetch_cal.py's launches (the trace drops the template argument)
 rows = {}
-for r in csv.DictReader(open(f)):
-    m = re.search(r"k_fetch_cal<(\d+)>", r["Kernel_Name"])
-    if not m or r["Counter_Name"] != "FETCH_SIZE":
-        continue
-    w = int(m.group(1))
+cal = [r for r in csv.DictReader(open(f)) if r["Counter_Name"] == "FETCH_SIZE" and
+       re.match(r"(void )?(lz4mt::shard::)?k_fetch_cal", r["Kernel_Name"])]
+cal.sort(key=lambda r: int(r["Dispatch_Id"]))
+for w, r in zip(ORDER, cal):
     ns = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     rows.setdefault(w, []).append((float(r["Counter_Value"]) * 1024.0, ns))
 res = {}

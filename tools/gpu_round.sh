@@ -64,6 +64,9 @@ for step in "$@"; do
     ab)
       bash tools/ab.sh > "$out/ab.txt" 2>&1 && bash tools/ab.sh >> "$out/ab.txt" 2>&1
       cat "$out/ab.txt" ;;
+    ab5)   # the same at 256 KiB blocks (32768 blocks per 8 GiB: occupancy-sensitive)
+      BID=5 bash tools/ab.sh > "$out/ab5.txt" 2>&1 && BID=5 bash tools/ab.sh >> "$out/ab5.txt" 2>&1
+      cat "$out/ab5.txt" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -5,13 +5,11 @@ bytes (rocprofv3 reports KiB) on 8 GiB of App. F input, 4 MiB blocks,
 -Sx -BX (flg 0x70) -- the bench configuration, recorded in "config" so
 bench.py uses it only for that configuration.
 
-Calibration (MI355X_MICROARCH.md: gfx950 FETCH_SIZE counts ~1/2 of the bytes
-of wide streaming reads; other widths need a known byte count): the same
-kernels on 8 GiB of random bytes, where every block is stored raw, so
-k_encode streams its source once (n bytes) and k_decode copies n raw bytes;
-fetch_factor = FETCH_SIZE / n.  k_xxh32_frame_blocks (reads exactly the
-stored bytes) is the cross-check on the App. F run.
-usage: python tools/pmcsum.py gpurun_out/prof_<tag> <tag> [--current]"""
+Calibration: FETCH_SIZE / bytes of a kernel that reads a known byte count
+exactly once at the load widths these kernels use (tools/fetch_cal.py,
+summarised by tools/fetchcal_sum.py into the json given as the third
+argument); bench.py divides each kernel's FETCH_SIZE by that factor.
+usage: python tools/pmcsum.py <gpu_round dir> <tag> [fcal_summary.json] [--current]"""
 import csv
 import glob
 import json
@@ -46,20 +44,30 @@ if stats:
         if name in appf:
             appf[name]["trace_avg_ns"] = float(r["AverageNs"])
             appf[name]["trace_calls"] = int(r["Calls"])
-# k_encode: its source stream (n bytes, every launch) is counted at the
-# factor the random-input run measures; what App. F input fetches beyond that
-# (candidate-verify and match-count words: 256-B wave loads) at the guide's
-# 1/2.  k_decode: the raw-copy run gives the factor of its 16-B-per-lane reads.
+# Calibration: FETCH_SIZE / bytes of a kernel that reads
+# a known byte count exactly once (tools/fetch_cal.py: k_fetch_cal over 8 GiB
+# with 1-, 4-, 8- and 16-byte loads per lane, the widths k_encode / k_decode
+# use), accepted only at a physically possible rate (tools/fetchcal_sum.py).
+# The random-input runs stay as diagnostics: k_encode does NOT stream random
+# input once (its probe step grows after misses), so their ratio is a
+# coverage, not a counter factor.
 cal = {}
+fc_path = sys.argv[3] if len(sys.argv) > 3 and not sys.argv[3].startswith("--") else None
+fc = json.load(open(fc_path)) if fc_path else None
+if fc:
+    facs = {w: v["factor"] for w, v in fc["widths"].items() if v["factor"]}
+    f_lo, f_hi = min(facs.values()), max(facs.values())
+    how = ("FETCH_SIZE / bytes read by k_fetch_cal (8 GiB read exactly once; tools/fetch_cal.py) per load width: " +
+           ", ".join(f"{w.split('_')[1]} B {f}" for w, f in sorted(facs.items(), key=lambda x: int(x[0].split('_')[1]))) +
+           f"; implied rates <= {fc['achievable_Bps'] / 1e12:.1f} TB/s")
+    for k in ("k_encode", "k_decode"):
+        cal[k] = {"fetch_factor": (f_lo + f_hi) / 2, "fetch_factor_range": [f_lo, f_hi], "how": how,
+                  "source": fc_path}
 if "k_encode" in rnd:
-    cal["k_encode"] = {"stream_bytes": N, "stream_factor": rnd["k_encode"]["fetch_bytes"] / N, "other_factor": 0.5,
-                       "how": "source stream calibrated by k_encode over 8 GiB of random bytes (all blocks raw: the "
-                              "source streamed once, n bytes known); the remaining fetches at the guide's x2",
-                       "fetch_raw": rnd["k_encode"]["fetch_bytes"], "write_raw": rnd["k_encode"]["write_bytes"]}
-if "k_decode" in rnd:
-    cal["k_decode"] = {"fetch_factor": rnd["k_decode"]["fetch_bytes"] / N,
-                       "how": "k_decode over the raw-block frame of 8 GiB of random bytes (n bytes copied)",
-                       "fetch_raw": rnd["k_decode"]["fetch_bytes"], "write_raw": rnd["k_decode"]["write_bytes"]}
+    cal.setdefault("diagnostics", {})["k_encode_random_input_coverage"] = {
+        "fetch_raw": rnd["k_encode"]["fetch_bytes"], "bytes": N,
+        "note": "k_encode over 8 GiB of random bytes (every block raw): FETCH_SIZE / n, the probe coverage times "
+                "the counter factor -- not a calibration"}
 res = {"tag": tag, "config": {"bytes": N, "block_bytes": 4 << 20, "flg": 0x70,
                               "workload": "tools/kprof.py 8: 8 GiB App. F synthetic, 4 MiB blocks, -Sx -BX"},
        "kernels": appf, "calibration": cal, "random_input": rnd}
