@@ -336,7 +336,7 @@ def main():
         transport_name = a.transport
     L.lib.lz4mtHipSetTiming(1)
     tc = td = ts = tg = 0.0
-    enc_ms, dec_ms, frame_len, exposed_ms, rounds = [], [], 0, [], []
+    enc_ms, dec_ms, frame_len, exposed_ms, rounds, tails = [], [], 0, [], [], []
     full = piece = None
     for it in range(a.warmup + a.steps):
         timed = it >= a.warmup
@@ -363,6 +363,7 @@ def main():
             exposed_ms.append(eng.enc_done.elapsed_time(end_ev) if rank == 0 else 0.0)
             tgr = exposed_ms[-1] * 1e-3
             rounds.append(st_.get("rounds", 0))
+            tails.append((st_.get("tail_rounds_s") or 0.0, st_.get("rounds_after_encode", 0)))
             frame_len = full.numel() if rank == 0 else 0
             own_body = st_.get("own_body_bytes", 0)
         else:
@@ -482,7 +483,9 @@ def main():
         if streamed:   # root's GPU time from its own encode's end to the assembled frame
             line.update({"gather": f"streamed beside the encode (dist.compress_gather_streamed, {transport_name})",
                          "gather_exposed_ms": round(sum(exposed_ms[a.warmup:]) / max(1, K), 3),
-                         "gather_rounds": round(sum(rounds[a.warmup:]) / max(1, K), 1)})
+                         "gather_rounds": round(sum(rounds[a.warmup:]) / max(1, K), 1),
+                         "gather_tail_rounds": round(sum(t[1] for t in tails[a.warmup:]) / max(1, K), 1),
+                         "gather_tail_rounds_ms": round(sum(t[0] for t in tails[a.warmup:]) / max(1, K) * 1e3, 3)})
         elif world > 1:
             line.update({"gather": "after the encode (dist.gather_frame)"})
         if world > 1:

@@ -69,7 +69,7 @@ struct WalkScratch {
 // for work that can run beside the main stream.
 struct AuxStream {
     hipStream_t st = nullptr;
-    hipEvent_t evIn = nullptr, evOut = nullptr;
+    hipEvent_t evIn = nullptr, evMid = nullptr, evOut = nullptr;
     int dev = -1;
     bool ensure();
     void release();
@@ -88,6 +88,13 @@ hipError_t launch_decode(const uint8_t* frame, const BlockRec* recs, uint32_t nB
                          uint8_t* out, uint64_t outCap, int32_t* dsize, hipStream_t st);
 hipError_t launch_xxh32_stored(const uint8_t* src, const uint8_t* slots, uint64_t srcSize, uint32_t blockSize,
                                uint32_t nBlocks, const int32_t* csize, uint32_t* digest, hipStream_t st);
+// block checksums while k_encode_pub runs (on another stream; pub / xdone
+// zeroed before both), and the fix-up of blocks it did not finish
+hipError_t launch_xxh32_follow(const uint8_t* src, const uint8_t* slots, uint64_t srcSize, uint32_t blockSize,
+                               uint32_t nBlocks, uint32_t* pub, uint32_t* digest, uint32_t* xdone, hipStream_t st);
+hipError_t launch_xxh32_fixup(const uint8_t* src, const uint8_t* slots, uint64_t srcSize, uint32_t blockSize,
+                              uint32_t nBlocks, const int32_t* csize, uint32_t* digest, const uint32_t* xdone,
+                              hipStream_t st);
 hipError_t launch_xxh32_frame_blocks(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t* digest,
                                      hipStream_t st);
 hipError_t launch_xxh32_stream(const uint8_t* p, uint64_t len, uint32_t* digest, hipStream_t st);

@@ -64,6 +64,8 @@ struct CompressWs {
     uint64_t* recOff;
     uint32_t* ssum;
     uint64_t* fsize;
+    uint32_t* pub;     // k_encode_pub's per-block progress (the checksum follower reads it)
+    uint32_t* xdone;   // k_xxh32_follow's finished flags
     // block-dependent frames of the asynchronous calls (bd != 0): the host
     // plan copied in, the carried lz4 table, the parallel rounds' scratch
     // (bd == 1), or the HC stream's packed segments (bd == 2)
@@ -88,6 +90,8 @@ CompressWs carve_compress(uint8_t* base, uint64_t nb, uint64_t bm, int level = 0
     w.recOff = reinterpret_cast<uint64_t*>(take((nb + 1) * 8));
     w.ssum = reinterpret_cast<uint32_t*>(take(16));
     w.fsize = reinterpret_cast<uint64_t*>(take(16));
+    w.pub = reinterpret_cast<uint32_t*>(take(nb * 4 + 4));
+    w.xdone = reinterpret_cast<uint32_t*>(take(nb * 4 + 4));
     const uint64_t nbp = nb > 0 ? nb : 1;
     if (bd == 1) {
         w.bdPlan = take(nbp * sizeof(LinkPlan));
@@ -231,6 +235,15 @@ struct DevBuf {
     }
 };
 
+// LZ4MT_AMD_FOLLOW=0: block checksums after the encode (k_xxh32_stored), A/B
+bool follow_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("LZ4MT_AMD_FOLLOW");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // A few bytes of device memory per thread and device (frame-size / digest
 // results): no hipMalloc/hipFree per call (hipFree waits for the whole
 // device).  One buffer per device ordinal, made on first use, so a thread
@@ -349,6 +362,18 @@ Lz4MtResult device_compress_body(const uint8_t* src, uint64_t n, uint32_t bm, in
                                  const AuxStream* aux, const LinkState* link, int level) {
     const uint64_t nb = (n + bm - 1) / bm;
     CompressWs w = carve_compress(ws, nb, bm, level);
+    // Independent 1 / 4 MiB blocks with block checksums and a side stream:
+    // the encoder publishes its progress and k_xxh32_follow hashes the
+    // stored bytes beside it (no LDS, so it runs while the encoder holds all
+    // of it).  Never on one stream (a graph capture): the follower waits for
+    // the encode, which would then queue behind it.
+    const bool follow = !link && level < 3 && blockChecksum && aux && aux->st && aux->evMid && follow_enabled() &&
+                        bm >= (1u << 20) && bm <= (4u << 20);
+    if (follow) {
+        HIPCHK(hipMemsetAsync(w.pub, 0, nb * 4 + 4, st));
+        HIPCHK(hipMemsetAsync(w.xdone, 0, nb * 4 + 4, st));
+        HIPCHK(hipEventRecord(aux->evIn, st));
+    }
     g_timing.mark(0, st);
     if (link && level >= 3 && link->hcPerBlock) {   // -BD LZ4-HC, one segment per block: level 9, cap n - 1
         HIPCHK(launch_encode_hc(src, n, bm, (uint32_t)nb, w.slots, bm, 0xFFFFFFFEu, 9, w.delta, w.csize, st, w.hcSplit));
@@ -368,11 +393,23 @@ Lz4MtResult device_compress_body(const uint8_t* src, uint64_t n, uint32_t bm, in
     else if (level >= 3)   // LZ4-HC, a wave per block (lz4mt_hc.hip)
         HIPCHK(launch_encode_hc(src, n, bm, (uint32_t)nb, w.slots, bm, 0xFFFFFFFFu, level, w.delta, w.csize, st,
                                 w.hcSplit));
+    else if (follow) {   // block checksums hashed beside the encode (k_xxh32_follow), as the output appears
+        HIPCHK(launch_encode_pub(src, n, bm, (uint32_t)nb, w.slots, w.csize, w.pub, st));
+        // launched AFTER the encoder: were the two streams ever mapped onto
+        // one hardware queue, the follower would merely run after it
+        HIPCHK(hipStreamWaitEvent(aux->st, aux->evIn, 0));
+        HIPCHK(launch_xxh32_follow(src, w.slots, n, bm, (uint32_t)nb, w.pub, w.bsum, w.xdone, aux->st));
+    }
     else
         HIPCHK(launch_encode(src, n, bm, (uint32_t)nb, w.slots, bm, 0xFFFFFFFFu, w.csize, st));
     g_timing.mark(1, st);
     const bool side = blockChecksum && aux && aux->st;
-    if (side) {
+    if (follow) {   // the follower ends once every block is done; the fix-up waits for the encode
+        HIPCHK(hipEventRecord(aux->evMid, st));
+        HIPCHK(hipStreamWaitEvent(aux->st, aux->evMid, 0));
+        HIPCHK(launch_xxh32_fixup(src, w.slots, n, bm, (uint32_t)nb, w.csize, w.bsum, w.xdone, aux->st));
+        HIPCHK(hipEventRecord(aux->evOut, aux->st));
+    } else if (side) {
         HIPCHK(hipEventRecord(aux->evIn, st));
         HIPCHK(hipStreamWaitEvent(aux->st, aux->evIn, 0));
         HIPCHK(launch_xxh32_stored(src, w.slots, n, bm, (uint32_t)nb, w.csize, w.bsum, aux->st));
@@ -399,6 +436,7 @@ bool AuxStream::ensure() {
     release();
     if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) { st = nullptr; return false; }
     if (hipEventCreateWithFlags(&evIn, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&evMid, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&evOut, hipEventDisableTiming) != hipSuccess) {
         release();
         return false;
@@ -410,8 +448,9 @@ bool AuxStream::ensure() {
 void AuxStream::release() {
     if (st) { hipStreamSynchronize(st); hipStreamDestroy(st); }
     if (evIn) hipEventDestroy(evIn);
+    if (evMid) hipEventDestroy(evMid);
     if (evOut) hipEventDestroy(evOut);
-    st = nullptr; evIn = nullptr; evOut = nullptr; dev = -1;
+    st = nullptr; evIn = nullptr; evMid = nullptr; evOut = nullptr; dev = -1;
 }
 
 uint64_t compress_ws_bytes(uint64_t n, uint32_t bm, int level, int bd) {

@@ -806,6 +806,9 @@ __device__ __forceinline__ void store_pend(const PendSeq& p, const SrcRing& V, g
 // e.g. a new launch) the slot's bytes below it sees them final
 // (MI355X_MICROARCH.md, valid hand-off forms).
 constexpr uint32_t kPubShift = 16;   // publish every 64 KiB of output
+// pub[b] at the end of block b: the stored size | kPubDone, or kPubDone |
+// kPubRaw when the block is stored raw (its source bytes are the payload)
+constexpr uint32_t kPubDone = 0x80000000u, kPubRaw = 0x40000000u, kPubLen = 0x3FFFFFFFu;
 __device__ __forceinline__ void publish_progress(uint32_t* pub, uint32_t v) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -1152,10 +1155,10 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
     if (laneid() == 0) csize[b] = r;
 }
 
-// k_encode with progress publishing (block-sharded streamed gather): the
-// same parse and bytes; pub[b] = bytes of slot b already final.  Only the
-// v5 path (65 547 B .. 4 MiB blocks) publishes; other blocks are sent whole
-// once the launch is done.
+// k_encode with progress publishing (the block checksums' follower, the
+// block-sharded streamed gather): the same parse and bytes; pub[b] = bytes
+// of slot b already final, while the block encodes (the v5 path, 65 547 B ..
+// 4 MiB blocks, every 64 KiB of output), then kPubDone | size (or kPubRaw).
 __global__ void __launch_bounds__(64) k_encode_pub(const uint8_t* __restrict__ src, uint64_t srcSize,
                                                    uint32_t blockSize, uint8_t* __restrict__ slots,
                                                    uint64_t slotStride, int32_t* __restrict__ csize,
@@ -1178,6 +1181,7 @@ __global__ void __launch_bounds__(64) k_encode_pub(const uint8_t* __restrict__ s
     else
         r = encode_block<false, false, false>(s, n, d, n, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
     if (laneid() == 0) csize[b] = r;
+    publish_progress(pub + b, kPubDone | (r > 0 ? (uint32_t)r : kPubRaw));   // the block is final
 }
 
 hipError_t launch_encode_pub(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
@@ -3023,6 +3027,120 @@ __global__ void __launch_bounds__(64) k_xxh32_stream(const uint8_t* __restrict__
     if (laneid() == 0) *digest = h;
 }
 
+// Block checksums WHILE the encoder runs (k_encode_pub publishes pub[b]):
+// a quad of lanes per block (lane c keeps XXH32 accumulator v_c), 16 blocks
+// per wave, no LDS (every CU's LDS belongs to the encoder meanwhile).  A
+// wave polls pub[] and hashes what became final -- whole 128-B lines only
+// while a block is still encoding, so no line is ever cached half-written
+// -- behind an agent-scope acquire; once a block is done it hashes the rest
+// (or, for a block stored raw, its source bytes) and writes the digest and
+// xdone[b] = 1.  Every wave leaves once its blocks are done, or after ~2 s
+// without progress (k_xxh32_fixup then computes what is missing), so the
+// grid always drains.  Replaces the k_xxh32_stored pass after the encode
+// (~4.3 ms at 8 GiB) by the last blocks' tails.
+constexpr int kFollowBatch = 8;   // stripes per lane loaded ahead
+
+__global__ void __launch_bounds__(64) k_xxh32_follow(const uint8_t* __restrict__ src, const uint8_t* __restrict__ slots,
+                                                     uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                                                     uint32_t* pub, uint32_t* __restrict__ digest,
+                                                     uint32_t* __restrict__ xdone) {
+    const uint32_t L = laneid(), c = L & 3u;
+    const uint32_t b = blockIdx.x * 16u + (L >> 2);
+    const bool ok = b < nBlocks;
+    const uint64_t off = (uint64_t)(ok ? b : 0u) * blockSize;
+    const uint32_t n = ok ? (uint32_t)min<uint64_t>(blockSize, srcSize - off) : 0u;
+    const uint32_t vInit = (c == 0) ? kP1 + kP2 : (c == 1) ? kP2 : (c == 2) ? 0u : (uint32_t)(0u - kP1);
+    uint32_t v = vInit;
+    uint32_t hs = 0;              // stripes of the block hashed so far
+    bool raw = false, fin = !ok;  // raw: hashing the source bytes (block stored raw)
+    uint64_t tLast = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+    while (__builtin_amdgcn_ballot_w64(!fin)) {
+        uint32_t pv = 0;
+        if (!fin) pv = __hip_atomic_load(pub + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool done = !fin && (pv & kPubDone);
+        if (done && (pv & kPubRaw) && !raw) {   // restart on the source bytes
+            raw = true;
+            v = vInit;
+            hs = 0;
+        }
+        const uint32_t len = fin ? 0u : done ? (raw ? n : (pv & kPubLen)) : 0u;
+        const uint32_t target = fin ? hs : done ? (len >> 4) : ((pv & kPubLen) & ~127u) >> 4;
+        const uint32_t todo = target > hs ? target - hs : 0u;
+        uint32_t most = todo;
+        for (uint32_t d = 4; d < 64; d <<= 1) most = max(most, (uint32_t)__shfl_xor((int)most, (int)d, 64));
+        most = (uint32_t)__builtin_amdgcn_readfirstlane((int)max(most, (uint32_t)__shfl_xor((int)most, 1, 64)));
+        if (most == 0 && !__builtin_amdgcn_ballot_w64(done)) {   // nothing new: wait a little
+            if (__builtin_amdgcn_s_memrealtime() - tLast > 200000000ull) break;   // ~2 s: leave it to the fixup
+            __builtin_amdgcn_s_sleep(127);
+            continue;
+        }
+        tLast = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the bytes behind the counts just read
+        g_cu32* q = (g_cu32*)((raw ? gptr(src) : gptr(slots)) + off);
+        const uint32_t lastW = target ? 4u * target - 1u : 0u;   // loads never pass the final lines
+        for (uint32_t i = 0; i < most; i += kFollowBatch) {
+            uint32_t w[kFollowBatch];
+#pragma unroll
+            for (int u = 0; u < kFollowBatch; ++u) w[u] = q[min(4u * (hs + i + u) + c, lastW)];
+#pragma unroll
+            for (int u = 0; u < kFollowBatch; ++u) v = (i + u < todo) ? xround(v, w[u]) : v;
+        }
+        hs += todo;
+        // finish the blocks that are done: lane 0 of the quad folds the
+        // accumulators, the length and the tail (len & 15 bytes)
+        const uint32_t v1 = quad_get(v, 0), v2 = quad_get(v, 1), v3 = quad_get(v, 2), v4 = quad_get(v, 3);
+        if (done) {
+            if (c == 0) {
+                g_cu8* p = (raw ? gptr(src) : gptr(slots)) + off;
+                uint32_t h = len >= 16 ? rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18) : kP5;
+                h += len;
+                uint32_t o = len & ~15u;
+                for (; o + 4 <= len; o += 4) h = rotl32(h + ld32u(p + o) * kP3, 17) * kP4;
+                for (; o < len; ++o) h = rotl32(h + p[o] * kP5, 11) * kP1;
+                h ^= h >> 15; h *= kP2; h ^= h >> 13; h *= kP3; h ^= h >> 16;
+                digest[b] = h;
+                xdone[b] = 1u;
+            }
+            fin = true;
+        }
+    }
+}
+
+// the blocks k_xxh32_follow did not finish (normally none): their digests
+// from the stored bytes, after the encode
+__global__ void __launch_bounds__(64) k_xxh32_fixup(const uint8_t* __restrict__ src, const uint8_t* __restrict__ slots,
+                                                    uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
+                                                    const int32_t* __restrict__ csize, uint32_t* __restrict__ digest,
+                                                    const uint32_t* __restrict__ xdone) {
+    const uint32_t b = blockIdx.x * 16u + (laneid() >> 2);
+    const bool ok = b < nBlocks;
+    const bool need = ok && xdone[b] == 0u;
+    if (!__builtin_amdgcn_ballot_w64(need)) return;
+    const uint64_t off = (uint64_t)(ok ? b : 0u) * blockSize;
+    const uint32_t n = ok ? (uint32_t)min<uint64_t>(blockSize, srcSize - off) : 0u;
+    const int32_t cs = ok ? csize[b] : 0;
+    g_cu8* p = cs > 0 ? gptr(slots) + off : gptr(src) + off;
+    const uint32_t h = xxh32_quad(p, need ? (cs > 0 ? (uint32_t)cs : n) : 0u, gptr(src));
+    if (need && (laneid() & 3u) == 0) digest[b] = h;
+}
+
+hipError_t launch_xxh32_follow(const uint8_t* src, const uint8_t* slots, uint64_t srcSize, uint32_t blockSize,
+                               uint32_t nBlocks, uint32_t* pub, uint32_t* digest, uint32_t* xdone, hipStream_t st) {
+    if (nBlocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_xxh32_follow, dim3((nBlocks + 15) / 16), dim3(64), 0, st, src, slots, srcSize, blockSize,
+                       nBlocks, pub, digest, xdone);
+    return hipGetLastError();
+}
+
+hipError_t launch_xxh32_fixup(const uint8_t* src, const uint8_t* slots, uint64_t srcSize, uint32_t blockSize,
+                              uint32_t nBlocks, const int32_t* csize, uint32_t* digest, const uint32_t* xdone,
+                              hipStream_t st) {
+    if (nBlocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_xxh32_fixup, dim3((nBlocks + 15) / 16), dim3(64), 0, st, src, slots, srcSize, blockSize,
+                       nBlocks, csize, digest, xdone);
+    return hipGetLastError();
+}
+
 hipError_t launch_xxh32_stored(const uint8_t* src, const uint8_t* slots, uint64_t srcSize, uint32_t blockSize,
                                uint32_t nBlocks, const int32_t* csize, uint32_t* digest, hipStream_t st) {
     if (nBlocks == 0) return hipSuccess;
@@ -3075,6 +3193,12 @@ __global__ void __launch_bounds__(1024) k_frame_scan(const int32_t* __restrict__
     if (t == 1023) recOff[nBlocks] = part[1023];
 }
 
+// LZ4MT_ASM_DWORD=1: the dword-gather middle loop for every block (A/B)
+#ifndef LZ4MT_ASM_DWORD
+#define LZ4MT_ASM_DWORD 0
+#endif
+constexpr bool kAssembleDwordLoads = LZ4MT_ASM_DWORD;
+
 __global__ void __launch_bounds__(256) k_frame_assemble(const uint8_t* __restrict__ src, const uint8_t* __restrict__ slots,
                                                         uint64_t srcSize, uint32_t blockSize,
                                                         const int32_t* __restrict__ csize,
@@ -3105,6 +3229,39 @@ __global__ void __launch_bounds__(256) k_frame_assemble(const uint8_t* __restric
     for (uint64_t i = tailStart + t; i < L; i += 256) D[i] = sp[i];
     // middle: 16-B aligned destination chunks gathered from the source
     const uint64_t nchunks = (E0 - A0) >> 4;
+    if (cs > 0 && !kAssembleDwordLoads) {
+        // compressed block (its slot has 64 B of slack past any payload):
+        // two aligned 16-B loads per destination chunk, the source offset
+        // r = (sp + head) mod 16 is one value for the whole block, so the
+        // byte selection is a uniform switch on r / 4 + alignbyte by r % 4
+        const uintptr_t S0 = reinterpret_cast<uintptr_t>(sp) + head;
+        const uint32_t r = (uint32_t)(S0 & 15), q = r >> 2, s3 = r & 3;
+        g_cu4* base = (g_cu4*)(S0 - r);
+        g_u4* Dm = (g_u4*)(D + head);
+        auto pick = [&](v4u a, v4u b) -> v4u {
+            uint32_t d0, d1, d2, d3, d4;
+            switch (q) {   // wave-uniform
+                case 0: d0 = a.x; d1 = a.y; d2 = a.z; d3 = a.w; d4 = b.x; break;
+                case 1: d0 = a.y; d1 = a.z; d2 = a.w; d3 = b.x; d4 = b.y; break;
+                case 2: d0 = a.z; d1 = a.w; d2 = b.x; d3 = b.y; d4 = b.z; break;
+                default: d0 = a.w; d1 = b.x; d2 = b.y; d3 = b.z; d4 = b.w; break;
+            }
+            v4u o;
+            o.x = __builtin_amdgcn_alignbyte(d1, d0, s3);
+            o.y = __builtin_amdgcn_alignbyte(d2, d1, s3);
+            o.z = __builtin_amdgcn_alignbyte(d3, d2, s3);
+            o.w = __builtin_amdgcn_alignbyte(d4, d3, s3);
+            return o;
+        };
+        uint64_t j = t;
+        for (; j + 256 < nchunks; j += 512) {   // two chunks per thread in flight
+            const v4u a0 = base[j], b0 = base[j + 1], a1 = base[j + 256], b1 = base[j + 257];
+            Dm[j] = pick(a0, b0);
+            Dm[j + 256] = pick(a1, b1);
+        }
+        for (; j < nchunks; j += 256) Dm[j] = pick(base[j], base[j + 1]);
+        return;
+    }
     for (uint64_t j = t; j < nchunks; j += 256) {
         const uint64_t so = head + 16 * j;                 // source byte offset of this chunk
         g_cu32* q = (g_cu32*)(sp + (so & ~3ull));

@@ -82,6 +82,7 @@ struct ShardWs {
     uint64_t* recOff;  // nb + 1: record offsets (assembly)
     uint32_t* pub;     // nb: published bytes (k_encode_pub)
     uint32_t* sent;    // nb: bytes already packed (| kRawBit: source bytes)
+    uint32_t* xdone;   // nb: block checksum finished by k_xxh32_follow
     uint64_t bytes;
 };
 inline ShardWs carve(uint8_t* base, uint64_t nb, uint64_t bm) {
@@ -94,6 +95,7 @@ inline ShardWs carve(uint8_t* base, uint64_t nb, uint64_t bm) {
     w.recOff = reinterpret_cast<uint64_t*>(take((nb + 1) * 8));
     w.pub = reinterpret_cast<uint32_t*>(take(nb * 4 + 4));
     w.sent = reinterpret_cast<uint32_t*>(take(nb * 4 + 4));
+    w.xdone = reinterpret_cast<uint32_t*>(take(nb * 4 + 4));
     w.bytes = o;
     return w;
 }
@@ -181,7 +183,10 @@ __global__ void __launch_bounds__(64) k_shard_plan(uint32_t* pub, uint32_t* __re
             pcs[b] = cs;
             pbs[b] = bck ? bsum[b] : 0u;
         } else {
-            hi = __hip_atomic_load(pub + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // while encoding: bytes final so far; once done: the stored size
+            // (or kPubRaw: the final round sends the source bytes instead)
+            const uint32_t pv = __hip_atomic_load(pub + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            hi = (pv & 0x40000000u) ? 0u : (pv & 0x3FFFFFFFu);
         }
         lo = s & ~kRawBit;
         const uint32_t avail = hi > lo ? hi - lo : 0u;
@@ -307,11 +312,26 @@ extern "C" Lz4MtResult lz4mtHipShardEncode(const void* d_src, uint64_t n, const 
     const uint8_t* src = static_cast<const uint8_t*>(d_src);
     SHCHK(hipMemsetAsync(w.pub, 0, nb * 4 + 4, st));
     SHCHK(hipMemsetAsync(w.sent, 0, nb * 4 + 4, st));
+    SHCHK(hipMemsetAsync(w.xdone, 0, nb * 4 + 4, st));
     if (nb == 0) return LZ4MT_RESULT_OK;
+    // block checksums hashed beside the encode (k_xxh32_follow on a side
+    // stream; `stream` waits for it, so the shard is complete on `stream`)
+    thread_local AuxStream aux;
+    const bool follow = use_pub(bm) && sd->flg.blockChecksum && aux.ensure();
+    if (follow) SHCHK(hipEventRecord(aux.evIn, st));
     SHCHK(use_pub(bm) ? launch_encode_pub(src, n, bm, (uint32_t)nb, w.slots, w.csize, w.pub, st)
                       : launch_encode(src, n, bm, (uint32_t)nb, w.slots, bm, 0xFFFFFFFFu, w.csize, st));
-    if (sd->flg.blockChecksum)
+    if (follow) {   // launched after the encoder (one shared hardware queue would only serialise them)
+        SHCHK(hipStreamWaitEvent(aux.st, aux.evIn, 0));
+        SHCHK(launch_xxh32_follow(src, w.slots, n, bm, (uint32_t)nb, w.pub, w.bsum, w.xdone, aux.st));
+        SHCHK(hipEventRecord(aux.evMid, st));
+        SHCHK(hipStreamWaitEvent(aux.st, aux.evMid, 0));
+        SHCHK(launch_xxh32_fixup(src, w.slots, n, bm, (uint32_t)nb, w.csize, w.bsum, w.xdone, aux.st));
+        SHCHK(hipEventRecord(aux.evOut, aux.st));
+        SHCHK(hipStreamWaitEvent(st, aux.evOut, 0));
+    } else if (sd->flg.blockChecksum) {
         SHCHK(launch_xxh32_stored(src, w.slots, n, bm, (uint32_t)nb, w.csize, w.bsum, st));
+    }
     return LZ4MT_RESULT_OK;
 }
 

@@ -590,11 +590,16 @@ def compress_gather_streamed(src, sd, dst=0, group=None, engine=None, per_block_
     body = {}
     rounds, sent_log = 0, []
     t_last = 0.0
+    t_start = time.perf_counter()
+    t_final = None          # when this rank first found its encode finished
+    rounds_after = 0        # rounds from then on (the tail)
     while True:
         nbytes, body_now, now_complete = 0, 0, complete
         buf = None
         if not complete:
             final = E.encode_finished()
+            if final and t_final is None:
+                t_final = time.perf_counter()
             if not final:
                 wait = t_last + min_round_s - time.perf_counter()
                 if wait > 0:
@@ -621,11 +626,16 @@ def compress_gather_streamed(src, sd, dst=0, group=None, engine=None, per_block_
                 body[r] = rows[r][2]
         complete = now_complete
         rounds += 1
+        if t_final is not None:
+            rounds_after += 1
         sent_log.append(sum(row[0] for row in rows))
         if all(row[1] for row in rows):
             break
+    t_rounds = time.perf_counter()
     if stats is not None:
-        stats.update(rounds=rounds, bytes_per_round=sent_log)
+        stats.update(rounds=rounds, bytes_per_round=sent_log, rounds_after_encode=rounds_after,
+                     loop_s=t_rounds - t_start,
+                     tail_rounds_s=(t_rounds - t_final) if t_final is not None else None)
     if rank != dst:
         return None
     body[rank] = E.body_bytes(n, sd, ws)
@@ -644,4 +654,6 @@ def compress_gather_streamed(src, sd, dst=0, group=None, engine=None, per_block_
             E.assemble(None, sizes[r], sd, mirrors[r], piece)
         pos += body[r]
     out[pos:pos + 4] = 0
+    if stats is not None:   # host time of the root's own-size readback + assembly launches (not synchronised)
+        stats["assemble_launch_s"] = time.perf_counter() - t_rounds
     return out

@@ -61,9 +61,23 @@ for step in "$@"; do
     tail)
       timeout -k 10 300 python3 tools/tail_model.py 8 8 > "$out/tail_model.txt" 2>&1
       cat "$out/tail_model.txt" ;;
+    tailab)   # tools/tail_model.py for every exp_libs/*.so
+      for f in exp_libs/*.so; do
+        echo "== $f" >> "$out/tail_ab.txt"
+        LZ4MT_AMD_LIB=$f timeout -k 10 300 python3 tools/tail_model.py 8 8 2>&1 | grep -v amdgpu >> "$out/tail_ab.txt"
+      done
+      cat "$out/tail_ab.txt" ;;
     ab)
       bash tools/ab.sh > "$out/ab.txt" 2>&1 && bash tools/ab.sh >> "$out/ab.txt" 2>&1
       cat "$out/ab.txt" ;;
+    follow)   # block checksums beside the encode (default) vs after it (LZ4MT_AMD_FOLLOW=0), twice each
+      for k in 1 2; do
+        for f in 1 0; do
+          LZ4MT_AMD_FOLLOW=$f timeout -k 10 120 python3 -u tools/ktime.py 2>&1 | grep -v amdgpu | sed "s/^/FOLLOW=$f /" \
+              >> "$out/follow.txt"
+        done
+      done
+      cat "$out/follow.txt" ;;
     ab5)   # the same at 256 KiB blocks (32768 blocks per 8 GiB: occupancy-sensitive)
       BID=5 bash tools/ab.sh > "$out/ab5.txt" 2>&1 && BID=5 bash tools/ab.sh >> "$out/ab5.txt" 2>&1
       cat "$out/ab5.txt" ;;
