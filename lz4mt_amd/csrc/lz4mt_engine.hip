@@ -25,6 +25,20 @@
 
 using namespace lz4mt;
 
+// LZ4MT_AMD_FOLLOW=1: block checksums hashed beside the encode
+// (k_xxh32_follow).  Off by default: measured, the encoder runs ~6 ms longer
+// beside it at 8 GiB (185.9 vs 179.0 ms; the compress call 188.4 vs 184.3),
+// more than the 4.3 ms of k_xxh32_stored it hides
+// (profiles/r03e_follow_ab.txt).
+bool follow_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("LZ4MT_AMD_FOLLOW");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
+
 namespace {
 
 #define HIPCHK(x)                                   \
@@ -234,15 +248,6 @@ struct DevBuf {
         return true;
     }
 };
-
-// LZ4MT_AMD_FOLLOW=0: block checksums after the encode (k_xxh32_stored), A/B
-bool follow_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("LZ4MT_AMD_FOLLOW");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
 
 // A few bytes of device memory per thread and device (frame-size / digest
 // results): no hipMalloc/hipFree per call (hipFree waits for the whole

@@ -3193,11 +3193,10 @@ __global__ void __launch_bounds__(1024) k_frame_scan(const int32_t* __restrict__
     if (t == 1023) recOff[nBlocks] = part[1023];
 }
 
-// LZ4MT_ASM_DWORD=1: the dword-gather middle loop for every block (A/B)
-#ifndef LZ4MT_ASM_DWORD
-#define LZ4MT_ASM_DWORD 0
+// LZ4MT_ASM_NT=1: non-temporal stores for the frame bytes (A/B)
+#ifndef LZ4MT_ASM_NT
+#define LZ4MT_ASM_NT 0
 #endif
-constexpr bool kAssembleDwordLoads = LZ4MT_ASM_DWORD;
 
 __global__ void __launch_bounds__(256) k_frame_assemble(const uint8_t* __restrict__ src, const uint8_t* __restrict__ slots,
                                                         uint64_t srcSize, uint32_t blockSize,
@@ -3229,39 +3228,6 @@ __global__ void __launch_bounds__(256) k_frame_assemble(const uint8_t* __restric
     for (uint64_t i = tailStart + t; i < L; i += 256) D[i] = sp[i];
     // middle: 16-B aligned destination chunks gathered from the source
     const uint64_t nchunks = (E0 - A0) >> 4;
-    if (cs > 0 && !kAssembleDwordLoads) {
-        // compressed block (its slot has 64 B of slack past any payload):
-        // two aligned 16-B loads per destination chunk, the source offset
-        // r = (sp + head) mod 16 is one value for the whole block, so the
-        // byte selection is a uniform switch on r / 4 + alignbyte by r % 4
-        const uintptr_t S0 = reinterpret_cast<uintptr_t>(sp) + head;
-        const uint32_t r = (uint32_t)(S0 & 15), q = r >> 2, s3 = r & 3;
-        g_cu4* base = (g_cu4*)(S0 - r);
-        g_u4* Dm = (g_u4*)(D + head);
-        auto pick = [&](v4u a, v4u b) -> v4u {
-            uint32_t d0, d1, d2, d3, d4;
-            switch (q) {   // wave-uniform
-                case 0: d0 = a.x; d1 = a.y; d2 = a.z; d3 = a.w; d4 = b.x; break;
-                case 1: d0 = a.y; d1 = a.z; d2 = a.w; d3 = b.x; d4 = b.y; break;
-                case 2: d0 = a.z; d1 = a.w; d2 = b.x; d3 = b.y; d4 = b.z; break;
-                default: d0 = a.w; d1 = b.x; d2 = b.y; d3 = b.z; d4 = b.w; break;
-            }
-            v4u o;
-            o.x = __builtin_amdgcn_alignbyte(d1, d0, s3);
-            o.y = __builtin_amdgcn_alignbyte(d2, d1, s3);
-            o.z = __builtin_amdgcn_alignbyte(d3, d2, s3);
-            o.w = __builtin_amdgcn_alignbyte(d4, d3, s3);
-            return o;
-        };
-        uint64_t j = t;
-        for (; j + 256 < nchunks; j += 512) {   // two chunks per thread in flight
-            const v4u a0 = base[j], b0 = base[j + 1], a1 = base[j + 256], b1 = base[j + 257];
-            Dm[j] = pick(a0, b0);
-            Dm[j + 256] = pick(a1, b1);
-        }
-        for (; j < nchunks; j += 256) Dm[j] = pick(base[j], base[j + 1]);
-        return;
-    }
     for (uint64_t j = t; j < nchunks; j += 256) {
         const uint64_t so = head + 16 * j;                 // source byte offset of this chunk
         g_cu32* q = (g_cu32*)(sp + (so & ~3ull));
@@ -3273,7 +3239,11 @@ __global__ void __launch_bounds__(256) k_frame_assemble(const uint8_t* __restric
         v.y = __builtin_amdgcn_alignbyte(a2, a1, s3);
         v.z = __builtin_amdgcn_alignbyte(a3, a2, s3);
         v.w = __builtin_amdgcn_alignbyte(a4, a3, s3);
+#if LZ4MT_ASM_NT
+        __builtin_nontemporal_store(v, (g_u4*)(D + (A0 - Da) + 16 * j));
+#else
         *(g_u4*)(D + (A0 - Da) + 16 * j) = v;
+#endif
     }
 }
 

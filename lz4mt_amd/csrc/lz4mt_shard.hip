@@ -273,6 +273,10 @@ Lz4MtResult shard_sd(const Lz4MtStreamDescriptor* sd, uint32_t* bm) {
     return LZ4MT_RESULT_OK;
 }
 
+}  // namespace
+bool follow_enabled();   // lz4mt_engine.hip: LZ4MT_AMD_FOLLOW=1
+namespace {
+
 bool use_pub(uint32_t bm) {   // k_encode_pub's v5 path: 1 and 4 MiB blocks (64 / 256 KiB keep their own kernels)
     return bm >= (1u << 20) && bm <= (4u << 20);
 }
@@ -317,7 +321,7 @@ extern "C" Lz4MtResult lz4mtHipShardEncode(const void* d_src, uint64_t n, const 
     // block checksums hashed beside the encode (k_xxh32_follow on a side
     // stream; `stream` waits for it, so the shard is complete on `stream`)
     thread_local AuxStream aux;
-    const bool follow = use_pub(bm) && sd->flg.blockChecksum && aux.ensure();
+    const bool follow = use_pub(bm) && sd->flg.blockChecksum && follow_enabled() && aux.ensure();
     if (follow) SHCHK(hipEventRecord(aux.evIn, st));
     SHCHK(use_pub(bm) ? launch_encode_pub(src, n, bm, (uint32_t)nb, w.slots, w.csize, w.pub, st)
                       : launch_encode(src, n, bm, (uint32_t)nb, w.slots, bm, 0xFFFFFFFFu, w.csize, st));
