@@ -617,6 +617,14 @@ constexpr uint32_t kSR = 2048;        // source ring bytes
 #define LZ4MT_COUNT_LANES 32
 #endif
 constexpr uint32_t kCountLanes = LZ4MT_COUNT_LANES;
+// catch-up bytes the round trip loads per side (the bytes just before ip
+// and before the candidate); longer catch-ups take 64-byte rounds
+#ifndef LZ4MT_CATCH_LANES
+#define LZ4MT_CATCH_LANES 64
+#endif
+constexpr uint32_t kCatchLanes = LZ4MT_CATCH_LANES;
+static_assert(kCatchLanes >= 1 && kCatchLanes <= 64, "catch-up lanes");
+constexpr uint64_t kCatchMask = kCatchLanes >= 64 ? ~0ull : (1ull << kCatchLanes) - 1ull;
 static_assert(kCountLanes >= 1 && kCountLanes <= 63, "count lanes");
 constexpr uint32_t kSRMirror = 64;    // ring[kSR .. kSR+64) mirrors ring[0 .. 64)
 
@@ -989,7 +997,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                     const uint32_t ci = cOn ? cd + 4 * L : cd, ii = cOn ? ip + 4 * L : ip;
                     cw = gld4u(s + (ci < last4 ? ci : last4));
                     iw = gld4u(s + (ii < last4 ? ii : last4));
-                    const bool bOn = L < maxb;
+                    const bool bOn = L < maxb && L < kCatchLanes;
                     bi = s[bOn ? ip - L - 1 : o0];   // (o0: a byte of the block itself)
                     bc = s[bOn ? cd - L - 1 : o0];
                     if (havePe) {
@@ -1034,8 +1042,14 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             // bi/bc are consumed on every path, so no load of this window is
             // left pending into the next window's round trip.
             asm volatile("" ::"v"(bi), "v"(bc));
-            uint64_t fm = ~(bal(L < maxb) & bal(bi == bc));
+            uint64_t fm = ~(bal(L < maxb) & bal(bi == bc)) & kCatchMask;
             uint32_t back = 0;
+            if (kCatchLanes < 64 && fm == 0) {   // every loaded byte matched, the limit lies beyond them
+                back = kCatchLanes;
+                const uint32_t kb = back + L + 1;
+                const bool on = kb <= maxb;
+                fm = ~bal(on && s[on ? ip - kb : o0] == s[on ? cd - kb : o0]);
+            }
             while (fm == 0 && back + 64 < maxb) {   // catch-up longer than 64 bytes
                 back += 64;
                 const uint32_t kb = back + L + 1;
