@@ -285,9 +285,12 @@ def main():
     flg = (0x64 if sck else 0x70) & ~(0x20 if a.block_dependent else 0)
     if (a.level >= 3 or a.block_dependent) and world > 1:
         raise SystemExit("--level / --block-dependent are single-GPU measurements")
+    streamed = world > 1 and a.gather == "streamed" and not a.decompress_only
     cap = L.frame_bound(n, sd)
-    frame_buf = torch.empty(cap, dtype=torch.uint8, device=dev)
-    ws = L.compress_workspace(n, sd, device=dev, level=a.level)
+    # the streamed gather builds the frame on rank 0 from the shard workspace:
+    # no per-rank frame buffer or frame workspace (8 + 8 GiB per GPU spared)
+    frame_buf = None if streamed else torch.empty(cap, dtype=torch.uint8, device=dev)
+    ws = None if streamed else L.compress_workspace(n, sd, device=dev, level=a.level)
     out = torch.empty(n + (1 << 20), dtype=torch.uint8, device=dev)
     fsz = torch.zeros(2, dtype=torch.int64, device=dev)
 
@@ -325,12 +328,10 @@ def main():
     if a.decompress_only:   # compress once, untimed
         compress()
         torch.cuda.synchronize()
-    streamed = world > 1 and a.gather == "streamed" and not a.decompress_only
     own_body = 0
     if streamed:   # the shard engine's streams and workspace, the control group and transport, made once
         eng = D.HipShardEngine(dev)
         shard_ws = L.shard_workspace(n, sd, device=dev)
-        del ws
         ctrl = dist.new_group(backend="gloo") if backend == "nccl" else None
         transport = D.IpcPushTransport(dev) if a.transport == "ipc" else D.RcclTransport()
         transport_name = a.transport

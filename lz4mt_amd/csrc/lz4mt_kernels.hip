@@ -1698,8 +1698,17 @@ constexpr int32_t kFlush = 1024;   // ring -> HBM flush granule (64 lanes x 16 B
 // into the table, so a hop is one dependent ds_read_u16
 constexpr int32_t kNxOff = kInWin + 128;      // inside the win[] allocation
 constexpr uint32_t kNxPast = 1024, kNxDead = 1026;
-constexpr int32_t kFpOff = kInWin + 128 + 1040;   // far-match table of a batch (8 x 16 B)
-[[maybe_unused]] constexpr int32_t kWinAlloc = kFpOff + 128;
+// far matches of a batch whose bytes load together (LZ4MT_FAR_TAB, A/B):
+// App. F batches hold ~31 sequences, ~8 of them far (offset > the ring);
+// the rest are loaded one at a time
+#ifndef LZ4MT_FAR_TAB
+#define LZ4MT_FAR_TAB 8
+#endif
+constexpr int kFarTab = LZ4MT_FAR_TAB;
+static_assert(kFarTab >= 1 && kFarTab <= 24, "far table");
+constexpr int32_t kFpOff = kInWin + 128 + 1040;   // far-match table of a batch (kFarTab x 16 B)
+[[maybe_unused]] constexpr int32_t kWinAlloc = kFpOff + 16 * kFarTab;
+static_assert(kRing + kWinAlloc <= 20480 || kRing != 16384, "decoder LDS: 8 waves per CU need <= 20 KiB each");
 
 template <bool ST>
 struct Dec {
@@ -1981,9 +1990,9 @@ struct Dec {
         // 5a. far loads (up to 8 sequences, lane per byte), in flight during 5b.
         // The far lanes publish (source, ring target, length) in rank order to
         // a small LDS table that the wave reads back by broadcast.
-        uint32_t fv[8], fv2[8];
+        uint32_t fv[kFarTab], fv2[kFarTab];
         const uint32_t fr = __builtin_amdgcn_mbcnt_hi((uint32_t)(farM >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)farM, 0u));
-        const uint32_t nf8 = min((uint32_t)__popcll(farM), 8u);
+        const uint32_t nf8 = min((uint32_t)__popcll(farM), (uint32_t)kFarTab);
         l_u4* const fprm = (l_u4*)(win + kFpOff);
         if (farM) {
             if (completed < (int64_t)ringLo) {   // their bytes were stored to dst: make sure the stores landed
@@ -1991,10 +2000,10 @@ struct Dec {
                 completed = flushed;
             }
             if (ST) acc[7] += __popcll(farM);
-            if (far && fr < 8) fprm[fr] = (v4u){(uint32_t)src, (uint32_t)om & (kRing - 1), mlen, 0u};
+            if (far && fr < (uint32_t)kFarTab) fprm[fr] = (v4u){(uint32_t)src, (uint32_t)om & (kRing - 1), mlen, 0u};
             WAVE_SYNC();
 #pragma unroll
-            for (int g = 0; g < 8; ++g) {
+            for (int g = 0; g < kFarTab; ++g) {
                 fv[g] = 0; fv2[g] = 0;
                 if ((uint32_t)g < nf8) {
                     const v4u q = fprm[g];   // bytes past the match repeat its last one (never written)
@@ -2103,7 +2112,7 @@ struct Dec {
         // 5c. far bytes into the ring at the match outputs
         if (farM) {
 #pragma unroll
-            for (int g = 0; g < 8; ++g) {
+            for (int g = 0; g < kFarTab; ++g) {
                 if ((uint32_t)g < nf8) {
                     const v4u q = fprm[g];
                     *(L < q.z ? ringp + ((q.y + L) & (kRing - 1)) : dummy + L) = (uint8_t)fv[g];
@@ -2111,8 +2120,8 @@ struct Dec {
                         *(L + 64 < q.z ? ringp + ((q.y + 64 + L) & (kRing - 1)) : dummy + 64 + L) = (uint8_t)fv2[g];
                 }
             }
-            uint64_t farLeft = ballot(far && fr >= 8);
-            while (farLeft) {   // more than 8 far matches: one at a time
+            uint64_t farLeft = ballot(far && fr >= (uint32_t)kFarTab);
+            while (farLeft) {   // more than kFarTab far matches: one at a time
                 const int j = __ffsll((long long)farLeft) - 1;
                 const uint32_t js = (uint32_t)rdlane((uint32_t)src, j), jm = rdlane(mlen, j);
                 const uint32_t jo = (uint32_t)rdlane((uint32_t)om, j);

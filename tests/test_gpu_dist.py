@@ -129,3 +129,17 @@ def test_streamed_gather_on_device(n, bid, cap, kind):
         assert p.exitcode == 0
     assert same, (rounds, size)
     assert rounds >= 2
+
+
+@pytest.mark.gpu
+def test_bench_gpus3_strong_uneven_1mib_blocks():
+    """Three ranks, ONE 0.25 GiB buffer of 1 MiB blocks (256 blocks: shards of
+    86 / 85 / 85), streamed gather with the IPC push: the stitched frame is
+    checked against every shard (dist.verify_stitched) and each rank decodes
+    its scattered piece back to its source."""
+    line = _bench("--gpus", "3", "--total-gib", "0.25", "--block-id", "6", "--steps", "1", "--warmup", "1",
+                  "--no-cpu-baseline")
+    assert line["n_gpus"] == 3 and line["scaling"] == "strong"
+    assert line["config"]["bytes_total"] == 1 << 28 and line["config"]["block_bytes"] == 1 << 20
+    assert line["gather"].startswith("streamed") and "ipc" in line["gather"]
+    assert line["stitched_frame_ok"] is True and line["roundtrip_ok"] is True

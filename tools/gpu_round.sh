@@ -78,6 +78,11 @@ for step in "$@"; do
         done
       done
       cat "$out/follow.txt" ;;
+    abtest)   # parity tests against exp_libs/$ABLIB.so (the candidate of an A/B)
+      LZ4MT_AMD_LIB=exp_libs/$ABLIB.so timeout -k 10 900 python3 -u -m pytest -m gpu -x -q --timeout 300 \
+          --timeout-method thread tests/test_gpu.py tests/test_gpu_configs.py tests/test_gpu_bd.py \
+          > "$out/abtest_$ABLIB.log" 2>&1 || { tail -30 "$out/abtest_$ABLIB.log"; exit 1; }
+      tail -2 "$out/abtest_$ABLIB.log" ;;
     ab5)   # the same at 256 KiB blocks (32768 blocks per 8 GiB: occupancy-sensitive)
       BID=5 bash tools/ab.sh > "$out/ab5.txt" 2>&1 && BID=5 bash tools/ab.sh >> "$out/ab5.txt" 2>&1
       cat "$out/ab5.txt" ;;
