@@ -627,6 +627,12 @@ static_assert(kCatchLanes >= 1 && kCatchLanes <= 64, "catch-up lanes");
 constexpr uint64_t kCatchMask = kCatchLanes >= 64 ? ~0ull : (1ull << kCatchLanes) - 1ull;
 static_assert(kCountLanes >= 1 && kCountLanes <= 63, "count lanes");
 constexpr uint32_t kSRMirror = 64;    // ring[kSR .. kSR+64) mirrors ring[0 .. 64)
+// near candidates: when every byte of a stop's round trip (verify and count
+// words, catch-up bytes) lies in the source ring, read them from LDS
+#ifndef LZ4MT_RING_RT
+#define LZ4MT_RING_RT 0
+#endif
+constexpr bool kRingRT = LZ4MT_RING_RT != 0;
 
 __device__ __forceinline__ uint32_t gld4u(g_cu8* p) { return *(g_cu32u*)p; }
 __device__ __forceinline__ uint64_t gld8u(g_cu8* p) { return *(g_cu64u*)p; }
@@ -995,11 +1001,20 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                     // rest repeat lane 0's address (no further lines touched)
                     const bool cOn = L <= kCountLanes;
                     const uint32_t ci = cOn ? cd + 4 * L : cd, ii = cOn ? ip + 4 * L : ip;
-                    cw = gld4u(s + (ci < last4 ? ci : last4));
-                    iw = gld4u(s + (ii < last4 ? ii : last4));
                     const bool bOn = L < maxb && L < kCatchLanes;
-                    bi = s[bOn ? ip - L - 1 : o0];   // (o0: a byte of the block itself)
-                    bc = s[bOn ? cd - L - 1 : o0];
+                    if (kRingRT && cd >= V.B + kCatchLanes && ip + 4 * kCountLanes + 4 <= V.B + kSR) {
+                        // every byte the round trip would load lies in the source
+                        // ring (a near candidate): read them from LDS instead
+                        cw = *(const l_u32u*)(V.r + ((ci < last4 ? ci : last4) & (kSR - 1)));
+                        iw = *(const l_u32u*)(V.r + ((ii < last4 ? ii : last4) & (kSR - 1)));
+                        bi = V.r[(bOn ? ip - L - 1 : ip - 1) & (kSR - 1)];
+                        bc = V.r[(bOn ? cd - L - 1 : cd - 1) & (kSR - 1)];
+                    } else {
+                        cw = gld4u(s + (ci < last4 ? ci : last4));
+                        iw = gld4u(s + (ii < last4 ? ii : last4));
+                        bi = s[bOn ? ip - L - 1 : o0];   // (o0: a byte of the block itself)
+                        bc = s[bOn ? cd - L - 1 : o0];
+                    }
                     if (havePe) {
                         store_pend(pe, V, s, d);
                         havePe = false;
