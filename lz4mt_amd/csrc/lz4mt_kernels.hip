@@ -633,6 +633,9 @@ constexpr uint32_t kSRMirror = 64;    // ring[kSR .. kSR+64) mirrors ring[0 .. 6
 #define LZ4MT_RING_RT 0
 #endif
 constexpr bool kRingRT = LZ4MT_RING_RT != 0;
+#ifndef LZ4MT_NOSTORE_TEST
+#define LZ4MT_NOSTORE_TEST 0
+#endif
 
 __device__ __forceinline__ uint32_t gld4u(g_cu8* p) { return *(g_cu32u*)p; }
 __device__ __forceinline__ uint64_t gld8u(g_cu8* p) { return *(g_cu64u*)p; }
@@ -796,7 +799,12 @@ __device__ __forceinline__ void store_pend(const PendSeq& p, const SrcRing& V, g
             const uint32_t x = min(base + L, e.total - 1);   // lanes past the end repeat the last byte
             uint32_t lv = V.r[(p.anchor + x - e.a1) & (kSR - 1)];
             asm volatile("" : "+v"(lv));
+#if LZ4MT_NOSTORE_TEST   // timing experiment only: the bytes are computed, never stored
+            const uint32_t pb = pend_byte(e, x, lv);
+            asm volatile("" ::"v"(pb));
+#else
             d[p.op + x] = (uint8_t)pend_byte(e, x, lv);
+#endif
         }
     } else {   // literals no longer (or not yet) in the ring: global bytes
         for (uint32_t base = 0; base < e.total; base += 64) {
@@ -2879,6 +2887,14 @@ hipError_t launch_decode(const uint8_t* frame, const BlockRec* recs, uint32_t nB
 // XXH32: 4 lanes per block (one per accumulator), 16 blocks per wavefront
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t xround(uint32_t acc, uint32_t w) { return rotl32(acc + w * kP2, 13) * kP1; }
+// a round on a word premultiplied by P2 (LLVM fuses the multiply with the
+// next round's add into one v_mad_u64_u32: the chain is alignbit + mad)
+__device__ __forceinline__ uint32_t xround_pm(uint32_t acc, uint32_t wp) { return rotl32(acc + wp, 13) * kP1; }
+// LZ4MT_XXH_FULL: a whole 1 KiB chunk's LDS reads in flight before its 64
+// rounds (k_xxh32_stored 4.05 -> 3.78 ms at 8 GiB; profiles/r03n_xxh32_ab.txt)
+#ifndef LZ4MT_XXH_FULL
+#define LZ4MT_XXH_FULL 1
+#endif
 
 // One wavefront hashes one byte range: the range streams through LDS in
 // 1 KiB chunks (64 lanes x 16 B, loaded one chunk ahead), lanes 0..3 run
@@ -2905,7 +2921,9 @@ __device__ uint32_t xxh32_wave(g_cu8* p, uint64_t len, l_u32* __restrict__ buf /
     if (nch && (uint64_t)L < ns) r = load16u(p + 16 * L);
     uint32_t cur = 0;
     for (uint64_t ch = 0; ch < nch; ++ch) {
-        ((l_u4*)(buf + cur * 256))[L] = r;
+        // words stored premultiplied by P2 (64 lanes at once): the chain
+        // below keeps only rotl + mul per round
+        ((l_u4*)(buf + cur * 256))[L] = (v4u){r.x * kP2, r.y * kP2, r.z * kP2, r.w * kP2};
         const uint64_t nxt = (ch + 1) * 64 + L;
         if (ch + 1 < nch && nxt < ns) r = load16u(p + 16 * nxt);
         WAVE_SYNC();
@@ -2913,14 +2931,24 @@ __device__ uint32_t xxh32_wave(g_cu8* p, uint64_t len, l_u32* __restrict__ buf /
             const uint32_t m = (uint32_t)min<uint64_t>(64, ns - ch * 64);
             const l_u32* cb = buf + cur * 256 + L;
             uint32_t i = 0;
+#if LZ4MT_XXH_FULL
+            if (m == 64) {   // a whole chunk: every read issued before the chain starts
+                uint32_t w[64];
+#pragma unroll
+                for (int u = 0; u < 64; ++u) w[u] = cb[4 * u];
+#pragma unroll
+                for (int u = 0; u < 64; ++u) v = xround_pm(v, w[u]);
+                i = 64;
+            }
+#endif
             for (; i + 8 <= m; i += 8) {
                 uint32_t w[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) w[u] = cb[4 * (i + u)];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) v = xround(v, w[u]);
+                for (int u = 0; u < 8; ++u) v = xround_pm(v, w[u]);
             }
-            for (; i < m; ++i) v = xround(v, cb[4 * i]);
+            for (; i < m; ++i) v = xround_pm(v, cb[4 * i]);
         }
         WAVE_SYNC();
         cur ^= 1;
@@ -3235,6 +3263,10 @@ __global__ void __launch_bounds__(1024) k_frame_scan(const int32_t* __restrict__
 #ifndef LZ4MT_ASM_NT
 #define LZ4MT_ASM_NT 0
 #endif
+// chunks per thread in flight in the assembly's middle loop (A/B)
+#ifndef LZ4MT_ASM_UNROLL
+#define LZ4MT_ASM_UNROLL 1
+#endif
 
 __global__ void __launch_bounds__(256) k_frame_assemble(const uint8_t* __restrict__ src, const uint8_t* __restrict__ slots,
                                                         uint64_t srcSize, uint32_t blockSize,
@@ -3266,6 +3298,7 @@ __global__ void __launch_bounds__(256) k_frame_assemble(const uint8_t* __restric
     for (uint64_t i = tailStart + t; i < L; i += 256) D[i] = sp[i];
     // middle: 16-B aligned destination chunks gathered from the source
     const uint64_t nchunks = (E0 - A0) >> 4;
+#pragma unroll LZ4MT_ASM_UNROLL
     for (uint64_t j = t; j < nchunks; j += 256) {
         const uint64_t so = head + 16 * j;                 // source byte offset of this chunk
         g_cu32* q = (g_cu32*)(sp + (so & ~3ull));
