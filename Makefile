@@ -16,13 +16,17 @@ $(BUILD):
 	mkdir -p $(BUILD)
 
 # One source, two objects: the decoder's dependent-load chains schedule
-# better under max-ilp (decode kernel 31.8 -> 30.1 ms at 8 GiB); the encoder
-# gains ~0.5 % under max-memory-clause (191.0 vs 192.2 ms, measured twice).
+# better under max-ilp (decode kernel 31.8 -> 30.1 ms at 8 GiB; 33.2 ms with
+# the default scheduler); the encoder is fastest under iterative-ilp (8 GiB
+# B7: 182.4 / 182.7 ms vs 184.5 / 185.0 under max-memory-clause, 182.9 /
+# 183.7 default, 183.5 / 184.1 max-ilp; profiles/r03p_sched_ab.txt).
+ENC_SCHED ?= -mllvm --amdgpu-sched-strategy=iterative-ilp
 $(BUILD)/lz4mt_kernels_enc.o: $(CSRC)/lz4mt_kernels.hip $(HDRS) | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -DLZ4MT_PART=1 -mllvm --amdgpu-sched-strategy=max-memory-clause -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) -DLZ4MT_PART=1 $(ENC_SCHED) -c -o $@ $<
 
+DEC_SCHED ?= -mllvm --amdgpu-sched-strategy=max-ilp
 $(BUILD)/lz4mt_kernels_dec.o: $(CSRC)/lz4mt_kernels.hip $(HDRS) | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -DLZ4MT_PART=2 -mllvm --amdgpu-sched-strategy=max-ilp -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) -DLZ4MT_PART=2 $(DEC_SCHED) -c -o $@ $<
 
 $(BUILD)/%.o: $(CSRC)/%.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
