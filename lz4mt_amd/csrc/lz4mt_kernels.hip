@@ -636,6 +636,11 @@ constexpr bool kRingRT = LZ4MT_RING_RT != 0;
 #ifndef LZ4MT_NOSTORE_TEST
 #define LZ4MT_NOSTORE_TEST 0
 #endif
+// LZ4MT_ENC_NT: the encoder's byte stores non-temporal, so output lines do not
+// displace the source lines the round trips read back from L2 (A/B)
+#ifndef LZ4MT_ENC_NT
+#define LZ4MT_ENC_NT 0
+#endif
 
 __device__ __forceinline__ uint32_t gld4u(g_cu8* p) { return *(g_cu32u*)p; }
 __device__ __forceinline__ uint64_t gld8u(g_cu8* p) { return *(g_cu64u*)p; }
@@ -802,6 +807,8 @@ __device__ __forceinline__ void store_pend(const PendSeq& p, const SrcRing& V, g
 #if LZ4MT_NOSTORE_TEST   // timing experiment only: the bytes are computed, never stored
             const uint32_t pb = pend_byte(e, x, lv);
             asm volatile("" ::"v"(pb));
+#elif LZ4MT_ENC_NT
+            __builtin_nontemporal_store((uint8_t)pend_byte(e, x, lv), (g_u8*)&d[p.op + x]);
 #else
             d[p.op + x] = (uint8_t)pend_byte(e, x, lv);
 #endif
