@@ -28,6 +28,10 @@ DEC_SCHED ?= -mllvm --amdgpu-sched-strategy=max-ilp
 $(BUILD)/lz4mt_kernels_dec.o: $(CSRC)/lz4mt_kernels.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DLZ4MT_PART=2 $(DEC_SCHED) -c -o $@ $<
 
+HC_SCHED ?=
+$(BUILD)/lz4mt_hc.o: $(CSRC)/lz4mt_hc.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $(HC_SCHED) -c -o $@ $<
+
 $(BUILD)/%.o: $(CSRC)/%.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 

@@ -637,10 +637,12 @@ constexpr bool kRingRT = LZ4MT_RING_RT != 0;
 #define LZ4MT_NOSTORE_TEST 0
 #endif
 // LZ4MT_ENC_NT: the encoder's byte stores non-temporal, so output lines do not
-// displace the source lines the round trips read back from L2 (k_encode
-// 182.2 -> 181.6 ms at 8 GiB B7, profiles/r03s_enc_nt_ab.txt)
+// displace the source lines the round trips read back from L2.  Off: it
+// saves 0.3 % of k_encode but the byte stores then reach HBM uncombined --
+// WRITE_SIZE 24.2 GB per 8 GiB launch instead of 4.24 GB
+// (profiles/r03s_enc_nt_ab.txt, r03t_pmc.json)
 #ifndef LZ4MT_ENC_NT
-#define LZ4MT_ENC_NT 1
+#define LZ4MT_ENC_NT 0
 #endif
 
 __device__ __forceinline__ uint32_t gld4u(g_cu8* p) { return *(g_cu32u*)p; }
