@@ -28,7 +28,7 @@ DEC_SCHED ?= -mllvm --amdgpu-sched-strategy=max-ilp
 $(BUILD)/lz4mt_kernels_dec.o: $(CSRC)/lz4mt_kernels.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DLZ4MT_PART=2 $(DEC_SCHED) -c -o $@ $<
 
-HC_SCHED ?=
+HC_SCHED ?= -mllvm --amdgpu-sched-strategy=iterative-ilp
 $(BUILD)/lz4mt_hc.o: $(CSRC)/lz4mt_hc.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $(HC_SCHED) -c -o $@ $<
 
