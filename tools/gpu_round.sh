@@ -12,6 +12,8 @@
 #   fcal    FETCH_SIZE calibration on a known byte count (tools/fetch_cal.py + fetchcal_sum.py)
 #   tail    the streamed gather's exposed tail on one GPU (tools/tail_model.py)
 #   ab      kernel times of every exp_libs/*.so (tools/mkvariants.sh), two passes
+#   abtrace kernel-trace stats of every exp_libs/*.so;  abbid  ab at every block size
+#   fuzz    random differential campaign (300 s);  sweep  the secondary bench configs
 set -euo pipefail
 tag=$1; shift
 out=gpurun_out/$tag
@@ -86,6 +88,31 @@ for step in "$@"; do
     ab5)   # the same at 256 KiB blocks (32768 blocks per 8 GiB: occupancy-sensitive)
       BID=5 bash tools/ab.sh > "$out/ab5.txt" 2>&1 && BID=5 bash tools/ab.sh >> "$out/ab5.txt" 2>&1
       cat "$out/ab5.txt" ;;
+    abtrace)   # kernel-trace stats of tools/ktime.py for every exp_libs/*.so (per-kernel times per variant)
+      for f in exp_libs/*.so; do
+        nm=$(basename $f .so)
+        LZ4MT_AMD_LIB=$f timeout -k 10 200 rocprofv3 --kernel-trace --stats -T -f csv -d "$out/$nm" -o t -- \
+            python3 tools/ktime.py > "$out/$nm.txt" 2>&1
+        grep -v amdgpu "$out/$nm.txt"
+      done ;;
+    abbid)   # tools/ab.sh at BID = 4, 6, 5, 7 (block-size dependence of an A/B)
+      for b in 4 6 5 7; do
+        echo "## BID $b" >> "$out/ab_bid.txt"
+        BID=$b bash tools/ab.sh >> "$out/ab_bid.txt" 2>&1
+      done
+      cat "$out/ab_bid.txt" ;;
+    fuzz)   # time-boxed random differential campaign (seed 7) against the oracle / liblz4
+      timeout -k 10 420 python3 -u tools/fuzz_campaign.py 300 7 > "$out/fuzz.txt" 2>&1
+      tail -2 "$out/fuzz.txt" ;;
+    sweep)   # secondary configs: block sizes, 32 GiB decompress-only, default flags, HC level 9, -BD B7
+      for spec in "b4 --block-id 4 --steps 5 --warmup 2" "b5 --block-id 5 --steps 5 --warmup 2" \
+                  "b6 --block-id 6 --steps 5 --warmup 2" "dec32 --gib 32 --decompress-only --steps 3 --warmup 1" \
+                  "sck --stream-checksum --steps 3 --warmup 1" "hc9 --level 9 --steps 2 --warmup 1" \
+                  "bd7 --block-dependent --steps 2 --warmup 1"; do
+        set -- $spec; name=$1; shift
+        timeout -k 10 300 python3 bench.py --no-cpu-baseline "$@" > "$out/$name.json" 2> "$out/$name.err"
+        echo "$name $(cut -c1-300 "$out/$name.json")"
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
