@@ -50,6 +50,7 @@ torch = dist = L = D = None
 GiB = float(1 << 30)
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 GOLDEN = 0x9E3779B97F4A7C15
+# the headline's PMC profile; the sweep points' are profiles/pmc_b<id>.json
 PMC_PROFILE = os.path.join(ROOT, "profiles", "pmc_current.json")
 
 
@@ -201,13 +202,20 @@ def pmc_traffic(kernel, n, bm, flg):
     FETCH_SIZE is divided by the calibration the profile measured on a known
     byte count (MI355X_MICROARCH.md: gfx950 FETCH_SIZE is ~1/2 of wide
     streaming reads; other widths need their own calibration)."""
-    try:
-        prof = json.load(open(PMC_PROFILE))
-    except (OSError, ValueError):
-        return None, "no profiles/pmc_current.json"
-    cfg = prof.get("config", {})
-    if (cfg.get("bytes"), cfg.get("block_bytes"), cfg.get("flg")) != (n, bm, flg):
-        return None, f"profile config {cfg} is not this run's"
+    import glob
+    prof, seen = None, []
+    for path in [PMC_PROFILE] + sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_b*.json"))):
+        try:
+            p = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        cfg = p.get("config", {})
+        seen.append(cfg.get("workload", os.path.basename(path)))
+        if (cfg.get("bytes"), cfg.get("block_bytes"), cfg.get("flg")) == (n, bm, flg):
+            prof = p
+            break
+    if prof is None:
+        return None, f"no PMC profile of this configuration (have: {seen})"
     k = prof.get("kernels", {}).get(kernel)
     if not k:
         return None, f"{kernel} not in the profile"
@@ -222,6 +230,26 @@ def pmc_traffic(kernel, n, bm, flg):
             "fetch_calibrated": round(fetch),
             "write": k["write_bytes"], "calibration": cal.get("how", "guide x2 (uncalibrated)"),
             "source": "profiles/pmc_current.json (" + prof.get("tag", "?") + ")"}, None
+
+
+def frame_encoder(bm):
+    """The kernel lz4mtHipCompressFrameAsyncEx runs for bm-byte blocks
+    (launch_encode, lz4mt_kernels.hip): the byU16 table below 65 547 B, the
+    3-byte table at 256 KiB (LZ4MT_AMD_ENC overrides), else k_encode."""
+    enc = os.environ.get("LZ4MT_AMD_ENC", "")
+    if bm < 65547:
+        return "k_encode16"
+    if enc == "p17" or (enc != "base" and bm <= (256 << 10)):
+        return "k_encode_p17"
+    return "k_encode"
+
+
+def workload_id(world, block_id):
+    """configs[1] is the 4 MiB headline; other block sizes are the configs[4]
+    sweep; N > 1 is configs[3]."""
+    if world > 1:
+        return "configs[3]"
+    return "configs[1]" if block_id == 7 else "configs[4] (block-size sweep)"
 
 
 def _free_port():
@@ -259,9 +287,13 @@ def main():
     # ranks sharing the GPUs there are (gloo moves CUDA tensors through the
     # host); the measured multi-GPU path is RCCL, one rank per GPU
     backend = os.environ.get("LZ4MT_BENCH_BACKEND", "nccl")
+    # LZ4MT_BENCH_DIST=1 runs the N > 1 path (process group, streamed gather,
+    # scatter, stitched-frame check) at world size 1 too: the nccl backend on
+    # a one-GPU box (RCCL allows one rank per device)
+    distributed = world > 1 or os.environ.get("LZ4MT_BENCH_DIST") == "1"
     local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
     torch.cuda.set_device(local)
-    if world > 1:
+    if distributed:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -279,13 +311,13 @@ def main():
     seed = (42 + (first_byte // 65536) * GOLDEN) % (1 << 64)   # App. F segment index of the shard's start
     src = L.gen_synthetic(n, seed=seed, device=dev)
     sck = a.stream_checksum
-    if sck and world > 1:
+    if sck and distributed:
         raise SystemExit("the content checksum (FLG.2) is one serial chain over the whole stream: it does not shard")
     sd = L.make_sd(a.block_id, stream_checksum=sck, block_checksum=not sck, block_dependence=a.block_dependent)
     flg = (0x64 if sck else 0x70) & ~(0x20 if a.block_dependent else 0)
-    if (a.level >= 3 or a.block_dependent) and world > 1:
+    if (a.level >= 3 or a.block_dependent) and distributed:
         raise SystemExit("--level / --block-dependent are single-GPU measurements")
-    streamed = world > 1 and a.gather == "streamed" and not a.decompress_only
+    streamed = distributed and a.gather == "streamed" and not a.decompress_only
     cap = L.frame_bound(n, sd)
     # the streamed gather builds the frame on rank 0 from the shard workspace:
     # no per-rank frame buffer or frame workspace (8 + 8 GiB per GPU spared)
@@ -321,7 +353,7 @@ def main():
 
     def sync_all():
         torch.cuda.synchronize()
-        if world > 1:
+        if distributed:
             dist.barrier()
         return time.perf_counter()
 
@@ -332,12 +364,13 @@ def main():
     if streamed:   # the shard engine's streams and workspace, the control group and transport, made once
         eng = D.HipShardEngine(dev)
         shard_ws = L.shard_workspace(n, sd, device=dev)
-        ctrl = dist.new_group(backend="gloo") if backend == "nccl" else None
+        ctrl = D.control_group()
         transport = D.IpcPushTransport(dev) if a.transport == "ipc" else D.RcclTransport()
         transport_name = a.transport
+        peers = D.peer_access_matrix() if rank == 0 else None
     L.lib.lz4mtHipSetTiming(1)
     tc = td = ts = tg = 0.0
-    enc_ms, dec_ms, frame_len, exposed_ms, rounds, tails = [], [], 0, [], [], []
+    enc_ms, dec_ms, frame_len, exposed_ms, rounds, tails, scat = [], [], 0, [], [], [], []
     full = piece = None
     for it in range(a.warmup + a.steps):
         timed = it >= a.warmup
@@ -349,11 +382,10 @@ def main():
             try:
                 full = D.compress_gather_streamed(src, sd, dst=0, engine=eng, ws=shard_ws, stats=st_,
                                                   transport=transport, ctrl=ctrl)
-            except RuntimeError as e:   # the IPC setup failed on some rank (collectively): RCCL instead
-                if transport_name != "ipc":
-                    raise
-                print(f"bench.py: IPC push unavailable ({e}); streamed gather over RCCL", file=sys.stderr)
-                transport, transport_name = D.RcclTransport(), "rccl (IPC setup failed)"
+            except D.IpcSetupError as e:   # raised on every rank together: all switch to RCCL
+                print(f"bench.py: IPC PUSH UNAVAILABLE ({e}); streamed gather falls back to RCCL point-to-point",
+                      file=sys.stderr, flush=True)
+                transport, transport_name = D.RcclTransport(), f"rccl (IPC setup failed: {e})"
                 full = D.compress_gather_streamed(src, sd, dst=0, engine=eng, ws=shard_ws, stats=st_,
                                                   transport=transport, ctrl=ctrl)
             end_ev = torch.cuda.Event(enable_timing=True)
@@ -374,19 +406,22 @@ def main():
             if not a.decompress_only:
                 tm = timings()
             tl = time.perf_counter()
-            if world > 1:   # the gather belongs to compress
+            if distributed:   # the gather belongs to compress
                 full = D.gather_frame(frame_buf, frame_len, dst=0)
                 torch.cuda.synchronize()
             t1 = sync_all()
-            tgr = time.perf_counter() - tl if world > 1 else 0.0
-        if world > 1:
+            tgr = time.perf_counter() - tl if distributed else 0.0
+        if distributed:
+            sst = {}
             piece = D.scatter_frame(full if rank == 0 else None, full.numel() if rank == 0 else 0, src=0,
-                                    device=dev)
+                                    device=dev, stats=sst)
+            if timed:
+                scat.append(sst)
             torch.cuda.synchronize()
             t2 = sync_all()
         else:
             piece, t2 = frame_buf, t1
-        decompress(piece, piece.numel() if world > 1 else frame_len)
+        decompress(piece, piece.numel() if distributed else frame_len)
         tmd = timings()
         t3 = sync_all()
         if timed:
@@ -404,7 +439,15 @@ def main():
     # N > 1 the root decodes the stitched frame and checks every shard
     ok = bool(torch.equal(out[:n], src))
     stitched_ok = None
-    if world > 1:
+    mem = None
+    if distributed:
+        # the root's device memory at its peak: torch's allocator (sources,
+        # workspaces, mirrors, the stitched frame, pieces) and the device as
+        # a whole (hipMemGetInfo: + the IPC receive buffers, library scratch)
+        free_b, total_b = torch.cuda.mem_get_info(dev)
+        mem = {"max_allocated_GiB": round(torch.cuda.max_memory_allocated(dev) / GiB, 2),
+               "device_used_GiB": round((total_b - free_b) / GiB, 2), "device_total_GiB": round(total_b / GiB, 2)}
+
         def digests(t):
             return L.xxh32_chunks(t, 16 << 20).to(torch.int64)
 
@@ -412,6 +455,7 @@ def main():
             o, r = L.decompress_frame(f)
             return o if r == 0 else o[:0]
         stitched_ok = D.verify_stitched(full if rank == 0 else None, src, decode_full, digests)
+        mem["after_verify_max_allocated_GiB"] = round(torch.cuda.max_memory_allocated(dev) / GiB, 2)
         t = torch.tensor([tc, td, ts, tg, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         tc, td, ts, tg, bad = t.tolist()
@@ -430,7 +474,7 @@ def main():
     # the kernels the timing marks bracket in this mode
     enc_k = ("k_encode_hc_bd" if a.block_dependent and a.level >= 3 else "k_encode_linked_round"
              if a.block_dependent else "k_encode_hc" if a.level >= 3 else
-             "k_encode_pub (+ k_xxh32_stored)" if streamed else "k_encode")
+             "k_encode_pub (+ k_xxh32_stored)" if streamed else frame_encoder(bm))
     dec_k = "k_decode_linked" if a.block_dependent else "k_decode"
     roof = dec_roof = None
     if enc_avg:
@@ -471,11 +515,11 @@ def main():
                                     f"{world} GPU(s), {bm >> 10} KiB independent blocks, {flags} frame, "
                                     f"compress+decompress+XXH32, device-resident")
                                    if a.total_gib is not None else
-                                   (f"configs[{1 if world == 1 else 3}]: {a.gib:g} GiB/GPU synthetic, {bm >> 10} KiB "
+                                   (f"{workload_id(world, a.block_id)}: {a.gib:g} GiB/GPU synthetic, {bm >> 10} KiB "
                                     f"independent blocks, {flags} frame, compress+decompress+XXH32, device-resident"),
                        "bytes_per_gpu": n, "bytes_total": n_total, "block_bytes": bm,
                        "parallelism": f"block-sharded x{world}" + (", RCCL gather to one frame on rank 0 (in compress)"
-                                                                   if world > 1 else "")},
+                                                                   if distributed else "")},
             "compress_GiBps": round(comp_gibps, 3) if comp_gibps else None,
             "decompress_GiBps": round(decomp_gibps, 3),
             "ratio": round((n_total / frame_len) if streamed else (n / frame_len), 4), "frame_bytes": frame_len,
@@ -487,16 +531,23 @@ def main():
                          "gather_rounds": round(sum(rounds[a.warmup:]) / max(1, K), 1),
                          "gather_tail_rounds": round(sum(t[1] for t in tails[a.warmup:]) / max(1, K), 1),
                          "gather_tail_rounds_ms": round(sum(t[0] for t in tails[a.warmup:]) / max(1, K) * 1e3, 3)})
-        elif world > 1:
+        elif distributed:
             line.update({"gather": "after the encode (dist.gather_frame)"})
-        if world > 1:
-            line.update({"gather_ms": round(tg / K * 1e3, 3), "scatter_ms": round(ts / K * 1e3, 3),
+        if distributed:
+            def avg(k):
+                return round(sum(x[k] for x in scat) / max(1, len(scat)) * 1e3, 3)
+            line.update({"backend": backend, "transport": transport_name if streamed else backend,
+                         "gather_ms": round(tg / K * 1e3, 3), "scatter_ms": round(ts / K * 1e3, 3),
+                         "scatter_split_ms": {"walk": avg("walk_s"), "table": avg("table_s"), "p2p": avg("p2p_s"),
+                                              "assemble": avg("assemble_s"),
+                                              "host_staged": bool(scat and scat[0]["host_staged"])},
+                         "root_memory": mem, "peer_access": peers if streamed else D.peer_access_matrix(),
                          "stitched_frame_bytes": full.numel(), "stitched_frame_ok": stitched_ok,
                          "roundtrip_with_scatter_GiBps": round(total / GiB / (tc + ts + td), 3)})
         print(json.dumps(line), flush=True)
     if streamed:
         transport.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
     if not ok:
         sys.exit(1)

@@ -153,8 +153,14 @@ uint64_t lz4mtHipShardPackBound(uint64_t n, const Lz4MtStreamDescriptor* sd, uin
 /* The frame header lz4mtCompress writes for `sd` (magic .. header checksum)
  * into out[19]; returns its length, -1 on a bad descriptor. */
 int lz4mtHipFrameHeader(const Lz4MtStreamDescriptor* sd, uint8_t* out);
+/* Zeroes the workspace's round state (published, packed and hashed counts)
+ * on `stream`.  Required before every encode into the workspace, and it must
+ * be stream-ordered before the encode AND before the call's first pack (the
+ * two usually run on different streams: reset on a stream both wait on). */
+Lz4MtResult lz4mtHipShardReset(uint64_t n, const Lz4MtStreamDescriptor* sd, void* d_ws, uint64_t wsSize, void* stream);
 /* Launches the shard's encode (+ block checksums) on `stream`; 1 and 4 MiB
- * blocks publish their progress as they go.  Asynchronous. */
+ * blocks publish their progress as they go.  Asynchronous.  The workspace
+ * must have been reset (lz4mtHipShardReset) after its previous use. */
 Lz4MtResult lz4mtHipShardEncode(const void* d_src, uint64_t n, const Lz4MtStreamDescriptor* sd, void* d_ws,
                                 uint64_t wsSize, void* stream);
 /* One round into d_pack (capacity >= lz4mtHipShardPackBound): final = 0 while

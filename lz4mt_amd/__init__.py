@@ -25,7 +25,7 @@ __all__ = [
     "compress", "decompress", "compress_block", "decompress_block", "compress_bound",
     "compress_frame", "decompress_frame", "frame_info", "frame_bound", "gen_synthetic", "xxh32",
     "device_count", "stream_bound", "frame_records", "xxh32_chunks", "frame_header", "shard_workspace",
-    "shard_pack_bound", "shard_encode", "shard_pack", "shard_unpack", "shard_assemble", "shard_body_bytes",
+    "shard_pack_bound", "shard_reset", "shard_encode", "shard_pack", "shard_unpack", "shard_assemble", "shard_body_bytes",
 ]
 
 lib = _abi.load()
@@ -291,8 +291,17 @@ def shard_pack_bound(n, sd, per_block_cap):
     return int(lib.lz4mtHipShardPackBound(int(n), ctypes.byref(sd), int(per_block_cap)))
 
 
+def shard_reset(n, sd, ws, stream=None):
+    """Zeroes the round state of ``ws`` on ``stream`` (before every encode, and
+    stream-ordered before that call's first pack too)."""
+    r = lib.lz4mtHipShardReset(int(n), ctypes.byref(sd), ctypes.c_void_p(ws.data_ptr()), ws.numel(), _stream(stream))
+    if r != Result.OK:
+        raise Lz4MtError(r, "lz4mtHipShardReset")
+
+
 def shard_encode(src, sd, ws, stream=None):
-    """Launches the shard's encode (+ block checksums); asynchronous on ``stream``."""
+    """Launches the shard's encode (+ block checksums); asynchronous on
+    ``stream``.  ``ws`` must have been reset (``shard_reset``) first."""
     _check_dev(src, "src")
     r = lib.lz4mtHipShardEncode(ctypes.c_void_p(src.data_ptr() if src.numel() else ws.data_ptr()), src.numel(),
                                 ctypes.byref(sd), ctypes.c_void_p(ws.data_ptr()), ws.numel(), _stream(stream))

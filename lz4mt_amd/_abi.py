@@ -117,6 +117,7 @@ PROTOTYPES = {
     "lz4mtHipShardWorkspaceSize": (c_uint64, [c_uint64, SD_P]),
     "lz4mtHipShardPackBound": (c_uint64, [c_uint64, SD_P, c_uint32]),
     "lz4mtHipFrameHeader": (c_int, [SD_P, c_void_p]),
+    "lz4mtHipShardReset": (c_int, [c_uint64, SD_P, c_void_p, c_uint64, c_void_p]),
     "lz4mtHipShardEncode": (c_int, [c_void_p, c_uint64, SD_P, c_void_p, c_uint64, c_void_p]),
     "lz4mtHipShardPack": (c_int, [c_void_p, c_uint64, SD_P, c_void_p, c_uint64, c_void_p, c_uint64, c_uint32, c_int,
                                   c_void_p]),

@@ -301,6 +301,28 @@ extern "C" int lz4mtHipFrameHeader(const Lz4MtStreamDescriptor* sd, uint8_t* out
     return build_header(sd, out);
 }
 
+// The round state (published / packed / hashed counts) of a workspace back to
+// zero.  Separate from the encode: the encode and the rounds' packs run on
+// two streams, and both must be ordered after the reset -- a pack that read
+// `sent` or `pub` while another stream still zeroed them could pack from a
+// stale (or, on a fresh buffer, arbitrary) offset.
+extern "C" Lz4MtResult lz4mtHipShardReset(uint64_t n, const Lz4MtStreamDescriptor* sd, void* d_ws, uint64_t wsSize,
+                                          void* stream) {
+    uint32_t bm = 0;
+    const Lz4MtResult v = shard_sd(sd, &bm);
+    if (v != LZ4MT_RESULT_OK) return v;
+    const uint64_t nb = (n + bm - 1) / bm;
+    if (!d_ws || wsSize < carve(nullptr, nb, bm).bytes || nb > 0xFFFFFFFFull) return LZ4MT_RESULT_BAD_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return LZ4MT_RESULT_ERROR;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    const ShardWs w = carve(static_cast<uint8_t*>(d_ws), nb, bm);
+    SHCHK(hipMemsetAsync(w.pub, 0, nb * 4 + 4, st));
+    SHCHK(hipMemsetAsync(w.sent, 0, nb * 4 + 4, st));
+    SHCHK(hipMemsetAsync(w.xdone, 0, nb * 4 + 4, st));
+    return LZ4MT_RESULT_OK;
+}
+
 extern "C" Lz4MtResult lz4mtHipShardEncode(const void* d_src, uint64_t n, const Lz4MtStreamDescriptor* sd, void* d_ws,
                                            uint64_t wsSize, void* stream) {
     uint32_t bm = 0;
@@ -314,9 +336,6 @@ extern "C" Lz4MtResult lz4mtHipShardEncode(const void* d_src, uint64_t n, const 
     const hipStream_t st = static_cast<hipStream_t>(stream);
     const ShardWs w = carve(static_cast<uint8_t*>(d_ws), nb, bm);
     const uint8_t* src = static_cast<const uint8_t*>(d_src);
-    SHCHK(hipMemsetAsync(w.pub, 0, nb * 4 + 4, st));
-    SHCHK(hipMemsetAsync(w.sent, 0, nb * 4 + 4, st));
-    SHCHK(hipMemsetAsync(w.xdone, 0, nb * 4 + 4, st));
     if (nb == 0) return LZ4MT_RESULT_OK;
     // block checksums hashed beside the encode (k_xxh32_follow on a side
     // stream; `stream` waits for it, so the shard is complete on `stream`)

@@ -124,14 +124,17 @@ def gather_frame(frame, frame_len, dst=0, group=None, async_op=False):
             raise err
         raise ValueError(f"gather_frame: rank {lens.index(min(lens))} holds no valid -Sx shard frame")
     peer = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+    staged = _host_staged(group, dev)   # gloo: device bytes through pinned host copies
     if rank == dst:
         out = torch.empty(hdr + sum(lens) + 4, dtype=torch.uint8, device=dev)
-        ops, pos, mine = [], hdr, None
+        ops, pos, mine, land = [], hdr, None, []
         for r, n in enumerate(lens):
             if r == rank:
                 mine = (pos, n)
             elif n:
-                ops.append(dist.P2POp(dist.irecv, out[pos:pos + n], peer(r), group))
+                buf = torch.empty(n, dtype=torch.uint8, pin_memory=True) if staged else out[pos:pos + n]
+                land.append((pos, buf))
+                ops.append(dist.P2POp(dist.irecv, buf, peer(r), group))
             pos += n
         # receives first (their kernels then get the GPU before anything
         # launched after this call), then the local pieces, which touch
@@ -141,12 +144,20 @@ def gather_frame(frame, frame_len, dst=0, group=None, async_op=False):
         if mine and mine[1]:
             out[mine[0]:mine[0] + mine[1]] = frame[hdr:hdr + mine[1]]
         out[pos:pos + 4] = 0
-        if async_op:
+        if async_op and not staged:
             return out, works
         for w in works:
             w.wait()
-        return out
-    works = dist.batch_isend_irecv([dist.P2POp(dist.isend, frame[hdr:hdr + rec], peer(dst), group)]) if rec else []
+        if staged:
+            for p0, buf in land:
+                out[p0:p0 + buf.numel()].copy_(buf)
+        return (out, []) if async_op else out
+    payload = frame[hdr:hdr + rec].cpu() if staged and rec else frame[hdr:hdr + rec]
+    works = dist.batch_isend_irecv([dist.P2POp(dist.isend, payload, peer(dst), group)]) if rec else []
+    if staged:
+        for w in works:
+            w.wait()
+        works = []
     if async_op:
         return None, works
     for w in works:
@@ -220,7 +231,14 @@ def device_records(frame, frame_len=None):
     return hdr, starts
 
 
-def scatter_frame(frame, frame_len, src=0, group=None, records=None, async_op=False, device=None):
+def _host_staged(group, dev):
+    """gloo moves a CUDA tensor by reading it through the host's mapping of
+    device memory, ~24 MB/s here (profiles/r04_scatter_split.json): stage
+    such transfers through pinned host buffers instead."""
+    return dev.type == "cuda" and dist.get_backend(group) == "gloo"
+
+
+def scatter_frame(frame, frame_len, src=0, group=None, records=None, async_op=False, device=None, stats=None):
     """Cuts ONE -Sx frame held by ``src`` into per-rank sub-frames of whole
     records and delivers piece r to rank r (the decompress side of SURVEY.md
     §8(e): blocks are independent, src/lz4mt.cpp:914-918,991-995).
@@ -233,13 +251,18 @@ def scatter_frame(frame, frame_len, src=0, group=None, records=None, async_op=Fa
     (the source header, its records, EOS) -- the same split ``shard_blocks``
     makes of the content.  Exchange: one broadcast of the cut table
     (header + 2 x u64 per rank), then grouped sends root -> peers straight
-    into each peer's buffer.  Returns the piece (and the works with
-    ``async_op``).
+    into each peer's buffer (under gloo, device pieces travel through pinned
+    host copies).  Returns the piece (and the works with ``async_op``; host-
+    staged transfers are complete on return).  ``stats`` (dict), if given,
+    receives the host seconds of the walk, the table broadcast, the
+    point-to-point transfers and the piece assembly.
     """
+    import time
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     peer = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
     err = None
+    t0 = time.perf_counter()
     if rank == src:
         dev = frame.device
         table = torch.zeros(4 + 2 * world, dtype=torch.int64)
@@ -267,31 +290,57 @@ def scatter_frame(frame, frame_len, src=0, group=None, records=None, async_op=Fa
             dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
                 else torch.device("cpu")
         table = torch.zeros(4 + 2 * world, dtype=torch.int64, device=dev)
-    dist.broadcast(table, peer(src), group=group)
+    t1 = time.perf_counter()
+    staged = _host_staged(group, dev)
+    if staged:   # the table too: 8 B per rank through gloo's host path
+        tb = table.cpu()
+        dist.broadcast(tb, peer(src), group=group)
+        table = tb
+    else:
+        dist.broadcast(table, peer(src), group=group)
     if int(table[0].item()) < 0:   # the source rank could not cut the frame: all ranks raise together
         if err is not None:
             raise err
         raise ValueError(f"scatter_frame: rank {src} could not walk the frame")
     t = table.cpu().tolist()
+    t2 = time.perf_counter()
     hdr = int(t[0])
     head = torch.tensor(t[1:4], dtype=torch.int64).numpy().tobytes()[:hdr]
     off, ln = int(t[4 + 2 * rank]), int(t[5 + 2 * rank])
     piece = torch.empty(hdr + ln + 4, dtype=torch.uint8, device=dev)
-    works = []
+    works, landing = [], None
     if rank == src:
-        ops = [dist.P2POp(dist.isend, frame[int(t[4 + 2 * r]):int(t[4 + 2 * r]) + int(t[5 + 2 * r])], peer(r), group)
-               for r in range(world) if r != rank and int(t[5 + 2 * r])]
+        ops = []
+        for r in range(world):
+            a, b = int(t[4 + 2 * r]), int(t[5 + 2 * r])
+            if r == rank or not b:
+                continue
+            chunk = frame[a:a + b]
+            if staged:
+                chunk = chunk.to("cpu", non_blocking=False)
+            ops.append(dist.P2POp(dist.isend, chunk, peer(r), group))
         works = dist.batch_isend_irecv(ops) if ops else []
-        if ln:
-            piece[hdr:hdr + ln] = frame[off:off + ln]
     elif ln:
-        works = dist.batch_isend_irecv([dist.P2POp(dist.irecv, piece[hdr:hdr + ln], peer(src), group)])
+        landing = torch.empty(ln, dtype=torch.uint8, pin_memory=True) if staged else piece[hdr:hdr + ln]
+        works = dist.batch_isend_irecv([dist.P2POp(dist.irecv, landing, peer(src), group)])
+    if staged or not async_op:
+        for w in works:
+            w.wait()
+        works = []
+    t3 = time.perf_counter()
+    if rank == src and ln:
+        piece[hdr:hdr + ln] = frame[off:off + ln]
+    elif staged and ln:
+        piece[hdr:hdr + ln].copy_(landing)
     piece[:hdr] = torch.frombuffer(bytearray(head), dtype=torch.uint8).to(dev)
     piece[hdr + ln:] = 0
+    if stats is not None:
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        stats.update(walk_s=t1 - t0, table_s=t2 - t1, p2p_s=t3 - t2, assemble_s=time.perf_counter() - t3,
+                     host_staged=staged, piece_bytes=piece.numel())
     if async_op:
         return piece, works
-    for w in works:
-        w.wait()
     return piece
 
 
@@ -310,15 +359,20 @@ def _all_gather_var(t, group=None):
     return [b[:k] for b, k in zip(bufs, lens)]
 
 
-def verify_stitched(full, shard_src, decode, digests, dst=0, group=None):
+def verify_stitched(full, shard_src, decode, digests, dst=0, group=None, records=None):
     """Checks a stitched frame (on ``dst``) against every rank's source shard.
 
     Every rank passes its source ``shard_src`` (uint8 tensor); ``digests``
     maps a uint8 tensor to an int64 tensor of chunk digests (e.g. XXH32 of
-    16 MiB pieces, lz4mtHipXxh32Chunks); ``decode`` maps the stitched frame
-    to its content (root only).  The root decodes once, cuts the content at
-    the shard sizes and compares each piece's digests with the all-gathered
-    ones.  Returns True on every rank iff all shards match.
+    16 MiB pieces, lz4mtHipXxh32Chunks); ``decode`` maps a frame to its
+    content (root only).  The root walks the stitched frame's size words
+    (``records``: default the device walk for device tensors, the host walk
+    otherwise), cuts it at each shard's block range and decodes the pieces
+    one at a time (header + that shard's records + EOS: valid frames,
+    src/lz4mt.cpp:914-918), comparing each piece's content digests with the
+    all-gathered ones.  So the root holds one shard's content at a time, not
+    the whole stream's (64 GiB at configs[3]).  Returns True on every rank
+    iff every shard matches and the frame holds exactly their blocks.
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -329,16 +383,27 @@ def verify_stitched(full, shard_src, decode, digests, dst=0, group=None):
     err = None
     if rank == dst:
         try:
-            out = decode(full)
-            pos = 0
-            good = True
+            recs_fn = records or (device_records if full.is_cuda else host_records)
+            hdr, starts = recs_fn(full, full.numel())
+            head = full[:hdr]
+            bd = int(head[5].item())
+            bm = block_bytes((bd >> 4) & 7)
+            counts = [(int(sizes[r].item()) + bm - 1) // bm for r in range(world)]
+            good = sum(counts) == len(starts) - 1
+            first = 0
             for r in range(world):
+                if not good:
+                    break
                 n = int(sizes[r].item())
-                piece = out[pos:pos + n]
-                if piece.numel() != n or not torch.equal(digests(piece).to(torch.int64).cpu(), allsum[r].cpu()):
+                body = full[starts[first]:starts[first + counts[r]]]
+                first += counts[r]
+                piece = torch.cat([head, body, torch.zeros(4, dtype=torch.uint8, device=full.device)])
+                del body
+                out = decode(piece)
+                del piece
+                if out.numel() != n or not torch.equal(digests(out).to(torch.int64).cpu(), allsum[r].cpu()):
                     good = False
-                pos += n
-            good = good and pos == out.numel()
+                del out
             ok[0] = 1 if good else 0
         except Exception as e:   # still reach the broadcast, so no rank waits forever
             err = e
@@ -392,7 +457,12 @@ class HipShardEngine:
         return torch.empty(self.L.shard_pack_bound(n, sd, cap), dtype=torch.uint8, device=self.device)
 
     def encode(self, src, sd, ws):
-        self.enc_stream.wait_stream(torch.cuda.current_stream(self.device))   # src / ws ready
+        # the round state is zeroed on the CURRENT stream, which both the
+        # encode stream (here) and the pack stream (every pack) wait on: no
+        # pack can read `sent` / `pub` before the reset, and no reset can
+        # land after a pack wrote them
+        self.L.shard_reset(src.numel(), sd, ws, stream=torch.cuda.current_stream(self.device))
+        self.enc_stream.wait_stream(torch.cuda.current_stream(self.device))   # src / ws ready, ws reset
         self.enc_start = torch.cuda.Event(enable_timing=True)
         self.enc_done = torch.cuda.Event(enable_timing=True)
         self.enc_start.record(self.enc_stream)
@@ -463,6 +533,20 @@ class RcclTransport:
         self.recv = {}
 
 
+class IpcSetupError(RuntimeError):
+    """IpcPushTransport.setup failed on some rank; raised on EVERY rank (the
+    setup is collective), so the caller may fall back to another transport
+    together.  Any other error inside the rounds is not collective and must
+    end the process."""
+
+
+def peer_access_matrix():
+    """hipDeviceCanAccessPeer for every ordered pair of visible devices
+    (list of rows; True on the diagonal)."""
+    n = torch.cuda.device_count()
+    return [[i == j or bool(torch.cuda.can_device_access_peer(i, j)) for j in range(n)] for i in range(n)]
+
+
 class IpcPushTransport:
     """Each sender's pack goes straight into a receive buffer in the root's
     HBM, exported once by IPC handle (lz4mtHipIpcAlloc / lz4mtHipIpcOpen),
@@ -471,19 +555,35 @@ class IpcPushTransport:
     buffers per sender alternate, and the root finishes unpacking round k
     before it joins round k + 1's exchange, so a sender never overwrites a
     pack the root still reads.  Only the round's sizes go over the (gloo)
-    control group."""
+    control group.
+
+    The buffers are kept for the next call with the same layout (shard
+    sizes, descriptor, per-block cap, root); a call with another layout
+    tears them down and sets up again, on every rank alike (every rank sees
+    the same all-gathered layout).  A sender whose device cannot reach the
+    root's (hipDeviceCanAccessPeer) fails the setup on every rank."""
 
     def __init__(self, device):
         self.device = device
         self.bufs, self.remote, self.copy_stream = {}, [], None
+        self.key, self.cap_bytes = None, 0
+
+    @staticmethod
+    def _layout_key(sizes, sd, cap, dst):
+        return (tuple(sizes), bytes(sd), int(cap), int(dst))
 
     def setup(self, E, sizes, sd, cap, rank, dst, ctrl):
-        """Collective over ``ctrl``: every rank either sets up or raises."""
+        """Collective over ``ctrl``: every rank either sets up or raises IpcSetupError."""
         import lz4mt_amd as L
-        self.L, self.rank, self.dst = L, rank, dst
-        if self.bufs or self.remote:   # buffers of an earlier call with the same shapes
+        key = self._layout_key(sizes, sd, cap, dst)
+        if (self.bufs or self.remote) and key == self.key:   # an earlier call with this same layout
             return
+        if self.bufs or self.remote:   # another layout: every rank sees the same sizes, so all re-set up
+            self.close()
+        self.L, self.rank, self.dst = L, rank, dst
         handles, err = {}, None
+        # the root's device index, for the senders' peer-access check
+        root_dev = [self.device.index if rank == dst else -1]
         if rank == dst:
             try:
                 for r in range(len(sizes)):
@@ -494,37 +594,45 @@ class IpcPushTransport:
                     for _ in range(2):
                         ptr, h = ctypes.c_void_p(), (ctypes.c_uint8 * 64)()
                         if L.lib.lz4mtHipIpcAlloc(nbytes, ctypes.byref(ptr), h) != 0:
-                            raise RuntimeError("lz4mtHipIpcAlloc failed")
+                            raise IpcSetupError("lz4mtHipIpcAlloc failed")
                         pair.append(ptr.value)
                         handles.setdefault(r, []).append(bytes(h))
                     self.bufs[r] = pair
-            except RuntimeError as e:
+            except IpcSetupError as e:
                 err, handles = e, None
-        obj = [handles]
+        obj = [handles, root_dev[0]]
         dist.broadcast_object_list(obj, src=dst if ctrl is None else dist.get_global_rank(ctrl, dst), group=ctrl)
         ok = obj[0] is not None
         if ok and rank != dst:
             try:
+                rd = int(obj[1])
+                me = self.device.index if self.device.index is not None else torch.cuda.current_device()
+                if rd != me and not torch.cuda.can_device_access_peer(me, rd):
+                    raise IpcSetupError(f"device {me} cannot access the root's device {rd} (hipDeviceCanAccessPeer)")
+                self.cap_bytes = L.shard_pack_bound(sizes[rank], sd, cap)
                 for h in obj[0][rank]:
                     ptr = ctypes.c_void_p()
                     hb = (ctypes.c_uint8 * 64).from_buffer_copy(h)
                     if L.lib.lz4mtHipIpcOpen(hb, ctypes.byref(ptr)) != 0:
-                        raise RuntimeError("lz4mtHipIpcOpen failed")
+                        raise IpcSetupError("lz4mtHipIpcOpen failed")
                     self.remote.append(ptr.value)
                 self.copy_stream = torch.cuda.Stream(self.device)
-            except RuntimeError as e:
+            except IpcSetupError as e:
                 err, ok = e, False
         flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=ctrl)
         if int(flag.item()) == 0:
             self.close()
-            raise err or RuntimeError("IpcPushTransport: another rank could not set up its buffers")
+            raise err or IpcSetupError("IpcPushTransport: another rank could not set up its buffers")
+        self.key = key
 
     def push(self, k, buf, nbytes):
         if self.rank == self.dst or not nbytes:
             if self.rank == self.dst:   # round k - 1's unpacks are done before round k's exchange
                 torch.cuda.current_stream(self.device).synchronize()
             return
+        if nbytes > self.cap_bytes or nbytes > buf.numel():   # never write past the root's buffer
+            raise RuntimeError(f"IpcPushTransport: pack of {nbytes} B exceeds the root buffer ({self.cap_bytes} B)")
         st = self.copy_stream
         if self.L.lib.lz4mtHipCopyAsync(ctypes.c_void_p(self.remote[k % 2]), ctypes.c_void_p(buf.data_ptr()), nbytes,
                                         ctypes.c_void_p(st.cuda_stream)) != 0:
@@ -543,7 +651,23 @@ class IpcPushTransport:
         for pair in self.bufs.values():
             for p in pair:
                 self.L.lib.lz4mtHipFree(ctypes.c_void_p(p))
-        self.bufs, self.remote = {}, []
+        self.bufs, self.remote, self.key, self.cap_bytes = {}, [], None, 0
+
+
+_CTRL_GROUPS = {}
+
+
+def control_group(group=None):
+    """A gloo group over the ranks of ``group`` for the rounds' size
+    exchange (CPU tensors, no GPU kernel); ``group`` itself when it already
+    is gloo.  Made once per group (collective on first use)."""
+    if dist.get_backend(group) == "gloo":
+        return group
+    key = id(group) if group is not None else None
+    if key not in _CTRL_GROUPS:
+        ranks = dist.get_process_group_ranks(group) if group is not None else None
+        _CTRL_GROUPS[key] = dist.new_group(ranks=ranks, backend="gloo")
+    return _CTRL_GROUPS[key]
 
 
 def compress_gather_streamed(src, sd, dst=0, group=None, engine=None, per_block_cap=128 << 10, ws=None, stats=None,
@@ -571,7 +695,7 @@ def compress_gather_streamed(src, sd, dst=0, group=None, engine=None, per_block_
     While the encodes run, rounds start at least ``min_round_s`` apart.
     """
     import time
-    ctrl = ctrl if ctrl is not None else group
+    ctrl = ctrl if ctrl is not None else control_group(group)
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     E = engine or HipShardEngine(src.device)
@@ -581,6 +705,15 @@ def compress_gather_streamed(src, sd, dst=0, group=None, engine=None, per_block_
     alln = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
     dist.all_gather(alln, torch.tensor([n], dtype=torch.int64), group=ctrl)
     sizes = [int(x.item()) for x in alln]
+    # the stitched frame is the whole stream's only if every shard but the
+    # last non-empty one is a whole number of blocks (every rank sees the
+    # same sizes, so every rank raises here together)
+    bm = block_bytes(sd.bd.blockMaximumSize)
+    last = max([r for r in range(world) if sizes[r]] or [0])
+    bad = [r for r in range(last) if sizes[r] % bm]
+    if bad:
+        raise ValueError(f"compress_gather_streamed: shard(s) {bad} are not whole {bm}-byte blocks "
+                         "and are followed by another shard (use shard_blocks)")
     ws = ws if ws is not None else E.workspace(n, sd)
     T.setup(E, sizes, sd, per_block_cap, rank, dst, ctrl)
     E.encode(src, sd, ws)

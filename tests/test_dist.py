@@ -129,6 +129,14 @@ def _digests(t, chunk=1 << 16):
                         dtype=torch.int64)
 
 
+def _oracle_decode(cap):
+    """A frame (CPU uint8 tensor) -> its content (the stitched frame's per-shard pieces in verify_stitched)."""
+    def dec(f):
+        out = oracle.decompress_frame(f.numpy().tobytes(), cap)[1]
+        return torch.frombuffer(bytearray(out) or bytearray(1), dtype=torch.uint8)[:len(out)]
+    return dec
+
+
 def _roundtrip_worker(rank, world, port, n, block_id, q, corrupt_rank=None):
     """bench.py's N > 1 step on the CPU: local frame -> gather to root ->
     verify the stitched frame against every shard -> scatter it back ->
@@ -147,9 +155,7 @@ def _roundtrip_worker(rank, world, port, n, block_id, q, corrupt_rank=None):
         if rank == corrupt_rank and src:
             src[len(src) // 2] ^= 1
         ok = D.verify_stitched(full, torch.frombuffer(src, dtype=torch.uint8) if src else torch.zeros(0, dtype=torch.uint8),
-                               decode=lambda f: torch.frombuffer(bytearray(
-                                   oracle.decompress_frame(f.numpy().tobytes(), n + bm)[1]) or bytearray(1),
-                                   dtype=torch.uint8)[:n],
+                               decode=_oracle_decode(n + bm),
                                digests=_digests)
         piece = D.scatter_frame(full if rank == 0 else None, full.numel() if rank == 0 else 0)
         rc, dec = oracle.decompress_frame(piece.numpy().tobytes(), ln + bm)
@@ -439,3 +445,52 @@ def test_streamed_gather_stitches_whole_stream_frame(world, n, block_id, bck, ki
     want = oracle.compress_frame(_stream_input(n, kind), oracle.params(block_id, False, bck))
     assert rounds > world + 1
     assert got == want
+
+
+def _layout_worker(rank, world, port, q):
+    """A shard that is not a whole number of blocks, followed by another
+    shard: the stitched frame would not be the whole stream's, so EVERY
+    rank raises, none waits in a round."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import lz4mt_amd as L
+        bm = D.block_bytes(4)
+        ln = bm + 100 if rank == 0 else 2 * bm
+        sd = L.make_sd(4, stream_checksum=False, block_checksum=True)
+        eng = MockShardEngine(rank, 4, 2)
+        try:
+            D.compress_gather_streamed(torch.frombuffer(bytearray(oracle.gen_synthetic(ln, 3)), dtype=torch.uint8),
+                                       sd, engine=eng, min_round_s=0.0)
+            q.put((rank, "no error"))
+        except ValueError as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_streamed_gather_rejects_ragged_inner_shard():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_layout_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all("not whole" in m for _, m in res), res
+
+
+def test_ipc_layout_key_tracks_every_field():
+    """IpcPushTransport keeps its buffers only for the same shard sizes,
+    descriptor, per-block cap and root."""
+    import lz4mt_amd as L
+    sd6, sd7 = L.make_sd(6, False, True), L.make_sd(7, False, True)
+    k = D.IpcPushTransport._layout_key
+    base = k([8 << 20, 8 << 20], sd7, 1 << 17, 0)
+    assert base == k([8 << 20, 8 << 20], L.make_sd(7, False, True), 1 << 17, 0)
+    for other in (k([8 << 20, 12 << 20], sd7, 1 << 17, 0), k([8 << 20, 8 << 20], sd6, 1 << 17, 0),
+                  k([8 << 20, 8 << 20], sd7, 1 << 16, 0), k([8 << 20, 8 << 20], sd7, 1 << 17, 1)):
+        assert other != base

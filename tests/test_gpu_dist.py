@@ -78,24 +78,38 @@ def _streamed_rank(rank, world, port, n, bid, cap, kind, q):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        data = bytearray(oracle.gen_synthetic(n, 42))
-        rnd = oracle.gen_random(n, 5)
-        for s in range(0, n, 5 << 20):
-            data[s:s + 1_200_000] = rnd[s:s + 1_200_000]
+        def make(n, seed):
+            data = bytearray(oracle.gen_synthetic(n, seed))
+            rnd = oracle.gen_random(n, seed + 5)
+            for s in range(0, n, 5 << 20):
+                data[s:s + 1_200_000] = rnd[s:s + 1_200_000]
+            return data
+
         bm = 1 << (8 + 2 * bid)
-        off, ln, _, _ = D.shard_blocks(n, bm, world, rank)
-        src = torch.frombuffer(bytearray(data[off:off + ln]), dtype=torch.uint8).cuda()
         sd = L.make_sd(bid, stream_checksum=False, block_checksum=True)
         st = {}
         tr = D.IpcPushTransport(torch.device("cuda", 0)) if kind == "ipc" else D.RcclTransport()
-        full = None
-        for _ in range(2):   # twice: the IPC buffers are set up once and reused
+        eng = D.HipShardEngine(torch.device("cuda", 0))
+        results = []
+        ws = None
+        # three calls on one engine and transport: the same layout twice with
+        # DIFFERENT inputs into ONE reused workspace (its round state must be
+        # reset before the packs read it; the IPC buffers are reused), then a
+        # shorter stream (another layout: the IPC buffers are set up again)
+        for total, seed in ((n, 42), (n, 7), (n - 3 * bm, 11)):
+            data = make(total, seed)
+            off, ln, _, _ = D.shard_blocks(total, bm, world, rank)
+            src = torch.frombuffer(bytearray(data[off:off + ln]), dtype=torch.uint8).cuda()
+            if ws is None or total != n:
+                ws = L.shard_workspace(ln, sd)
             full = D.compress_gather_streamed(src, sd, per_block_cap=cap, stats=st, min_round_s=0.0005,
-                                              transport=tr)
+                                              transport=tr, engine=eng, ws=ws)
+            if rank == 0:
+                want = L.compress_frame(torch.frombuffer(data, dtype=torch.uint8).cuda(), sd)
+                results.append(full.numel() == want.numel() and bool(torch.equal(full, want)))
         tr.close()
         if rank == 0:
-            want = L.compress_frame(torch.frombuffer(data, dtype=torch.uint8).cuda(), sd)
-            q.put((full.numel() == want.numel() and bool(torch.equal(full, want)), st["rounds"], full.numel()))
+            q.put((all(results), st["rounds"], results))
     finally:
         dist.destroy_process_group()
 
@@ -123,11 +137,11 @@ def test_streamed_gather_on_device(n, bid, cap, kind):
     procs = [ctx.Process(target=_streamed_rank, args=(r, 2, port, n, bid, cap, kind, q)) for r in range(2)]
     for p in procs:
         p.start()
-    same, rounds, size = q.get(timeout=240)
+    same, rounds, each = q.get(timeout=300)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert same, (rounds, size)
+    assert same, (rounds, each)
     assert rounds >= 2
 
 
@@ -143,3 +157,79 @@ def test_bench_gpus3_strong_uneven_1mib_blocks():
     assert line["config"]["bytes_total"] == 1 << 28 and line["config"]["block_bytes"] == 1 << 20
     assert line["gather"].startswith("streamed") and "ipc" in line["gather"]
     assert line["stitched_frame_ok"] is True and line["roundtrip_ok"] is True
+
+
+def _nccl_world1(q, n, bid):
+    """World size 1 over the nccl backend (RCCL allows one rank per device, so
+    this is the most a one-GPU box can run): the whole N > 1 code path --
+    control group, IPC transport setup, streamed gather, the device-walk
+    scatter, the shard-by-shard stitched check -- on the device."""
+    import torch.distributed as dist
+
+    from lz4mt_amd import dist as D
+    import lz4mt_amd as L
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
+    try:
+        sd = L.make_sd(bid, stream_checksum=False, block_checksum=True)
+        src = L.gen_synthetic(n, seed=3)
+        tr = D.IpcPushTransport(dev)
+        st, sst = {}, {}
+        full = D.compress_gather_streamed(src, sd, stats=st, transport=tr)
+        tr.close()
+        want = L.compress_frame(src, sd)
+        same = full.numel() == want.numel() and bool(torch.equal(full, want))
+        piece = D.scatter_frame(full, full.numel(), stats=sst)
+        out, r = L.decompress_frame(piece)
+        ok = D.verify_stitched(full, src, lambda f: L.decompress_frame(f)[0],
+                               lambda t: L.xxh32_chunks(t, 1 << 20).to(torch.int64))
+        q.put((dist.get_backend(), same, r == 0 and bool(torch.equal(out, src)), ok, sst.get("host_staged")))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_nccl_world1_streamed_gather_scatter_verify():
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_world1, args=(q, (40 << 20) + 4099, 7))
+    p.start()
+    backend, same, dec_ok, ok, staged = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert backend == "nccl" and same and dec_ok and ok and staged is False
+
+
+@pytest.mark.gpu
+def test_bench_nccl_world1_distributed_path():
+    """bench.py under torch.distributed.run with one rank, backend nccl set
+    explicitly and the N > 1 path forced (LZ4MT_BENCH_DIST=1): the line
+    reports the backend, the transport, the root's memory and the
+    peer-access matrix, and every check passes."""
+    env = dict(os.environ, LZ4MT_BENCH_BACKEND="nccl", LZ4MT_BENCH_DIST="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "1", "--gib", "0.25", "--steps", "1", "--warmup", "1", "--no-cpu-baseline"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    line = json.loads(lines[0])
+    assert line["backend"] == "nccl" and line["transport"] == "ipc"
+    assert line["stitched_frame_ok"] is True and line["roundtrip_ok"] is True
+    assert line["gather"].startswith("streamed")
+    assert line["root_memory"]["max_allocated_GiB"] > 0.25 and line["peer_access"][0][0] is True
+    assert line["scatter_split_ms"]["host_staged"] is False

@@ -8,6 +8,7 @@
 #   trace   rocprofv3 kernel-trace stats of a 5-step bench run
 #   sq      SQ counters of the encoder / decoder (tools/kprof.py 2) + the window count (tools/kstats.py 2)
 #   pmc     FETCH_SIZE / WRITE_SIZE passes (tools/prof.sh without its trace)
+#   pmcbid  the same on App. F at block ids 4, 5, 6 (the configs[4] sweep: profiles/pmc_b<id>.json)
 #   dist2   bench.py --gpus 2 over gloo on this one GPU (rehearsal of the N > 1 path)
 #   fcal    FETCH_SIZE calibration on a known byte count (tools/fetch_cal.py + fetchcal_sum.py)
 #   tail    the streamed gather's exposed tail on one GPU (tools/tail_model.py)
@@ -51,6 +52,14 @@ for step in "$@"; do
             python3 tools/kprof.py 8 $flag > "$out/fetch_$input.log" 2>&1
         timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -T -f csv -d "$out/write_$input" -o write -- \
             python3 tools/kprof.py 8 $flag > "$out/write_$input.log" 2>&1
+      done ;;
+    pmcbid)
+      for bid in 4 5 6; do
+        mkdir -p "$out/bid$bid"
+        timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -T -f csv -d "$out/bid$bid/fetch_appf" -o fetch -- \
+            python3 tools/kprof.py 8 --bid=$bid > "$out/bid$bid/fetch.log" 2>&1
+        timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -T -f csv -d "$out/bid$bid/write_appf" -o write -- \
+            python3 tools/kprof.py 8 --bid=$bid > "$out/bid$bid/write.log" 2>&1
       done ;;
     dist2)
       LZ4MT_BENCH_BACKEND=gloo timeout -k 10 400 python3 bench.py --gpus 2 --gib 0.5 --steps 2 --warmup 1 \

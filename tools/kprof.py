@@ -1,4 +1,5 @@
-"""One compress + decompress of N GiB (default 8) for PMC profiling.
+"""One compress + decompress of N GiB (default 8) for PMC profiling
+(--bid K: block maximum size id K, default 7 = 4 MiB).
 --random: splitmix64 bytes instead of App. F (every block stored raw): the
 encoder then streams its source exactly once and the decoder copies raw
 blocks, so FETCH_SIZE of those launches is measured against a known byte
@@ -19,7 +20,8 @@ if "--random" in sys.argv:
     src = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
 else:
     src = L.gen_synthetic(n)
-sd = L.make_sd(7, False, True)
+bid = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--bid=")), 7))
+sd = L.make_sd(bid, False, True)
 fr = L.compress_frame(src, sd)
 out, r = L.decompress_frame(fr)
 torch.cuda.synchronize()

@@ -9,7 +9,10 @@ Calibration: FETCH_SIZE / bytes of a kernel that reads a known byte count
 exactly once at the load widths these kernels use (tools/fetch_cal.py,
 summarised by tools/fetchcal_sum.py into the json given as the third
 argument); bench.py divides each kernel's FETCH_SIZE by that factor.
-usage: python tools/pmcsum.py <gpu_round dir> <tag> [fcal_summary.json] [--current]"""
+With --bid=K (K != 7) the profile is the configs[4] sweep point of block id
+K (appf runs only): profiles/pmc_b<K>.json, its encoder kernel
+(k_encode16 at 64 KiB, k_encode_p17 at 256 KiB) calibrated like k_encode.
+usage: python tools/pmcsum.py <gpu_round dir> <tag> [fcal_summary.json] [--current] [--bid=K]"""
 import csv
 import glob
 import json
@@ -34,7 +37,9 @@ def counters(run):
                 "max_ns": max(e["ns"])} for k, e in out.items()}
 
 
-appf, rnd = counters("appf"), counters("random")
+bid = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--bid=")), 7))
+appf = counters("appf")
+rnd = counters("random") if bid == 7 else {}
 for k in appf.values():
     k["traffic_raw"] = k["fetch_bytes"] + k["write_bytes"]
 stats = glob.glob(f"{src}/trace/*kernel_stats.csv")
@@ -53,6 +58,7 @@ if stats:
 # coverage, not a counter factor.
 cal = {}
 fc_path = sys.argv[3] if len(sys.argv) > 3 and not sys.argv[3].startswith("--") else None
+enc_kernels = ("k_encode", "k_encode16", "k_encode_p17", "k_decode")
 fc = json.load(open(fc_path)) if fc_path else None
 if fc:
     facs = {w: v["factor"] for w, v in fc["widths"].items() if v["factor"]}
@@ -60,7 +66,7 @@ if fc:
     how = ("FETCH_SIZE / bytes read by k_fetch_cal (8 GiB read exactly once; tools/fetch_cal.py) per load width: " +
            ", ".join(f"{w.split('_')[1]} B {f}" for w, f in sorted(facs.items(), key=lambda x: int(x[0].split('_')[1]))) +
            f"; implied rates <= {fc['achievable_Bps'] / 1e12:.1f} TB/s")
-    for k in ("k_encode", "k_decode"):
+    for k in enc_kernels:
         cal[k] = {"fetch_factor": (f_lo + f_hi) / 2, "fetch_factor_range": [f_lo, f_hi], "how": how,
                   "source": fc_path}
 if "k_encode" in rnd:
@@ -68,11 +74,13 @@ if "k_encode" in rnd:
         "fetch_raw": rnd["k_encode"]["fetch_bytes"], "bytes": N,
         "note": "k_encode over 8 GiB of random bytes (every block raw): FETCH_SIZE / n, the probe coverage times "
                 "the counter factor -- not a calibration"}
-res = {"tag": tag, "config": {"bytes": N, "block_bytes": 4 << 20, "flg": 0x70,
-                              "workload": "tools/kprof.py 8: 8 GiB App. F synthetic, 4 MiB blocks, -Sx -BX"},
+bm = 1 << (8 + 2 * bid)
+res = {"tag": tag, "config": {"bytes": N, "block_bytes": bm, "flg": 0x70,
+                              "workload": f"tools/kprof.py 8 --bid={bid}: 8 GiB App. F synthetic, {bm >> 10} KiB "
+                                          "blocks, -Sx -BX"},
        "kernels": appf, "calibration": cal, "random_input": rnd}
-json.dump(res, open(f"profiles/{tag}_pmc.json", "w"), indent=1)
+json.dump(res, open(f"profiles/{tag}_pmc.json" if bid == 7 else f"profiles/pmc_b{bid}.json", "w"), indent=1)
 if "--current" in sys.argv:
     json.dump(res, open("profiles/pmc_current.json", "w"), indent=1)
-print(json.dumps({"kernels": {k: appf[k] for k in ("k_encode", "k_decode") if k in appf}, "calibration": cal},
+print(json.dumps({"kernels": {k: appf[k] for k in enc_kernels if k in appf}, "calibration": cal},
                  indent=1))

@@ -42,6 +42,7 @@ def ms(fn):
     return (time.perf_counter() - t) * 1e3, r
 
 
+L.shard_reset(n, sd, ws)
 t_enc, _ = ms(lambda: L.shard_encode(src, sd, ws))
 # everything published during the encode (cap = the block size: one round)
 _, _ = ms(lambda: L.shard_pack(src, sd, ws, pack, 4 << 20, False))
