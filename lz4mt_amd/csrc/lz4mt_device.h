@@ -30,8 +30,11 @@ struct BlockRec {
 // (see k_encode_linked): catch-up lower bounds for candidates in the block /
 // in the history and the dictSmall limit, in coordinates where the block
 // starts at 65536 and its 64 KiB history is [0, 65536).
+// shift: where the history bytes stand (BdSim): 0 = the 64 KiB before the
+// block; else position p < 65536 reads the block's own byte p - 65536 + shift
+// (the reference's 1 / 4 MiB buffer, LZ4MT_AMD_BD_REFERENCE=1).
 struct LinkPlan {
-    uint32_t lowIn, lowDict, candLow, pad;
+    uint32_t lowIn, lowDict, candLow, shift;
 };
 
 // Device state of a block-dependent encode: per-block plans, the carried table.
@@ -44,6 +47,7 @@ struct LinkState {
     const uint8_t* hcSegs = nullptr;
     uint32_t nSeg = 0;
     bool hcPerBlock = false;   // every block starts its own segment (1 / 4 MiB blocks)
+    bool xh = false;           // some plan has a shift: the encoder variant that reads such histories
 };
 
 // Frame-walk summary written by the walk kernel.
@@ -148,7 +152,7 @@ hipError_t launch_encode_hc_bd(const uint8_t* src, uint64_t srcSize, uint32_t bl
                                uint8_t* slots, const int64_t* segBegin, const int64_t* segEnd, uint32_t nSeg,
                                const uint32_t* blockSeg, uint16_t* delta0, int32_t* csize, hipStream_t st);
 hipError_t launch_encode_linked(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
-                                uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh, int32_t* csize,
+                                uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh, bool xh, int32_t* csize,
                                 hipStream_t st);
 // The block-dependent encode as parallel fixed-point rounds
 // (k_encode_linked_round / k_link_settle; the serial kernel finishes from
@@ -156,7 +160,7 @@ hipError_t launch_encode_linked(const uint8_t* src, uint64_t srcSize, uint32_t b
 constexpr int kLinkRounds = 32;
 uint64_t link_round_bytes(uint64_t nBlocks);   // scratch: entry + exit tables, round control words
 hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
-                                    uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh,
+                                    uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh, bool xh,
                                     uint32_t* scratch, int32_t* csize, int rounds, hipStream_t st);
 hipError_t launch_decode_linked(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax,
                                 uint8_t* out, uint64_t outCap, uint8_t* slot, uint8_t* hist, const uint32_t* digest,
@@ -170,6 +174,14 @@ uint64_t dlink_scratch_bytes(uint64_t nBlocks, uint32_t blockMax);
 inline int env_rounds() {
     const char* e = getenv("LZ4MT_AMD_BD_ROUNDS");
     return e ? atoi(e) : kLinkRounds;
+}
+// LZ4MT_AMD_BD_REFERENCE=1: -BD frames with 1 and 4 MiB blocks written byte
+// for byte as the reference writes them (its input buffer replayed by BdSim:
+// each block after the first read over its own dictionary, frames that do
+// not decode back -- DESIGN.md §1).  Off by default: the decodable stream.
+inline bool bd_reference_bytes() {
+    const char* e = getenv("LZ4MT_AMD_BD_REFERENCE");
+    return e && e[0] == '1';
 }
 // LZ4MT_AMD_BD_SERIAL=1: the one-wave -BD kernels only (A/B and tests)
 inline bool bd_serial() {

@@ -391,10 +391,10 @@ Lz4MtResult device_compress_body(const uint8_t* src, uint64_t n, uint32_t bm, in
                                    st));
     } else if (link && link->rounds && !bd_serial())   // block-dependent: parallel rounds (exact; serial fallback)
         HIPCHK(launch_encode_linked_par(src, n, bm, (uint32_t)nb, w.slots, link->plan, link->table, link->fresh,
-                                        link->rounds, w.csize, env_rounds(), st));
+                                        link->xh, link->rounds, w.csize, env_rounds(), st));
     else if (link)             // block-dependent frame: one wave, blocks in order (k_encode_linked)
-        HIPCHK(launch_encode_linked(src, n, bm, (uint32_t)nb, w.slots, link->plan, link->table, link->fresh, w.csize,
-                                    st));
+        HIPCHK(launch_encode_linked(src, n, bm, (uint32_t)nb, w.slots, link->plan, link->table, link->fresh,
+                                    link->xh, w.csize, st));
     else if (level >= 3)   // LZ4-HC, a wave per block (lz4mt_hc.hip)
         HIPCHK(launch_encode_hc(src, n, bm, (uint32_t)nb, w.slots, bm, 0xFFFFFFFFu, level, w.delta, w.csize, st,
                                 w.hcSplit));
@@ -622,12 +622,18 @@ static Lz4MtResult compress_frame_impl(const void* d_src, uint64_t srcSize, void
     } else if (bdk == 1) {
         const uint64_t nb = (srcSize + bm - 1) / bm;
         std::vector<LinkPlan> hplan(std::max<uint64_t>(nb, 1), LinkPlan{});
-        BdSim sim(sd->bd.blockMaximumSize);
-        for (uint64_t b = 0; b < nb; ++b)
+        const bool refBytes = bd_reference_bytes();
+        BdSim sim(sd->bd.blockMaximumSize, refBytes);
+        bool xh = false;
+        for (uint64_t b = 0; b < nb; ++b) {
             sim.next((uint32_t)std::min<uint64_t>(bm, srcSize - b * bm), &hplan[b].lowIn, &hplan[b].lowDict,
-                     &hplan[b].candLow);
+                     &hplan[b].candLow, refBytes ? &hplan[b].shift : nullptr);
+            xh = xh || hplan[b].shift != 0;
+        }
+        if (sim.bad) return LZ4MT_RESULT_ERROR;
         HIPCHK(hipMemcpyAsync(w.bdPlan, hplan.data(), hplan.size() * sizeof(LinkPlan), hipMemcpyHostToDevice, st));
         ls = LinkState{reinterpret_cast<LinkPlan*>(w.bdPlan), w.bdTable, true, w.bdRounds};
+        ls.xh = xh;
         lsp = &ls;
     }
     const Lz4MtResult r = device_compress_body(static_cast<const uint8_t*>(d_src), srcSize, bm, sd->flg.blockChecksum,

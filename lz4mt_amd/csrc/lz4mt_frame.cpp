@@ -527,7 +527,8 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
     const uint64_t pre = linked ? 65536 : 0;
     PipeShape P = pipe_shape(true);
     if (linked) P.slots = 1;
-    BdSim sim(sd->bd.blockMaximumSize);
+    const bool refBytes = linked && bd_reference_bytes();
+    BdSim sim(sd->bd.blockMaximumSize, refBytes);
     HcBdSim hsim(sd->bd.blockMaximumSize);   // level >= 3
     std::vector<uint8_t> hist(linked ? 65536 : 0, 0);
     std::vector<LinkPlan> plan;
@@ -576,9 +577,14 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
         } else if (linked) {
             memcpy(S.hIn, hist.data(), 65536);
             plan.resize(nb);
-            for (uint64_t b = 0; b < nb; ++b)
+            bool xh = false;
+            for (uint64_t b = 0; b < nb; ++b) {
+                plan[b].shift = 0;
                 sim.next((uint32_t)std::min<uint64_t>(bm, total - b * bm), &plan[b].lowIn, &plan[b].lowDict,
-                         &plan[b].candLow);
+                         &plan[b].candLow, refBytes ? &plan[b].shift : nullptr);
+                xh = xh || plan[b].shift != 0;
+            }
+            if (sim.bad) { s.quit(LZ4MT_RESULT_ERROR); return false; }
             if (nb > planCap) {
                 if (dplan.p) { hipStreamSynchronize(S.st); hipFree(dplan.p); dplan.p = nullptr; }
                 if (!dplan.alloc(nb * sizeof(LinkPlan))) { s.quit(LZ4MT_RESULT_ERROR); return false; }
@@ -596,6 +602,7 @@ void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
             }
             ls = LinkState{static_cast<LinkPlan*>(dplan.p), static_cast<uint32_t*>(table.p), batch == 1,
                            static_cast<uint32_t*>(rounds.p)};
+            ls.xh = xh;
         }
         if (linked) {   // the history of the next batch: the last 64 KiB of (hist ++ this input)
             if (total >= 65536) memcpy(hist.data(), in + total - 65536, 65536);

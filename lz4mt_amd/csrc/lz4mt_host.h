@@ -182,16 +182,25 @@ inline Lz4MtResult parse_header(const uint8_t* p, size_t avail, Lz4MtStreamDescr
 // same stream without that defect.
 // next() returns the block's catch-up bounds and dictSmall limit in the
 // coordinates of k_encode_linked (block at 65536, history below).
+// refBuffer: replay the reference's input buffer for 1 and 4 MiB blocks too
+// (LZ4MT_AMD_BD_REFERENCE=1).  There lz4 1.9.3's LZ4_slideInputBuffer hands
+// back the dictionary's own address, so from the second block on each full
+// block is read over its dictionary: its "history" is its own last 64 KiB
+// (the table still indexes the previous block).  `shift` then says where a
+// history byte lives: position p < 65536 (block coordinates) reads the
+// block's byte p - 65536 + shift; 0 = the true history before the block.
+// bad: a history that is partly the block and partly older bytes (no such
+// case in the reference's loop; refused rather than guessed).
 struct BdSim {
     uint64_t bm = 0, bufSize = 0;   // bufSize 0: one contiguous buffer
     uint64_t inStart = 0, dict = 0, dictSize = 0, cur = 0;
-    bool dictNull = true;
-    explicit BdSim(int blockMaxId) {
+    bool dictNull = true, bad = false;
+    explicit BdSim(int blockMaxId, bool refBuffer = false) {
         bm = (uint64_t)1 << (8 + 2 * blockMaxId);
         const uint64_t b = bm + 65536, m = (1024 + 64) * 1024;
-        bufSize = blockMaxId <= 5 ? (b > m ? b : m) : 0;
+        bufSize = (blockMaxId <= 5 || refBuffer) ? (b > m ? b : m) : 0;
     }
-    void next(uint32_t n, uint32_t* lowIn, uint32_t* lowDict, uint32_t* candLow) {
+    void next(uint32_t n, uint32_t* lowIn, uint32_t* lowDict, uint32_t* candLow, uint32_t* shift = nullptr) {
         if (bufSize && inStart + bm > bufSize) inStart = dict;   // translate()
         uint64_t dictEnd = dict + dictSize;
         if (cur + n > 0x80000000ull) {                           // LZ4_renormDictT
@@ -215,6 +224,12 @@ struct BdSim {
         *lowDict = 65536 - ds;
         *lowIn = prefix ? 65536 - ds : 65536;
         *candLow = small ? 65536 - ds : 0;
+        if (shift) {   // where the ds history bytes [dictEnd - ds, dictEnd) of the buffer stand
+            *shift = 0;
+            const uint64_t h0 = dict + dictSize - ds, h1 = dict + dictSize;
+            if (!prefix && ds && h0 >= inStart && h1 <= inStart + n) *shift = (uint32_t)(h1 - inStart);
+            else if (!prefix && ds && h0 < inStart + n && h1 > inStart) bad = true;
+        }
         cur += n;
         if (prefix) dictSize += n;
         else { dict = inStart; dictSize = n; dictNull = false; }

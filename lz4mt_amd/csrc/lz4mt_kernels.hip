@@ -344,9 +344,12 @@ __device__ __forceinline__ void put_head(OutView& O, uint32_t op, uint32_t lit, 
 //   candLow          dictSmall: candidates below it are out of the valid area
 //   fresh            a new stream: the table starts at the block's position 0
 constexpr uint32_t kLinkO0 = 65536;
+//   shift            (LZ4MT_AMD_BD_REFERENCE) history position p reads the
+//                    block's own byte p - kLinkO0 + shift (LinkPlan.shift)
 struct LinkArgs {
     uint32_t lowIn, lowDict, candLow;
     bool fresh;
+    uint32_t shift = 0;
 };
 
 template <bool U16, bool TAG, bool ST, bool LINK = false>
@@ -848,7 +851,13 @@ __device__ __forceinline__ void publish_progress(uint32_t* pub, uint32_t v) {
     if (laneid() == 0) __hip_atomic_store(pub, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool ST, bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false, bool PUB = false>
+// XH (LINK only): the history below o0 is the block's own bytes at
+// p - o0 + lk.shift (the reference's -BD buffer with 1 / 4 MiB blocks,
+// LZ4MT_AMD_BD_REFERENCE): every candidate-side load goes through xld4 /
+// xld1, and the carried entries' tags are recomputed from the bytes those
+// positions now hold (lz4 compares the memory as it is, not as it was).
+template <bool ST, bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false, bool PUB = false,
+          bool XH = false>
 __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
                                    l_u32* __restrict__ T, l_u8* __restrict__ R, uint64_t* acc,
                                    LinkArgs lk = LinkArgs{0, 0, 0, true}, uint32_t* pub = nullptr) {
@@ -857,6 +866,25 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     const uint32_t L = laneid();
     uint64_t ts = STAMP_T();
     const uint32_t o0 = LINK ? kLinkO0 : 0u;   // position of the block's first byte
+    // candidate-side loads (a candidate may lie in the history)
+    auto xld4 = [&](uint32_t pos) -> uint32_t {
+        if constexpr (!XH) {
+            return gld4u(s + pos);
+        } else {
+            if (pos >= o0) return gld4u(s + pos);
+            if (pos + 4 <= o0) return gld4u(s + pos + lk.shift);
+            uint32_t v = 0;   // straddles the history's end: the rest is the block's start
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t q = pos + j;
+                v |= (uint32_t)s[q < o0 ? q + lk.shift : q] << (8 * j);
+            }
+            return v;
+        }
+    };
+    auto xld1 = [&](uint32_t pos) -> uint32_t {
+        if constexpr (!XH) return s[pos];
+        else return s[pos < o0 ? pos + lk.shift : pos];
+    };
     const uint32_t blen = n - o0;
     const uint32_t bound = blen + blen / 255 + 16;
     const bool limited = cap < bound;
@@ -869,6 +897,15 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     if (!LINK || lk.fresh) {
         // a fresh entry is the block's position 0 -- a real candidate in LZ4 1.9.3
         tab.init(o0 | (G::tag(gld4u(s + o0)) << G::PB));
+    }
+    if constexpr (XH) {
+        if (!lk.fresh && lk.shift) {   // history entries: the tag of the bytes they point at now
+            for (uint32_t i = L; i < G::kTE; i += 64) {
+                const uint32_t e = tab.ld(i), pos = e & G::PM;
+                if (pos != 0 && pos < o0) tab.st(i, pos | (G::tag(xld4(pos)) << G::PB));
+            }
+            WAVE_SYNC();
+        }
     }
     SrcRing V{s, n, R, 0, 0, 0};
     V.init(o0);
@@ -1028,10 +1065,10 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                         bi = V.r[(bOn ? ip - L - 1 : ip - 1) & (kSR - 1)];
                         bc = V.r[(bOn ? cd - L - 1 : cd - 1) & (kSR - 1)];
                     } else {
-                        cw = gld4u(s + (ci < last4 ? ci : last4));
+                        cw = xld4(ci < last4 ? ci : last4);
                         iw = gld4u(s + (ii < last4 ? ii : last4));
                         bi = s[bOn ? ip - L - 1 : o0];   // (o0: a byte of the block itself)
-                        bc = s[bOn ? cd - L - 1 : o0];
+                        bc = xld1(bOn ? cd - L - 1 : o0);
                     }
                     if (havePe) {
                         store_pend(pe, V, s, d);
@@ -1081,13 +1118,13 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                 back = kCatchLanes;
                 const uint32_t kb = back + L + 1;
                 const bool on = kb <= maxb;
-                fm = ~bal(on && s[on ? ip - kb : o0] == s[on ? cd - kb : o0]);
+                fm = ~bal(on && s[on ? ip - kb : o0] == xld1(on ? cd - kb : o0));
             }
             while (fm == 0 && back + 64 < maxb) {   // catch-up longer than 64 bytes
                 back += 64;
                 const uint32_t kb = back + L + 1;
                 const bool on = kb <= maxb;
-                fm = ~bal(on && s[on ? ip - kb : o0] == s[on ? cd - kb : o0]);
+                fm = ~bal(on && s[on ? ip - kb : o0] == xld1(on ? cd - kb : o0));
             }
             back = fm ? back + (uint32_t)__builtin_ctzll(fm) : maxb;
             const uint32_t lim = matchlimit - (ip + kMinMatch);
@@ -1107,8 +1144,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                     while (!nf2) {   // long match: 256 bytes per round
                         const uint32_t r2 = mc + 4 * L;
                         const uint32_t a2 = ip + kMinMatch + r2, c2 = cd + kMinMatch + r2;
-                        const uint32_t x2 =
-                            gld4u(s + (a2 < last4 ? a2 : last4)) ^ gld4u(s + (c2 < last4 ? c2 : last4));
+                        const uint32_t x2 = gld4u(s + (a2 < last4 ? a2 : last4)) ^ xld4(c2 < last4 ? c2 : last4);
                         uint32_t e2 = min(x2 ? ((uint32_t)__builtin_ctz(x2) >> 3) : 4u, lim - r2);
                         e2 = r2 < lim ? e2 : 0u;
                         nf2 = bal(e2 < 4);
@@ -1328,6 +1364,7 @@ __device__ __forceinline__ uint32_t link_rebase(uint32_t e, uint32_t n) {
 // the table between calls: read unless `fresh`, written at the end.  The
 // per-block lz4 mode (prefix / external dictionary, dictionary size) comes
 // from the host's replay of the reference's buffer handling (LinkPlan).
+template <bool XH>
 __global__ void __launch_bounds__(64) k_encode_linked(const uint8_t* __restrict__ src, uint64_t srcSize,
                                                       uint32_t blockSize, uint32_t nBlocks,
                                                       uint8_t* __restrict__ slots, const LinkPlan* __restrict__ plan,
@@ -1354,9 +1391,9 @@ __global__ void __launch_bounds__(64) k_encode_linked(const uint8_t* __restrict_
         const uint64_t off = (uint64_t)b * blockSize;
         const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
         const LinkPlan pl = plan[b];
-        const LinkArgs lk{pl.lowIn, pl.lowDict, pl.candLow, fresh && b == 0};
-        const int32_t r = encode_block_v5<false, false, false, true>(gptr(src) + off - kLinkO0, kLinkO0 + n,
-                                                                     gptr(slots) + off, n - 1, Tl, Xl, nullptr, lk);
+        const LinkArgs lk{pl.lowIn, pl.lowDict, pl.candLow, fresh && b == 0, pl.shift};
+        const int32_t r = encode_block_v5<false, false, false, true, false, false, XH>(
+            gptr(src) + off - kLinkO0, kLinkO0 + n, gptr(slots) + off, n - 1, Tl, Xl, nullptr, lk);
         if (L == 0) csize[b] = r;
         WAVE_SYNC();
         // the next block's coordinates: x -> x - n; older than the window -> 0
@@ -1370,12 +1407,12 @@ __global__ void __launch_bounds__(64) k_encode_linked(const uint8_t* __restrict_
 }
 
 hipError_t launch_encode_linked(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
-                                uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh, int32_t* csize,
-                                hipStream_t st) {
+                                uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh, bool xh,
+                                int32_t* csize, hipStream_t st) {
     if (nBlocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_encode_linked, dim3(1), dim3(64), 0, st, src, srcSize, blockSize, nBlocks, slots, plan, table,
-                       fresh ? 1 : 0, csize, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
-                       (const uint32_t*)nullptr);
+    hipLaunchKernelGGL(xh ? k_encode_linked<true> : k_encode_linked<false>, dim3(1), dim3(64), 0, st, src, srcSize,
+                       blockSize, nBlocks, slots, plan, table, fresh ? 1 : 0, csize, (const uint32_t*)nullptr,
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr);
     return hipGetLastError();
 }
 
@@ -1396,6 +1433,7 @@ hipError_t launch_encode_linked(const uint8_t* src, uint64_t srcSize, uint32_t b
 // finishes from the first unsettled block (its entry is exact).
 //   ctl words: changed[kLinkRounds + 1] | first[kLinkRounds + 1] |
 //              flag[nBlocks] | enc[nBlocks]
+template <bool XH>
 __global__ void __launch_bounds__(64) k_encode_linked_round(const uint8_t* __restrict__ src, uint64_t srcSize,
                                                             uint32_t blockSize, uint8_t* __restrict__ slots,
                                                             const LinkPlan* __restrict__ plan,
@@ -1420,9 +1458,9 @@ __global__ void __launch_bounds__(64) k_encode_linked_round(const uint8_t* __res
     const uint64_t off = (uint64_t)b * blockSize;
     const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
     const LinkPlan pl = plan[b];
-    const LinkArgs lk{pl.lowIn, pl.lowDict, pl.candLow, fr};
-    const int32_t r = encode_block_v5<false, false, false, true>(gptr(src) + off - kLinkO0, kLinkO0 + n,
-                                                                 gptr(slots) + off, n - 1, Tl, (l_u8*)X, nullptr, lk);
+    const LinkArgs lk{pl.lowIn, pl.lowDict, pl.candLow, fr, pl.shift};
+    const int32_t r = encode_block_v5<false, false, false, true, false, false, XH>(
+        gptr(src) + off - kLinkO0, kLinkO0 + n, gptr(slots) + off, n - 1, Tl, (l_u8*)X, nullptr, lk);
     if (L == 0) {
         csize[b] = r;
         enc[b] = round;
@@ -1615,7 +1653,7 @@ uint64_t link_round_bytes(uint64_t nBlocks) {
 // then the serial kernel from the first unsettled block, which runs only if
 // none settled (exact either way).  scratch: link_round_bytes(nBlocks).
 hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
-                                    uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh,
+                                    uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh, bool xh,
                                     uint32_t* scratch, int32_t* csize, int rounds, hipStream_t st) {
     if (nBlocks == 0) return hipSuccess;
     if (rounds < 1 || rounds > kLinkRounds) rounds = kLinkRounds;
@@ -1634,7 +1672,8 @@ hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32
         hipLaunchKernelGGL(k_link_warm, dim3(nBlocks - 1), dim3(64), 0, st, src, blockSize, warm, slots, entry);
     const uint32_t nInit = 2 * (kLinkRounds + 1) + nBlocks;
     hipLaunchKernelGGL(k_link_init, dim3((nInit + 255) / 256), dim3(256), 0, st, ctl, nBlocks);
-    const uint32_t G = link_chain(blockSize);
+    // chains only below 1 MiB; the reference's own-history blocks (xh) are 1 / 4 MiB
+    const uint32_t G = xh ? 0u : link_chain(blockSize);
     for (int r = 0; r < rounds && G > 1; ++r) {   // chained rounds
         const uint32_t nc = (nBlocks + G - 1) / G;
         hipLaunchKernelGGL(k_encode_linked_chain, dim3(nc), dim3(64), 0, st, src, srcSize, blockSize, nBlocks, G, slots,
@@ -1646,17 +1685,19 @@ hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32
                                firstU + r + 1, (uint32_t)r);
     }
     for (int r = 0; r < rounds && G <= 1; ++r) {
-        hipLaunchKernelGGL(k_encode_linked_round, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, plan,
-                           (const uint32_t*)table, fresh ? 1 : 0, (const uint32_t*)entry, exitT, csize,
-                           (const uint32_t*)(changed + r), (const uint32_t*)flag, enc, (uint32_t)r);
+        hipLaunchKernelGGL(xh ? k_encode_linked_round<true> : k_encode_linked_round<false>, dim3(nBlocks), dim3(64), 0,
+                           st, src, srcSize, blockSize, slots, plan, (const uint32_t*)table, fresh ? 1 : 0,
+                           (const uint32_t*)entry, exitT, csize, (const uint32_t*)(changed + r), (const uint32_t*)flag,
+                           enc, (uint32_t)r);
         if (nBlocks > 1)
             hipLaunchKernelGGL(k_link_settle, dim3(nBlocks - 1), dim3(256), 0, st, (const uint32_t*)exitT, entry,
                                nBlocks, (const uint32_t*)(changed + r), (const uint32_t*)enc, flag, changed + r + 1,
                                firstU + r + 1, (uint32_t)r);
     }
     // a single block settles in round 0 (changed[1] stays 0)
-    hipLaunchKernelGGL(k_encode_linked, dim3(1), dim3(64), 0, st, src, srcSize, blockSize, nBlocks, slots, plan, table,
-                       fresh ? 1 : 0, csize, (const uint32_t*)(changed + rounds), (const uint32_t*)(firstU + rounds),
+    hipLaunchKernelGGL(xh ? k_encode_linked<true> : k_encode_linked<false>, dim3(1), dim3(64), 0, st, src, srcSize,
+                       blockSize, nBlocks, slots, plan, table, fresh ? 1 : 0, csize,
+                       (const uint32_t*)(changed + rounds), (const uint32_t*)(firstU + rounds),
                        (const uint32_t*)entry);
     hipLaunchKernelGGL(k_link_final, dim3(1), dim3(256), 0, st, (const uint32_t*)exitT, nBlocks,
                        (const uint32_t*)(changed + rounds), table);

@@ -304,6 +304,30 @@ def bd_ref_decode_main(manifest):
             "roundtrips": out == data, "contiguous_identical": f == bd_frame_contiguous(data, bid, sck, bck)})
 
 
+# Known answers (size + XXH32) of frames the reference writes with 1 and 4 MiB
+# blocks over several FULL blocks (each read over its own dictionary from
+# the second on), for the opt-in LZ4MT_AMD_BD_REFERENCE=1 compressor:
+# (name, bytes, seed, id, sck, bck, input: "bd" = bd_input, "appf" = App. F)
+BD_REF_KNOWN = [
+    ("bdrefk_b6_9m", 9_437_184 + 4321, 23, 6, False, True, "bd"),
+    ("bdrefk_b6_4m_exact", 4 << 20, 5, 6, True, True, "appf"),   # no short last block
+    ("bdrefk_b7_9m", 9_437_184 + 4321, 24, 7, True, False, "bd"),
+    ("bdrefk_b7_appf_17m", (17 << 20) + 99, 42, 7, False, True, "appf"),
+]
+
+
+def bd_ref_known_main(manifest):
+    from oracle import gen_synthetic
+    manifest["bd_ref_known"] = []
+    for name, n, seed, bid, sck, bck, kind in BD_REF_KNOWN:
+        data = bd_input(n, seed) if kind == "bd" else gen_synthetic(n, seed)
+        f = bd_frame_reference(data, bid, sck, bck)
+        manifest["bd_ref_known"].append({
+            "name": name, "bytes": n, "seed": seed, "kind": kind, "bid": bid, "stream_checksum": sck,
+            "block_checksum": bck, "size": len(f), "xxh32": xxh(f), "content_xxh32": xxh(data),
+            "contiguous_identical": f == bd_frame_contiguous(data, bid, sck, bck)})
+
+
 BD_CASES = [  # (name, bytes, seed, block id, stream checksum, block checksum[, input kind])
     ("bd_b4_sX", 1_500_000, 11, 4, False, True), ("bd_b4_SX", 1_500_000, 11, 4, True, True),
     ("bd_b5_Sx", 1_500_000, 12, 5, True, False),
@@ -521,7 +545,13 @@ def main():
 
 
 if __name__ == "__main__":
-    if "--bd-ref-decode" in sys.argv:   # add / refresh only that section of golden.json
+    if "--bd-ref-known" in sys.argv:   # add / refresh only that section of golden.json
+        path = os.path.join(HERE, "golden.json")
+        m = json.load(open(path))
+        bd_ref_known_main(m)
+        json.dump(m, open(path, "w"), indent=0)
+        print(json.dumps(m["bd_ref_known"], indent=1))
+    elif "--bd-ref-decode" in sys.argv:   # add / refresh only that section of golden.json
         path = os.path.join(HERE, "golden.json")
         m = json.load(open(path))
         bd_ref_decode_main(m)

@@ -253,3 +253,63 @@ def test_bd_async_calls_on_two_streams(golden):
     torch.cuda.synchronize()
     for f, data, sd, out, ws, fsz, st in jobs:
         assert host(out[:int(fsz[0].item())]) == read_golden(f["file"]), f["name"]
+
+
+def _ref_entries(golden):
+    """The reference-written 1 / 4 MiB -BD frames: fixtures (bd_ref_decode) and
+    known answers over several full blocks (bd_ref_known), with their inputs."""
+    from oracle import gen_synthetic
+    out = []
+    for f in golden["bd_ref_decode"] + golden["bd_ref_known"]:
+        data = bd_input(f["bytes"], f["seed"]) if f["kind"] == "bd" else gen_synthetic(f["bytes"], f["seed"])
+        out.append((f, data))
+    return out
+
+
+@pytest.mark.parametrize("api,batches,path", [
+    ("device", "one", "rounds"), ("device", "one", "serial"), ("device", "one", "round1"),
+    ("DEVICE", "one", "rounds"), ("DEVICE", "many", "rounds"), ("PARALLEL", "many", "rounds"),
+])
+def test_bd_reference_bytes_mode(golden, monkeypatch, api, batches, path):
+    """LZ4MT_AMD_BD_REFERENCE=1: -BD frames with 1 and 4 MiB blocks written
+    byte for byte as the reference writes them (compressBlockDependency,
+    src/lz4mt.cpp:460-538, translate() at 486-488: lz4 1.9.3's
+    LZ4_slideInputBuffer returns the dictionary's own address, so from the
+    second block on each full block is read over its own dictionary).  Pinned
+    by frames liblz4 1.9.3 wrote with the reference's call sequence
+    (make_golden.py bd_frame_reference): fixtures and size + XXH32 known
+    answers.  Parallel rounds, the one-wave serial kernel, one round + the
+    serial finish, the callback engine in one and many batches."""
+    monkeypatch.setenv("LZ4MT_AMD_BD_REFERENCE", "1")
+    if path == "serial":
+        monkeypatch.setenv("LZ4MT_AMD_BD_SERIAL", "1")
+    if path == "round1":
+        monkeypatch.setenv("LZ4MT_AMD_BD_ROUNDS", "1")
+    if batches == "many":
+        monkeypatch.setenv("LZ4MT_AMD_BATCH0_MIB", "1")
+        monkeypatch.setenv("LZ4MT_AMD_BATCH_MIB", "1")
+    for f, data in _ref_entries(golden):
+        sd = L.make_sd(f["bid"], stream_checksum=f["stream_checksum"], block_checksum=f["block_checksum"],
+                       block_dependence=True)
+        if api == "device":
+            frame = host(L.compress_frame(dev(data), sd))
+        else:
+            r, frame = L.compress(data, sd, mode=L.MODE_DEVICE if api == "DEVICE" else L.MODE_PARALLEL)
+            assert r == 0, (f["name"], L.result_to_string(r))
+        if "file" in f:
+            assert frame == read_golden(f["file"]), (f["name"], api, batches, path)
+        else:
+            assert (len(frame), xxhash.xxh32(frame).intdigest()) == (f["size"], f["xxh32"]), (f["name"], api, path)
+
+
+def test_bd_reference_bytes_mode_off_is_the_decodable_stream(golden):
+    """Without the knob the same inputs give the contiguous (decodable)
+    stream: a different frame wherever a full block follows the first, and
+    it decodes back to the input."""
+    for f, data in _ref_entries(golden)[-2:]:
+        sd = L.make_sd(f["bid"], stream_checksum=f["stream_checksum"], block_checksum=f["block_checksum"],
+                       block_dependence=True)
+        frame = L.compress_frame(dev(data), sd)
+        assert (frame.numel(), xxhash.xxh32(host(frame)).intdigest()) != (f["size"], f["xxh32"]), f["name"]
+        out, r = L.decompress_frame(frame)
+        assert r == 0 and host(out) == data, f["name"]
