@@ -207,6 +207,11 @@ uint64_t lz4mtHipShardBodyBytes(uint64_t n, const Lz4MtStreamDescriptor* sd, voi
  * / batch dependent copies, batch group + far copies, batches, total,
  * matches, far matches, batch sequences, serial-path sequences, -...]. */
 int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* stats16, void* stream);
+/* The frame path's block encoder alone over blocks of any size 65 547 B ..
+ * 4 MiB (frames use 64 KiB .. 4 MiB by 4x steps; the others are timing
+ * points of a split parse, tools/occ_sweep.py).  d_slots: nb x blockSize +
+ * 64 bytes, d_csize: nb int32.  Asynchronous; 0, or -1 on bad arguments. */
+int lz4mtHipDebugEncode(const void* d_src, uint64_t n, uint32_t blockSize, void* d_slots, void* d_csize, void* stream);
 int lz4mtHipDebugDecodeStats(const void* d_frame, uint64_t frameSize, uint64_t* stats16, void* stream);
 /* FETCH_SIZE calibration (tools/fetch_cal.py): reads n bytes of d_buf exactly
  * once with `width`-byte loads per lane (1, 4, 8 or 16); d_out4: 4 bytes of

@@ -1208,6 +1208,20 @@ extern "C" int lz4mtHipGetTimings(float* ms4) {
 // ===========================================================================
 // 4. diagnostics: phase cycle counts of the encode / decode kernels
 // ===========================================================================
+// The frame path's block encoder (launch_encode: the kernel LZ4MT_AMD_ENC /
+// the block size select) over n bytes in blocks of ANY size 65 547 B .. 4 MiB
+// -- also sizes no frame uses (512 KiB, 2 MiB): what one stream of a split
+// parse costs per byte at full occupancy (tools/occ_sweep.py).  d_slots:
+// nb x blockSize + 64 bytes, d_csize: nb int32.  Asynchronous; timing only.
+extern "C" int lz4mtHipDebugEncode(const void* d_src, uint64_t n, uint32_t blockSize, void* d_slots, void* d_csize,
+                                   void* stream) {
+    if (!have_device() || blockSize < 65547u || blockSize > (4u << 20) || !d_src || !d_slots || !d_csize) return -1;
+    const uint64_t nb = (n + blockSize - 1) / blockSize;
+    return launch_encode(static_cast<const uint8_t*>(d_src), n, blockSize, (uint32_t)nb, static_cast<uint8_t*>(d_slots),
+                         blockSize, 0xFFFFFFFFu, static_cast<int32_t*>(d_csize), static_cast<hipStream_t>(stream)) ==
+                   hipSuccess ? 0 : -1;
+}
+
 extern "C" int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* stats16,
                                         void* stream) {
     if (!have_device() || blockSize == 0) return -1;

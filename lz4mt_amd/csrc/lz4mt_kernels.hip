@@ -1716,21 +1716,30 @@ static bool enc_p17(uint32_t blockSize) {
     return blockSize <= (256u << 10);
 }
 
+// LZ4MT_AMD_ENC_LDS_PAD=<bytes>: dynamic LDS added to the frame encoder's
+// launch, i.e. fewer resident waves per CU (occupancy sweeps, timing only;
+// profiles/r04_occupancy_sweep.txt)
+static uint32_t enc_lds_pad() {
+    const char* e = getenv("LZ4MT_AMD_ENC_LDS_PAD");
+    return e ? (uint32_t)atoi(e) : 0u;
+}
+
 hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks, uint8_t* slots,
                          uint64_t slotStride, uint32_t capOverride, int32_t* csize, hipStream_t st) {
     if (nBlocks == 0) return hipSuccess;
+    const uint32_t pad = enc_lds_pad();
     if (blockSize < (uint32_t)kLimit64K)
-        hipLaunchKernelGGL(k_encode16, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, slotStride,
+        hipLaunchKernelGGL(k_encode16, dim3(nBlocks), dim3(64), pad, st, src, srcSize, blockSize, slots, slotStride,
                            capOverride, csize);
     else if (enc_p17(blockSize) && blockSize <= (1u << kPosBits)) {   // 3-byte table; a short last block on k_encode
-        hipLaunchKernelGGL(k_encode_p17, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, slotStride,
+        hipLaunchKernelGGL(k_encode_p17, dim3(nBlocks), dim3(64), pad, st, src, srcSize, blockSize, slots, slotStride,
                            capOverride, csize);
         const uint64_t lastOff = (uint64_t)(nBlocks - 1) * blockSize;
         if (srcSize - lastOff < (uint64_t)kLimit64K)
             hipLaunchKernelGGL(k_encode, dim3(1), dim3(64), 0, st, src + lastOff, srcSize - lastOff, blockSize,
                                slots + (nBlocks - 1) * slotStride, slotStride, capOverride, csize + (nBlocks - 1));
     } else
-        hipLaunchKernelGGL(k_encode, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots, slotStride,
+        hipLaunchKernelGGL(k_encode, dim3(nBlocks), dim3(64), pad, st, src, srcSize, blockSize, slots, slotStride,
                            capOverride, csize);
     return hipGetLastError();
 }

@@ -15,6 +15,9 @@
 #   ab      kernel times of every exp_libs/*.so (tools/mkvariants.sh), two passes
 #   abtrace kernel-trace stats of every exp_libs/*.so;  abbid  ab at every block size
 #   fuzz    random differential campaign (300 s);  sweep  the secondary bench configs
+#   occ     encoder time against resident waves per CU (tools/occ_sweep.py)
+#   bdref   the -BD reference-bytes tests (tests/test_gpu_bd.py -k reference)
+#   nccl1   the world-size-1 nccl tests (tests/test_gpu_dist.py -k nccl)
 set -euo pipefail
 tag=$1; shift
 out=gpurun_out/$tag
@@ -61,6 +64,17 @@ for step in "$@"; do
         timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -T -f csv -d "$out/bid$bid/write_appf" -o write -- \
             python3 tools/kprof.py 8 --bid=$bid > "$out/bid$bid/write.log" 2>&1
       done ;;
+    occ)
+      timeout -k 10 400 python3 tools/occ_sweep.py > "$out/occ.txt" 2>&1 || { tail -20 "$out/occ.txt"; exit 1; }
+      cat "$out/occ.txt" ;;
+    bdref)
+      timeout -k 10 600 python3 -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread tests/test_gpu_bd.py \
+          -k reference > "$out/pytest_bdref.log" 2>&1 || { tail -40 "$out/pytest_bdref.log"; exit 1; }
+      tail -3 "$out/pytest_bdref.log" ;;
+    nccl1)
+      timeout -k 10 600 python3 -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread tests/test_gpu_dist.py \
+          -k nccl > "$out/pytest_nccl1.log" 2>&1 || { tail -40 "$out/pytest_nccl1.log"; exit 1; }
+      tail -3 "$out/pytest_nccl1.log" ;;
     dist2)
       LZ4MT_BENCH_BACKEND=gloo timeout -k 10 400 python3 bench.py --gpus 2 --gib 0.5 --steps 2 --warmup 1 \
           --no-cpu-baseline > "$out/dist2.json" 2> "$out/dist2.err"
