@@ -1788,6 +1788,13 @@ constexpr uint32_t kNxPast = 1024, kNxDead = 1026;
 #define LZ4MT_FAR_TAB 8
 #endif
 constexpr int kFarTab = LZ4MT_FAR_TAB;
+// LZ4MT_FAR_LANES=1: a batch's far-match parameters are read straight from
+// their lanes (s_ff1 over the far mask + v_readlane) instead of a rank-
+// ordered LDS table read back by broadcast, so no far load waits on an LDS
+// round trip (A/B: -DLZ4MT_FAR_LANES=0)
+#ifndef LZ4MT_FAR_LANES
+#define LZ4MT_FAR_LANES 1
+#endif
 static_assert(kFarTab >= 1 && kFarTab <= 24, "far table");
 constexpr int32_t kFpOff = kInWin + 128 + 1040;   // far-match table of a batch (kFarTab x 16 B)
 [[maybe_unused]] constexpr int32_t kWinAlloc = kFpOff + 16 * kFarTab;
@@ -2076,6 +2083,30 @@ struct Dec {
         uint32_t fv[kFarTab], fv2[kFarTab];
         const uint32_t fr = __builtin_amdgcn_mbcnt_hi((uint32_t)(farM >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)farM, 0u));
         const uint32_t nf8 = min((uint32_t)__popcll(farM), (uint32_t)kFarTab);
+#if LZ4MT_FAR_LANES
+        uint32_t flane[kFarTab];   // lane of the g-th far sequence (uniform)
+        if (farM) {
+            if (completed < (int64_t)ringLo) {   // their bytes were stored to dst: make sure the stores landed
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                completed = flushed;
+            }
+            if (ST) acc[7] += __popcll(farM);
+            uint64_t fm = farM;
+#pragma unroll
+            for (int g = 0; g < kFarTab; ++g) {
+                fv[g] = 0; fv2[g] = 0; flane[g] = 0;
+                if ((uint32_t)g < nf8) {
+                    const uint32_t lg = (uint32_t)__builtin_ctzll(fm);
+                    fm &= fm - 1;
+                    flane[g] = lg;
+                    const int64_t fs = (int32_t)rdlane((uint32_t)src, (int)lg);   // a prefix source is negative
+                    const uint32_t fz = rdlane(mlen, (int)lg);
+                    fv[g] = dst[fs + min(L, fz - 1)];   // bytes past the match repeat its last one (never written)
+                    if (fz > 64) fv2[g] = dst[fs + min(L + 64, fz - 1)];
+                }
+            }
+        }
+#else
         l_u4* const fprm = (l_u4*)(win + kFpOff);
         if (farM) {
             if (completed < (int64_t)ringLo) {   // their bytes were stored to dst: make sure the stores landed
@@ -2096,6 +2127,7 @@ struct Dec {
                 }
             }
         }
+#endif
         STAMP_ADD(15, ts);
         // 5b. literal runs of every sequence + grouped matches, 8 per group
         const uint32_t tot = longLit ? 0u : lit + ((in && !far && !ord) ? mlen : 0u);
@@ -2197,10 +2229,18 @@ struct Dec {
 #pragma unroll
             for (int g = 0; g < kFarTab; ++g) {
                 if ((uint32_t)g < nf8) {
+#if LZ4MT_FAR_LANES
+                    const uint32_t qy = rdlane((uint32_t)om, (int)flane[g]) & (kRing - 1);
+                    const uint32_t qz = rdlane(mlen, (int)flane[g]);
+                    *(L < qz ? ringp + ((qy + L) & (kRing - 1)) : dummy + L) = (uint8_t)fv[g];
+                    if (qz > 64)
+                        *(L + 64 < qz ? ringp + ((qy + 64 + L) & (kRing - 1)) : dummy + 64 + L) = (uint8_t)fv2[g];
+#else
                     const v4u q = fprm[g];
                     *(L < q.z ? ringp + ((q.y + L) & (kRing - 1)) : dummy + L) = (uint8_t)fv[g];
                     if ((uint32_t)__builtin_amdgcn_readfirstlane((int)q.z) > 64)
                         *(L + 64 < q.z ? ringp + ((q.y + 64 + L) & (kRing - 1)) : dummy + 64 + L) = (uint8_t)fv2[g];
+#endif
                 }
             }
             uint64_t farLeft = ballot(far && fr >= (uint32_t)kFarTab);

@@ -15,6 +15,7 @@
 #   ab      kernel times of every exp_libs/*.so (tools/mkvariants.sh), two passes
 #   abtrace kernel-trace stats of every exp_libs/*.so;  abbid  ab at every block size
 #   fuzz    random differential campaign (300 s);  sweep  the secondary bench configs
+#   e2e     end-to-end rates (tools/e2e.py 8 7: host memory, then file -> file in /dev/shm)
 #   occ     encoder time against resident waves per CU (tools/occ_sweep.py)
 #   bdref   the -BD reference-bytes tests (tests/test_gpu_bd.py -k reference)
 #   nccl1   the world-size-1 nccl tests (tests/test_gpu_dist.py -k nccl)
@@ -64,6 +65,14 @@ for step in "$@"; do
         timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -T -f csv -d "$out/bid$bid/write_appf" -o write -- \
             python3 tools/kprof.py 8 --bid=$bid > "$out/bid$bid/write.log" 2>&1
       done ;;
+    e2e)
+      timeout -k 10 300 python3 tools/e2e.py 8 7 > "$out/e2e_mem.txt" 2>&1 || { tail -20 "$out/e2e_mem.txt"; exit 1; }
+      cat "$out/e2e_mem.txt"
+      mkdir -p /dev/shm/lz4mt_e2e
+      timeout -k 10 400 python3 tools/e2e.py 8 7 --file /dev/shm/lz4mt_e2e > "$out/e2e_file.txt" 2>&1 \
+          || { rm -rf /dev/shm/lz4mt_e2e; tail -20 "$out/e2e_file.txt"; exit 1; }
+      rm -rf /dev/shm/lz4mt_e2e
+      cat "$out/e2e_file.txt" ;;
     occ)
       timeout -k 10 400 python3 tools/occ_sweep.py > "$out/occ.txt" 2>&1 || { tail -20 "$out/occ.txt"; exit 1; }
       cat "$out/occ.txt" ;;
