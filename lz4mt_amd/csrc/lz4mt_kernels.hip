@@ -1797,7 +1797,15 @@ constexpr int kFarTab = LZ4MT_FAR_TAB;
 #endif
 static_assert(kFarTab >= 1 && kFarTab <= 24, "far table");
 constexpr int32_t kFpOff = kInWin + 128 + 1040;   // far-match table of a batch (kFarTab x 16 B)
-[[maybe_unused]] constexpr int32_t kWinAlloc = kFpOff + 16 * kFarTab;
+// LZ4MT_HOP2=1: the batch's hop takes two sequences per dependent LDS read:
+// D2[p] = next(next(p)) - p as a byte (0 = past the candidates, a complex
+// token or 256+ bytes on: one more single hop), beside the next table; the
+// single hop to the odd sequence is read in the same round (A/B: =0)
+#ifndef LZ4MT_HOP2
+#define LZ4MT_HOP2 1
+#endif
+constexpr int32_t kD2Off = kFpOff + 16 * kFarTab;   // 512 two-hop deltas + 2 sentinels (PAST, DEAD) = 0
+[[maybe_unused]] constexpr int32_t kWinAlloc = kD2Off + (LZ4MT_HOP2 ? 520 : 0);
 static_assert(kRing + kWinAlloc <= 20480 || kRing != 16384, "decoder LDS: 8 waves per CU need <= 20 KiB each");
 
 template <bool ST>
@@ -2013,6 +2021,40 @@ struct Dec {
             *(l_u4*)(nxb + 16 * L) = (v4u){nv[0], nv[1], nv[2], nv[3]};
             WAVE_SYNC();
             uint32_t x = 0, startA = 0, nextA = kNxDead;
+#if LZ4MT_HOP2
+            l_u8* const d2b = win + kD2Off;
+            {   // D2 for positions 8L .. 8L+7: next(next(p)) from the table just written
+                uint32_t q0 = 0, q1 = 0;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const uint32_t n1 = (nv[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;   // next(p), a byte offset
+                    const uint32_t nn = *(l_u16*)(nxb + n1);   // next(n1); PAST / DEAD map to DEAD
+                    const uint32_t t = nn < 1024 ? (nn >> 1) - (8 * L + (uint32_t)e) : 0u;
+                    const uint32_t v = t < 256 ? t : 0u;
+                    if (e < 4) q0 |= v << (8 * e);
+                    else q1 |= v << (8 * (e - 4));
+                }
+                *(l_u64*)(d2b + 8 * L) = ((uint64_t)q1 << 32) | q0;
+                WAVE_SYNC();
+            }
+            for (uint32_t m0 = 0; m0 < 64; m0 += 8) {
+#pragma unroll
+                for (uint32_t e = 0; e < 8; e += 2) {
+                    // sequence m0+e starts at x; x1 = its successor, x2 = the one after
+                    const uint32_t x1 = *(l_u16*)(nxb + x);
+                    const uint32_t dd = (uint32_t)__builtin_amdgcn_readfirstlane((int)d2b[x >> 1]);
+                    uint32_t x2;
+                    if (dd) x2 = x + 2 * dd;
+                    else x2 = *(l_u16*)(nxb + x1);
+                    nextA = L == m0 + e ? x1 : nextA;
+                    startA = L == m0 + e + 1 ? x1 : startA;
+                    nextA = L == m0 + e + 1 ? x2 : nextA;
+                    startA = L == m0 + e + 2 ? x2 : startA;
+                    x = x2;
+                }
+                if ((uint32_t)__builtin_amdgcn_readfirstlane((int)x) == kNxDead) break;
+            }
+#else
             for (uint32_t m0 = 0; m0 < 64; m0 += 8) {
 #pragma unroll
                 for (uint32_t e = 0; e < 8; ++e) {
@@ -2022,6 +2064,7 @@ struct Dec {
                 }
                 if ((uint32_t)__builtin_amdgcn_readfirstlane((int)x) == kNxDead) break;
             }
+#endif
             cnt = (uint32_t)__popcll(bal(nextA != kNxDead));
             startRel = startA >> 1;
         }
@@ -2320,6 +2363,7 @@ __device__ int32_t decode_block(Dec<ST>& D, int64_t cap) {
     if (cap == 0) return (D.len == 1 && D.in8(0) == 0) ? 0 : -1;
     if (D.len == 0) return -1;
     *(l_u32*)(D.win + kNxOff + kNxPast) = kNxDead | (kNxDead << 16);   // next(PAST) = next(DEAD) = DEAD
+    if (LZ4MT_HOP2) *(l_u32*)(D.win + kD2Off + 512) = 0u;                  // D2(PAST) = D2(DEAD) = 0
 
 #define PHYS_CHECK(end_) \
     if ((end_) > D.physcap) return kDecodeOutputTooSmall;
