@@ -103,24 +103,35 @@ while time.time() - t0 < budget:
     sck, bck = rnd.random() < 0.5, rnd.random() < 0.5
     level = rnd.choice([0, 0, 0, 1, 2, 3, 4, 6, 8, 9, 9, 10, 11, 12])
     bd = rnd.random() < 0.25   # -BD: expected frame from liblz4's stream API
+    # 1 / 4 MiB fast -BD blocks: half the cases with LZ4MT_AMD_BD_REFERENCE=1,
+    # whose frames are the reference's own (non-decodable) bytes
+    refb = bd and level < 3 and bid >= 6 and rnd.random() < 0.5
     if level >= 10 or (bd and level >= 3):
         data = data[:3 << 20]   # the CPU side of the optimal parser / the HC stream is slow
     if bd:   # 1 / 4 MiB fast blocks: the decodable contiguous stream (bugs not copied)
         want = (G.bd_hc_frame_reference(data, bid, sck, bck) if level >= 3
-                else G.bd_frame_contiguous(data, bid, sck, bck) if bid >= 6
+                else G.bd_frame_contiguous(data, bid, sck, bck) if bid >= 6 and not refb
                 else G.bd_frame_reference(data, bid, sck, bck))
     else:
         want = (oracle.compress_frame(data, oracle.params(bid, sck, bck)) if level < 3
                 else hc_frame(data, bid, sck, bck, level))
+    if refb:
+        os.environ["LZ4MT_AMD_BD_REFERENCE"] = "1"
     fr = L.compress_frame(dev(data), L.make_sd(bid, sck, bck, block_dependence=bd), level=level)
+    os.environ.pop("LZ4MT_AMD_BD_REFERENCE", None)
     got = host(fr)
     ok = got == want
-    if ok:
+    if ok and refb:   # the reference's bytes: decoding must match the oracle's decode of them
+        out, r = L.decompress_frame(fr, out=torch.empty(len(data) + (8 << 20), dtype=torch.uint8, device="cuda"),
+                                    check=False)
+        rw, ow = oracle.decompress_frame(want, len(data) + (8 << 20))
+        ok = (r, host(out)) == (rw, ow)
+    elif ok:
         out, r = L.decompress_frame(fr)
         ok = r == 0 and host(out) == data
     cases += 1
     nbytes += len(data)
-    key = f"{'BD' if bd else ''}{level}"
+    key = f"{'BDref' if refb else 'BD' if bd else ''}{level}"
     by_level[key] = by_level.get(key, 0) + 1
     if not ok:
         fails.append((cases, len(data), bid, sck, bck, level, bd))
