@@ -216,6 +216,14 @@ int lz4mtHipDebugDecodeStats(const void* d_frame, uint64_t frameSize, uint64_t* 
 /* FETCH_SIZE calibration (tools/fetch_cal.py): reads n bytes of d_buf exactly
  * once with `width`-byte loads per lane (1, 4, 8 or 16); d_out4: 4 bytes of
  * device scratch.  Asynchronous; 0, or -1 on a bad width. */
+/* The per-block lz4 stream plan of a -BD frame (host only): for blocks of
+ * sizes[0..nBlocks), plan4[4b..4b+3] = catch-up bound for candidates in the
+ * block, in the history, the dictSmall limit (block coordinates: the block
+ * at 65536) and where the history bytes stand (0 = before the block; else
+ * the block's own bytes from shift - 65536: the reference's buffer,
+ * refBuffer = 1).  0 on success, 1 if a history would be neither, -1 on a
+ * bad id. */
+int lz4mtDebugBdPlan(int blockMaxId, int refBuffer, const uint32_t* sizes, uint64_t nBlocks, uint32_t* plan4);
 int lz4mtHipDebugFetchCal(const void* d_buf, uint64_t n, int width, void* d_out4, void* stream);
 
 #ifdef __cplusplus

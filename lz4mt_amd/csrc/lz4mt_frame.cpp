@@ -990,3 +990,23 @@ extern "C" int lz4mtResultToLz4cExitCode(Lz4MtResult r) {
         default: return 1;
     }
 }
+
+// Diagnostics (host only, no device needed): the per-block lz4 stream plan
+// BdSim derives for a -BD frame of nBlocks blocks of the given sizes --
+// lowIn, lowDict, candLow, shift per block into plan4[4 * b] -- with the
+// reference's input buffer replayed for every block size (refBuffer = 1, as
+// LZ4MT_AMD_BD_REFERENCE does at 1 / 4 MiB) or only where lz4mt's buffer
+// keeps the history contiguous.  Returns 0, -1 on a bad id, 1 if the plan
+// needs a history that is neither (BdSim.bad).  tests/test_abi.py pins it
+// against a restatement of the reference's buffer loop.
+extern "C" int lz4mtDebugBdPlan(int blockMaxId, int refBuffer, const uint32_t* sizes, uint64_t nBlocks,
+                                uint32_t* plan4) {
+    if (blockMaxId < 4 || blockMaxId > 7 || (!sizes && nBlocks) || (!plan4 && nBlocks)) return -1;
+    lz4mt::BdSim sim(blockMaxId, refBuffer != 0);
+    for (uint64_t b = 0; b < nBlocks; ++b) {
+        uint32_t* p = plan4 + 4 * b;
+        p[3] = 0;
+        sim.next(sizes[b], &p[0], &p[1], &p[2], refBuffer ? &p[3] : nullptr);
+    }
+    return sim.bad ? 1 : 0;
+}

@@ -272,3 +272,102 @@ def test_large_writes_to_append_mode_file(tmp_path):
         assert L.lib.lz4mtIoWrite(ctypes.byref(ctx), c, len(c)) == len(c)
     libc.fclose(fp)
     assert dst.read_bytes() == b"head" + b"".join(chunks)
+
+
+def _ref_bd_plan(bid, sizes, ref_buffer):
+    """compressBlockDependency's buffer loop (reference src/lz4mt.cpp:460-538:
+    max(bm + 64 KiB, 1088 KiB) input buffer, translate() when the next block
+    would not fit) over lz4 1.9.3's LZ4_compress_fast_continue dictionary
+    bookkeeping, restated on buffer offsets, with the buffer's CONTENT
+    tracked byte range by byte range: for each block, what the encoder
+    needs in block coordinates (block at 65536) -- catch-up bounds for
+    candidates in the block / the history, the dictSmall limit -- and
+    whether the history bytes lz4 reads are the stream's own previous bytes
+    (shift 0), the block's own bytes (shift = where they start + 65536), or
+    neither (None).  ref_buffer = False: 1 and 4 MiB blocks in one
+    contiguous buffer (the decodable stream); 64 / 256 KiB always buffered."""
+    bm = 1 << (8 + 2 * bid)
+    buffered = bid <= 5 or ref_buffer
+    size = max(bm + 65536, 1088 * 1024) if buffered else 1 << 62
+    seg = []                      # (buf_lo, buf_hi, stream_lo): what the buffer holds
+    dic, dsz, cur = None, 0, 0    # LZ4_stream_t: dictionary (buffer offset or NULL), dictSize, currentOffset
+    ins, pos, out = 0, 0, []
+
+    def stored(x):
+        for lo, hi, s in reversed(seg):
+            if lo <= x < hi:
+                return s + (x - lo)
+        return None
+
+    for n in sizes:
+        if ins + bm > size:   # translate(): LZ4_slideInputBuffer returns the dictionary pointer (1.9.3)
+            ins = dic
+        seg.append((ins, ins + n, pos))
+        dend = (dic or 0) + dsz
+        if cur + n > 0x80000000:   # LZ4_renormDictT
+            cur = 65536
+            dsz = min(dsz, 65536)
+            dic = dend - dsz
+        if 0 < dsz < 4 and (dic is None or dend != ins):   # tiny dictionaries
+            dsz, dic, dend = 0, ins, ins
+        if dic is not None and ins + n > dic and ins + n < dend:   # input overlaps the dictionary
+            dsz = dend - (ins + n)
+            dsz = 0 if dsz < 4 else min(dsz, 65536)
+            dic = dend - dsz
+        prefix = dic is not None and dend == ins
+        small = dsz < 65536 and dsz < cur
+        ds = min(dsz, 65536)
+        # the buffer -> stream map is linear between segment edges: checking
+        # the history range at every edge inside it (and its ends) checks it all
+        lo_h, hi_h = dend - ds, dend
+        xs = {lo_h, hi_h - 1} | {e + d for a, b, _ in seg for e in (a, b) for d in (-1, 0)
+                                 if lo_h <= e + d < hi_h}
+        if ds == 0 or all(stored(x) == pos - (dend - x) for x in xs):
+            shift = 0
+        elif ins <= lo_h and hi_h <= ins + n:
+            shift = dend - ins
+        else:
+            shift = None
+        out.append((65536 - ds if prefix else 65536, 65536 - ds, 65536 - ds if small else 0, shift))
+        cur += n
+        if prefix:
+            dsz += n
+        else:
+            dic, dsz = ins, n
+        ins += n
+        pos += n
+    return out
+
+
+@pytest.mark.parametrize("bid", [4, 5, 6, 7])
+@pytest.mark.parametrize("ref_buffer", [False, True])
+def test_bd_plan_matches_the_reference_buffer_loop(bid, ref_buffer):
+    """BdSim (lz4mt_host.h, the host half of the -BD encode, exported as
+    lz4mtDebugBdPlan) against the restatement above on full, short and
+    ragged block sequences: lz4's modes and bounds per block, and where the
+    history the encoder must read stands.  With the reference's buffer at 1
+    and 4 MiB (ref_buffer) every full block after the first reads its own
+    bytes (shift = the block size); 64 / 256 KiB blocks and the contiguous
+    stream always read the true history."""
+    import random
+    import ctypes
+    bm = 1 << (8 + 2 * bid)
+    rnd = random.Random(bid * 2 + ref_buffer)
+    cases = [[bm] * 9, [bm] * 4 + [bm // 3], [bm, 100, bm, bm, 7, bm], [bm // 2] * 5 + [bm] * 3,
+             [rnd.choice([bm, bm, bm, rnd.randrange(1, bm)]) for _ in range(40)], [3, bm, 2, bm, bm]]
+    for sizes in cases:
+        want = _ref_bd_plan(bid, sizes, ref_buffer)
+        arr = (ctypes.c_uint32 * len(sizes))(*sizes)
+        plan = (ctypes.c_uint32 * (4 * len(sizes)))()
+        rc = L.lib.lz4mtDebugBdPlan(bid, 1 if ref_buffer else 0, arr, len(sizes), plan)
+        got = [tuple(plan[4 * i:4 * i + 4]) for i in range(len(sizes))]
+        bad = any(w[3] is None for w in want)
+        assert rc == (1 if bad else 0), (sizes[:8], rc)
+        for i, (w, g) in enumerate(zip(want, got)):
+            assert g[:3] == w[:3], (bid, ref_buffer, i, sizes[:8], g, w)
+            if w[3] is not None:
+                assert g[3] == (w[3] if ref_buffer else 0), (bid, ref_buffer, i, g, w)
+        if ref_buffer and bid >= 6 and sizes == [bm] * 9:
+            assert [g[3] for g in got] == [0] + [bm] * 8
+        if not ref_buffer or bid <= 5:
+            assert all(w[3] == 0 for w in want), (bid, sizes[:8])
