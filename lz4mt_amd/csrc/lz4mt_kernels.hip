@@ -1791,7 +1791,8 @@ constexpr int kFarTab = LZ4MT_FAR_TAB;
 // LZ4MT_FAR_LANES=1: a batch's far-match parameters are read straight from
 // their lanes (s_ff1 over the far mask + v_readlane) instead of a rank-
 // ordered LDS table read back by broadcast, so no far load waits on an LDS
-// round trip (A/B: -DLZ4MT_FAR_LANES=0)
+// round trip (k_decode 31.36 -> 31.03 ms at 8 GiB B7, two passes each,
+// profiles/r04c_decoder_ab.txt; A/B: -DLZ4MT_FAR_LANES=0)
 #ifndef LZ4MT_FAR_LANES
 #define LZ4MT_FAR_LANES 1
 #endif
@@ -1800,9 +1801,12 @@ constexpr int32_t kFpOff = kInWin + 128 + 1040;   // far-match table of a batch 
 // LZ4MT_HOP2=1: the batch's hop takes two sequences per dependent LDS read:
 // D2[p] = next(next(p)) - p as a byte (0 = past the candidates, a complex
 // token or 256+ bytes on: one more single hop), beside the next table; the
-// single hop to the odd sequence is read in the same round (A/B: =0)
+// single hop to the odd sequence is read in the same round.  Off: building
+// D2 (8 conflicting LDS gathers per lane) and the per-pair scalar branch cost
+// more than the halved chain saves (k_decode 31.0 -> 33.9 ms at 8 GiB B7,
+// profiles/r04c_decoder_ab.txt)
 #ifndef LZ4MT_HOP2
-#define LZ4MT_HOP2 1
+#define LZ4MT_HOP2 0
 #endif
 constexpr int32_t kD2Off = kFpOff + 16 * kFarTab;   // 512 two-hop deltas + 2 sentinels (PAST, DEAD) = 0
 [[maybe_unused]] constexpr int32_t kWinAlloc = kD2Off + (LZ4MT_HOP2 ? 520 : 0);
