@@ -43,6 +43,15 @@ def test_bench_gpus2_launches_two_ranks_weak():
     assert line["gather"].startswith("streamed") and line["gather_rounds"] >= 1
     assert line["stitched_frame_bytes"] == line["frame_bytes"]
     assert 1.9 < line["ratio"] < 2.2
+    # the N > 1 line reports what the 8-GPU run needs read:
+    # backend, transport, the root's memory, the peer-access matrix and the
+    # scatter's parts; gloo moves device pieces through pinned host copies
+    assert line["backend"] == "gloo" and line["transport"] == "ipc"
+    assert line["root_memory"]["max_allocated_GiB"] > 0 and line["root_memory"]["device_used_GiB"] > 0
+    assert line["peer_access"] and all(row[i] for i, row in enumerate(line["peer_access"]))
+    sp = line["scatter_split_ms"]
+    assert sp["host_staged"] is True and sp["p2p"] >= 0 and sp["walk"] >= 0
+    assert line["scatter_ms"] < 5000   # round 3's gloo scatter read device memory through the host: 11.2 s
 
 
 @pytest.mark.gpu
