@@ -1796,6 +1796,11 @@ constexpr int kFarTab = LZ4MT_FAR_TAB;
 #ifndef LZ4MT_FAR_LANES
 #define LZ4MT_FAR_LANES 1
 #endif
+// LZ4MT_ORD_LANES=1: the same for the ordered matches (5d): each one's
+// parameters by v_readlane from its lane, no rank table in LDS
+#ifndef LZ4MT_ORD_LANES
+#define LZ4MT_ORD_LANES 1
+#endif
 static_assert(kFarTab >= 1 && kFarTab <= 24, "far table");
 constexpr int32_t kFpOff = kInWin + 128 + 1040;   // far-match table of a batch (kFarTab x 16 B)
 // LZ4MT_HOP2=1: the batch's hop takes two sequences per dependent LDS read:
@@ -2312,15 +2317,25 @@ struct Dec {
         // rank into the (now free) copy table, read back by broadcast
         const uint32_t nOrd = (uint32_t)__popcll(ordM);
         if (nOrd) {
+            const uint32_t magicL = (off > 0 && off < 64) ? (65536u + off - 1) / off : 0u;
+#if LZ4MT_ORD_LANES
+            uint64_t oLeft = ordM;
+            for (uint32_t g = 0; g < nOrd; ++g) {
+                const int lg = (int)__builtin_ctzll(oLeft);
+                oLeft &= oLeft - 1;
+                const uint32_t jom = rdlane((uint32_t)om, lg) & (kRing - 1), joff = rdlane(off, lg);
+                const uint32_t jm = rdlane(mlen, lg), magic = rdlane(magicL, lg);
+                const uint32_t jmS = jm;
+#else
             l_u4* const oprm = (l_u4*)(win + kNxOff);
             const uint32_t orank = __builtin_amdgcn_mbcnt_hi((uint32_t)(ordM >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ordM, 0u));
-            const uint32_t magicL = (off > 0 && off < 64) ? (65536u + off - 1) / off : 0u;
             if (ord) oprm[orank] = (v4u){(uint32_t)om & (kRing - 1), off, mlen, magicL};
             WAVE_SYNC();
             for (uint32_t g = 0; g < nOrd; ++g) {
                 const v4u q = oprm[g];
                 const uint32_t jom = q.x, joff = q.y, jm = q.z, magic = q.w;
                 const uint32_t jmS = (uint32_t)__builtin_amdgcn_readfirstlane((int)jm);
+#endif
                 for (uint32_t base = 0; base < jmS; base += 64) {
                     const uint32_t k = base + L;
                     const uint32_t kk = (joff >= 64 || k < joff) ? k : k - ((k * magic) >> 16) * joff;
