@@ -1802,6 +1802,16 @@ constexpr int kFarTab = LZ4MT_FAR_TAB;
 #ifndef LZ4MT_ORD_LANES
 #define LZ4MT_ORD_LANES 1
 #endif
+// LZ4MT_FAR_DEFER=1: a batch's far bytes (up to kFarTab matches) are written
+// into the ring at the NEXT batch's first use of the ring (after its token
+// parse), so the far loads' latency overlaps the end of this batch and the
+// next batch's parse instead of stalling 5c; written at once when one of the
+// batch's ordered matches reads a far output, and before any serial
+// sequence (requires LZ4MT_FAR_LANES)
+#ifndef LZ4MT_FAR_DEFER
+#define LZ4MT_FAR_DEFER 1
+#endif
+static_assert(!LZ4MT_FAR_DEFER || LZ4MT_FAR_LANES, "deferred far writes read the far lanes' parameters");
 static_assert(kFarTab >= 1 && kFarTab <= 24, "far table");
 constexpr int32_t kFpOff = kInWin + 128 + 1040;   // far-match table of a batch (kFarTab x 16 B)
 // LZ4MT_HOP2=1: the batch's hop takes two sequences per dependent LDS read:
@@ -1834,6 +1844,26 @@ struct Dec {
     int64_t flushed;      // [0, flushed) stored to dst
     int64_t completed;    // [0, completed) known complete in memory
     int32_t lowP;         // lowest position a match may read: 0, or -65536 with a 64 KiB prefix before dst
+    // far bytes of the last batch not yet in the ring (LZ4MT_FAR_DEFER):
+    // pfN matches, ring target / length per match (uniform), their bytes per lane
+    uint32_t pfN;
+    uint32_t pfOm[kFarTab], pfLen[kFarTab], pfv[kFarTab], pfv2[kFarTab];
+
+    __device__ __forceinline__ void flush_far() {
+        if (!LZ4MT_FAR_DEFER || pfN == 0) return;
+        const uint32_t L = laneid();
+        l_u8* const dummy = win + kInWin;
+#pragma unroll
+        for (int g = 0; g < kFarTab; ++g) {
+            if ((uint32_t)g < pfN) {
+                const uint32_t qy = pfOm[g], qz = pfLen[g];
+                *(L < qz ? ring + ((qy + L) & (kRing - 1)) : dummy + L) = (uint8_t)pfv[g];
+                if (qz > 64) *(L + 64 < qz ? ring + ((qy + 64 + L) & (kRing - 1)) : dummy + 64 + L) = (uint8_t)pfv2[g];
+            }
+        }
+        pfN = 0;
+        WAVE_SYNC();
+    }
 
     __device__ __forceinline__ void refill(int64_t i) {
         const uintptr_t base = (reinterpret_cast<uintptr_t>(src) + (uintptr_t)i) & ~uintptr_t(15);
@@ -1980,7 +2010,10 @@ struct Dec {
     __device__ __forceinline__ int decode_batch(int64_t& ip64, int64_t& op64, int64_t iend64, int64_t oend64) {
         // every sequence is validated against 1.9.3's fast-loop conditions
         // below; this guard only keeps the batch machinery inside the block
-        if (ip64 + 17 > iend64 || op64 + 64 > oend64) return 0;
+        if (ip64 + 17 > iend64 || op64 + 64 > oend64) {
+            flush_far();   // the serial path reads the ring
+            return 0;
+        }
         STAMP_ADD(0, ts);
         if (ip64 < wlo || ip64 + 1024 > wlo + kInWin) refill(ip64);
         STAMP_ADD(10, ts);
@@ -2079,7 +2112,10 @@ struct Dec {
             startRel = startA >> 1;
         }
         STAMP_ADD(12, ts);
-        if (cnt == 0) return 0;
+        if (cnt == 0) {
+            flush_far();
+            return 0;
+        }
         if (ST) acc[4] += 1;
         // 3. fields (lane j = sequence j), branch-free
         const bool act = L < cnt;
@@ -2118,6 +2154,7 @@ struct Dec {
         const uint64_t bad = ballot(act && !ok);
         const uint32_t nb = bad ? (uint32_t)(__ffsll((long long)bad) - 1) : cnt;
         STAMP_ADD(13, ts);
+        flush_far();   // the last batch's far bytes: before this batch's copies and flushes read the ring
         if (nb == 0) return 0;
         const bool in = L < nb;
         if (ST) { acc[6] += nb; acc[8] += nb; }
@@ -2133,7 +2170,14 @@ struct Dec {
         // 5a. far loads (up to 8 sequences, lane per byte), in flight during 5b.
         // The far lanes publish (source, ring target, length) in rank order to
         // a small LDS table that the wave reads back by broadcast.
+#if LZ4MT_FAR_DEFER
+        // the far loads land straight in the pending registers (flush_far ran
+        // above): no register move that would wait for them
+        uint32_t (&fv)[kFarTab] = pfv;
+        uint32_t (&fv2)[kFarTab] = pfv2;
+#else
         uint32_t fv[kFarTab], fv2[kFarTab];
+#endif
         const uint32_t fr = __builtin_amdgcn_mbcnt_hi((uint32_t)(farM >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)farM, 0u));
         const uint32_t nf8 = min((uint32_t)__popcll(farM), (uint32_t)kFarTab);
 #if LZ4MT_FAR_LANES
@@ -2279,9 +2323,32 @@ struct Dec {
         }
         // 5c. far bytes into the ring at the match outputs
         if (farM) {
+#if LZ4MT_FAR_DEFER
+            // deferred to the next batch unless an ordered match of this one
+            // reads a far output (its source range meets [farLo, farHi))
+            int32_t farLo = INT32_MAX, farHi = INT32_MIN;
 #pragma unroll
             for (int g = 0; g < kFarTab; ++g) {
                 if ((uint32_t)g < nf8) {
+                    const int32_t o = (int32_t)rdlane((uint32_t)om, (int)flane[g]);
+                    farLo = min(farLo, o);
+                    farHi = max(farHi, o + (int32_t)rdlane(mlen, (int)flane[g]));
+                }
+            }
+            const bool deferFar = !ballot(ord && src < farHi && src + (int32_t)mlen > farLo);
+#else
+            const bool deferFar = false;
+#endif
+#pragma unroll
+            for (int g = 0; g < kFarTab; ++g) {
+                if ((uint32_t)g < nf8) {
+#if LZ4MT_FAR_DEFER
+                    if (deferFar) {   // fv / fv2 are pfv / pfv2
+                        pfOm[g] = rdlane((uint32_t)om, (int)flane[g]) & (kRing - 1);
+                        pfLen[g] = rdlane(mlen, (int)flane[g]);
+                        continue;
+                    }
+#endif
 #if LZ4MT_FAR_LANES
                     const uint32_t qy = rdlane((uint32_t)om, (int)flane[g]) & (kRing - 1);
                     const uint32_t qz = rdlane(mlen, (int)flane[g]);
@@ -2308,8 +2375,12 @@ struct Dec {
                 if (L + 64 < jm) ring[(jo + 64 + L) & (kRing - 1)] = (uint8_t)a1;
                 farLeft &= farLeft - 1;
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            completed = flushed;
+            if (deferFar) {
+                pfN = nf8;   // written by flush_far; their loads stay in flight until then
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                completed = flushed;
+            }
         }
         WAVE_SYNC();
         STAMP_ADD(3, ts);
@@ -2383,6 +2454,7 @@ __device__ int32_t decode_block(Dec<ST>& D, int64_t cap) {
     if (cap == 0) return (D.len == 1 && D.in8(0) == 0) ? 0 : -1;
     if (D.len == 0) return -1;
     *(l_u32*)(D.win + kNxOff + kNxPast) = kNxDead | (kNxDead << 16);   // next(PAST) = next(DEAD) = DEAD
+    D.pfN = 0;
     if (LZ4MT_HOP2) *(l_u32*)(D.win + kD2Off + 512) = 0u;                  // D2(PAST) = D2(DEAD) = 0
 
 #define PHYS_CHECK(end_) \
@@ -2496,6 +2568,7 @@ safe_decode:
         op = cpy;
     }
 #undef PHYS_CHECK
+    D.flush_far();
     D.flush_tail(op);
     return (int32_t)op;
 
