@@ -1807,9 +1807,13 @@ constexpr int kFarTab = LZ4MT_FAR_TAB;
 // parse), so the far loads' latency overlaps the end of this batch and the
 // next batch's parse instead of stalling 5c; written at once when one of the
 // batch's ordered matches reads a far output, and before any serial
-// sequence (requires LZ4MT_FAR_LANES)
+// sequence (requires LZ4MT_FAR_LANES).  Off: k_decode 30.9 -> 34.1 ms.
+// vmcnt retires in issue order, so the next batch's first waited load (its
+// input refill) waits for the deferred far loads anyway, and the loop-
+// carried far registers double the kernel's VGPRs (87 -> 175) and add SGPR
+// spills (profiles/r04g_decoder_far_defer_ab.txt)
 #ifndef LZ4MT_FAR_DEFER
-#define LZ4MT_FAR_DEFER 1
+#define LZ4MT_FAR_DEFER 0
 #endif
 static_assert(!LZ4MT_FAR_DEFER || LZ4MT_FAR_LANES, "deferred far writes read the far lanes' parameters");
 static_assert(kFarTab >= 1 && kFarTab <= 24, "far table");
