@@ -663,7 +663,9 @@ def control_group(group=None):
     is gloo.  Made once per group (collective on first use)."""
     if dist.get_backend(group) == "gloo":
         return group
-    key = id(group) if group is not None else None
+    # keyed by the group AND the default group, so a new process group in
+    # the same process (after destroy_process_group) gets a new control group
+    key = (id(group) if group is not None else None, id(dist.group.WORLD))
     if key not in _CTRL_GROUPS:
         ranks = dist.get_process_group_ranks(group) if group is not None else None
         _CTRL_GROUPS[key] = dist.new_group(ranks=ranks, backend="gloo")
