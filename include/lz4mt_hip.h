@@ -212,6 +212,12 @@ int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, 
  * points of a split parse, tools/occ_sweep.py).  d_slots: nb x blockSize +
  * 64 bytes, d_csize: nb int32.  Asynchronous; 0, or -1 on bad arguments. */
 int lz4mtHipDebugEncode(const void* d_src, uint64_t n, uint32_t blockSize, void* d_slots, void* d_csize, void* stream);
+/* The parse work of a split parse: n bytes in streams of S bytes, stream b
+ * parsed from ov bytes before its start (the overlap a join needs), S + ov
+ * <= 4 MiB, into d_slots (nb x (S + ov) + 64 bytes), sizes into d_csize;
+ * p17 = 1 selects the 3-byte table.  Timing only; 0, or -1 on bad args. */
+int lz4mtHipDebugEncodeOverlap(const void* d_src, uint64_t n, uint32_t S, uint32_t ov, int p17, void* d_slots,
+                               void* d_csize, void* stream);
 int lz4mtHipDebugDecodeStats(const void* d_frame, uint64_t frameSize, uint64_t* stats16, void* stream);
 /* FETCH_SIZE calibration (tools/fetch_cal.py): reads n bytes of d_buf exactly
  * once with `width`-byte loads per lane (1, 4, 8 or 16); d_out4: 4 bytes of

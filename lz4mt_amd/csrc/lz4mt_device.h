@@ -81,6 +81,8 @@ struct AuxStream {
 };
 
 // ---- kernel launchers (lz4mt_kernels.hip) ----
+hipError_t launch_encode_overlap(const uint8_t* src, uint64_t srcSize, uint32_t S, uint32_t ov, bool p17,
+                                 uint8_t* slots, int32_t* csize, hipStream_t st);
 hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                          uint8_t* slots, uint64_t slotStride, uint32_t capOverride, int32_t* csize,
                          hipStream_t st);

@@ -1222,6 +1222,18 @@ extern "C" int lz4mtHipDebugEncode(const void* d_src, uint64_t n, uint32_t block
                    hipSuccess ? 0 : -1;
 }
 
+// The parse work of a split parse of n bytes into streams of S bytes, each
+// parsed from ov bytes before its start (k_encode_overlap): d_slots nb x
+// (S + ov) + 64 bytes, d_csize nb int32; p17 selects the 3-byte table.
+// Asynchronous; timing only (tools/occ_sweep.py --overlap).
+extern "C" int lz4mtHipDebugEncodeOverlap(const void* d_src, uint64_t n, uint32_t S, uint32_t ov, int p17,
+                                          void* d_slots, void* d_csize, void* stream) {
+    if (!have_device() || S == 0 || (uint64_t)S + ov > (4u << 20) || !d_src || !d_slots || !d_csize) return -1;
+    return launch_encode_overlap(static_cast<const uint8_t*>(d_src), n, S, ov, p17 != 0, static_cast<uint8_t*>(d_slots),
+                                 static_cast<int32_t*>(d_csize), static_cast<hipStream_t>(stream)) == hipSuccess
+               ? 0 : -1;
+}
+
 extern "C" int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* stats16,
                                         void* stream) {
     if (!have_device() || blockSize == 0) return -1;

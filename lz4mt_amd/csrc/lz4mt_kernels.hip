@@ -1716,6 +1716,38 @@ static bool enc_p17(uint32_t blockSize) {
     return blockSize <= (256u << 10);
 }
 
+// The parse work of a split parse (timing only): stream b of S
+// bytes is parsed from `ov` bytes before its start -- the overlap its join
+// with stream b-1 needs -- into slot b (stride S + ov); k_encode's table
+// (P17 = 0) or the 3-byte one (P17 = 1).  No join: this is the part of the
+// split parse's cost that the joins would only add to.
+template <bool P17>
+__global__ void __launch_bounds__(64) k_encode_overlap(const uint8_t* __restrict__ src, uint64_t srcSize, uint32_t S,
+                                                       uint32_t ov, uint8_t* __restrict__ slots,
+                                                       int32_t* __restrict__ csize) {
+    constexpr uint32_t kWords = P17 ? (2 * (4096 + 64) + (4096 + 64) + kSR + kSRMirror) / 4 : 5120;
+    __shared__ __attribute__((aligned(16))) uint32_t OLDS[kWords];
+    const uint32_t b = blockIdx.x;
+    const uint64_t lo = (uint64_t)b * S > ov ? (uint64_t)b * S - ov : 0u;
+    const uint64_t hi = min<uint64_t>((uint64_t)(b + 1) * S, srcSize);
+    const uint32_t n = (uint32_t)(hi - lo);
+    if (n < (uint32_t)kLimit64K || n > (1u << kPosBits)) return;
+    l_u8* ring = P17 ? (l_u8*)OLDS + 3 * (4096 + 64) : (l_u8*)(OLDS + 4352);
+    const int32_t r = encode_block_v5<false, false, false, false, P17>(gptr(src) + lo, n,
+                                                                        gptr(slots) + (uint64_t)b * (S + ov), n,
+                                                                        (l_u32*)OLDS, ring, nullptr);
+    if (laneid() == 0) csize[b] = r;
+}
+
+hipError_t launch_encode_overlap(const uint8_t* src, uint64_t srcSize, uint32_t S, uint32_t ov, bool p17,
+                                 uint8_t* slots, int32_t* csize, hipStream_t st) {
+    const uint32_t nb = (uint32_t)((srcSize + S - 1) / S);
+    if (nb == 0) return hipSuccess;
+    if (p17) hipLaunchKernelGGL(k_encode_overlap<true>, dim3(nb), dim3(64), 0, st, src, srcSize, S, ov, slots, csize);
+    else hipLaunchKernelGGL(k_encode_overlap<false>, dim3(nb), dim3(64), 0, st, src, srcSize, S, ov, slots, csize);
+    return hipGetLastError();
+}
+
 // LZ4MT_AMD_ENC_LDS_PAD=<bytes>: dynamic LDS added to the frame encoder's
 // launch, i.e. fewer resident waves per CU (occupancy sweeps, timing only;
 // profiles/r04_occupancy_sweep.txt)

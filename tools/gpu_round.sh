@@ -17,6 +17,7 @@
 #   fuzz    random differential campaign (300 s);  sweep  the secondary bench configs
 #   e2e     end-to-end rates (tools/e2e.py 8 7: host memory, then file -> file in /dev/shm)
 #   occ     encoder time against resident waves per CU (tools/occ_sweep.py)
+#   ovl     the split parse's parse work with real overlap (occ_sweep.py --overlap)
 #   bdref   the -BD reference-bytes tests (tests/test_gpu_bd.py -k reference)
 #   nccl1   the world-size-1 nccl tests (tests/test_gpu_dist.py -k nccl)
 set -euo pipefail
@@ -73,6 +74,9 @@ for step in "$@"; do
           || { rm -rf /dev/shm/lz4mt_e2e; tail -20 "$out/e2e_file.txt"; exit 1; }
       rm -rf /dev/shm/lz4mt_e2e
       cat "$out/e2e_file.txt" ;;
+    ovl)
+      timeout -k 10 400 python3 tools/occ_sweep.py --overlap > "$out/ovl.txt" 2>&1 || { tail -20 "$out/ovl.txt"; exit 1; }
+      cat "$out/ovl.txt" ;;
     occ)
       timeout -k 10 400 python3 tools/occ_sweep.py > "$out/occ.txt" 2>&1 || { tail -20 "$out/occ.txt"; exit 1; }
       cat "$out/occ.txt" ;;

@@ -9,7 +9,11 @@ adds dynamic LDS to the launch, i.e. fewer resident waves.  A split parse
 of 4 MiB blocks into streams of S bytes costs about (time at S) x (1 +
 overlap / S) plus the joins, so these rows bound what it can gain.
 Timing: HIP events on the launch stream, best of 3.
-usage: python tools/occ_sweep.py"""
+--overlap: instead, time the split parse's parse work directly
+(lz4mtHipDebugEncodeOverlap: stream b of S bytes parsed cold from ov bytes
+before its start, the overlap its join needs; 410 KiB = the mean measured
+by tools/split_sim.py, 1018 KiB = its maximum), joins not included.
+usage: python tools/occ_sweep.py [--overlap]"""
 import ctypes
 import os
 import sys
@@ -46,6 +50,38 @@ def run(bs, enc, waves=None):
     total = int(csize[:nb].clamp(min=0).sum().item())
     return best, pad, total
 
+
+
+
+def run_overlap(S, ov, enc):
+    nb = (N + S - 1) // S
+    out = torch.empty(nb * (S + ov) + 64, dtype=torch.uint8, device="cuda")
+    cs = torch.empty(nb, dtype=torch.int32, device="cuda")
+    best = 1e9
+    for _ in range(3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        if L.lib.lz4mtHipDebugEncodeOverlap(ctypes.c_void_p(src.data_ptr()), N, S, ov, int(enc == "p17"),
+                                            ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(cs.data_ptr()),
+                                            ctypes.c_void_p(st.cuda_stream)) != 0:
+            raise RuntimeError("lz4mtHipDebugEncodeOverlap")
+        b.record(st)
+        b.synchronize()
+        best = min(best, a.elapsed_time(b))
+    bad = int((cs <= 0).sum().item())
+    del out
+    return best, bad
+
+
+if "--overlap" in sys.argv:
+    print("split parse, parse work only: stream S, overlap ov, encoder: ms per 8 GiB", flush=True)
+    for S in (512 << 10, 1 << 20, 2 << 20):
+        for ov in (0, 410 << 10, 1018 << 10):
+            for enc in ("base", "p17"):
+                t, bad = run_overlap(S, ov, enc)
+                print(f"S {S >> 10:5d} KiB ov {ov >> 10:5d} KiB {enc:4s}: {t:8.2f} ms"
+                      + (f"  ({bad} streams raw/failed)" if bad else ""), flush=True)
+    sys.exit(0)
 
 print("stream/block size, encoder, waves/CU (LDS pad): encode ms per 8 GiB, encoded bytes", flush=True)
 for bs in (256 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20):
