@@ -1232,7 +1232,7 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
     if (n < (uint32_t)kLimit64K)
         r = encode_block<true, false, false>(s, n, d, cap, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
     else if (n <= (1u << kPosBits))
-        r = encode_block_v5<false, false>(s, n, d, cap, Tl, Xl, nullptr);
+        [[clang::always_inline]] r = encode_block_v5<false, false>(s, n, d, cap, Tl, Xl, nullptr);
     else
         r = encode_block<false, false, false>(s, n, d, cap, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
     if (laneid() == 0) csize[b] = r;
@@ -1289,9 +1289,9 @@ __global__ void __launch_bounds__(64) k_encode_p17(const uint8_t* __restrict__ s
     if (n < (uint32_t)kLimit64K || n > (1u << kPosBits)) return;
     const uint32_t cap = (capOverride == 0xFFFFFFFFu) ? n : capOverride;   // lz4mt: cap = n
     l_u8* Xl = (l_u8*)PLDS + 3 * (4096 + 64);
-    const int32_t r = encode_block_v5<false, false, false, false, true>(gptr(src) + off, n,
-                                                                        gptr(slots) + (uint64_t)b * slotStride, cap,
-                                                                        (l_u32*)PLDS, Xl, nullptr);
+    int32_t r;
+    [[clang::always_inline]] r = encode_block_v5<false, false, false, false, true>(
+        gptr(src) + off, n, gptr(slots) + (uint64_t)b * slotStride, cap, (l_u32*)PLDS, Xl, nullptr);
     if (laneid() == 0) csize[b] = r;
 }
 
@@ -1733,9 +1733,13 @@ __global__ void __launch_bounds__(64) k_encode_overlap(const uint8_t* __restrict
     const uint32_t n = (uint32_t)(hi - lo);
     if (n < (uint32_t)kLimit64K || n > (1u << kPosBits)) return;
     l_u8* ring = P17 ? (l_u8*)OLDS + 3 * (4096 + 64) : (l_u8*)(OLDS + 4352);
-    const int32_t r = encode_block_v5<false, false, false, false, P17>(gptr(src) + lo, n,
-                                                                        gptr(slots) + (uint64_t)b * (S + ov), n,
-                                                                        (l_u32*)OLDS, ring, nullptr);
+    // inlined here, so k_encode / k_encode_p17 stay the only call sites of
+    // their instantiations (a second call site outlines the encoder into a
+    // called function in the product kernels too)
+    int32_t r;
+    [[clang::always_inline]] r = encode_block_v5<false, false, false, false, P17>(gptr(src) + lo, n,
+                                                                             gptr(slots) + (uint64_t)b * (S + ov),
+                                                                             n, (l_u32*)OLDS, ring, nullptr);
     if (laneid() == 0) csize[b] = r;
 }
 

@@ -371,3 +371,39 @@ def test_bd_plan_matches_the_reference_buffer_loop(bid, ref_buffer):
             assert [g[3] for g in got] == [0] + [bm] * 8
         if not ref_buffer or bid <= 5:
             assert all(w[3] == 0 for w in want), (bid, sizes[:8])
+
+
+def _device_functions(lib_path, tmp_path):
+    """Names of the outlined (called, not inlined) gfx950 functions in every
+    code object bundle of the library's .hip_fatbin section."""
+    bundler = "/opt/rocm/lib/llvm/bin/clang-offload-bundler"
+    readelf = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+    if not (os.path.exists(bundler) and os.path.exists(readelf)):
+        pytest.skip("ROCm LLVM tools absent")
+    fat = tmp_path / "fat.bin"
+    subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", lib_path, str(fat)], check=True)
+    data = fat.read_bytes()
+    offs = [m.start() for m in re.finditer(b"__CLANG_OFFLOAD_BUNDLE__|CCOB", data)] + [len(data)]
+    names = []
+    for i, (a, b) in enumerate(zip(offs, offs[1:])):
+        part, co = tmp_path / f"b{i}.bin", tmp_path / f"co{i}.o"
+        part.write_bytes(data[a:b])
+        subprocess.run([bundler, "--type=o", f"--input={part}", "--unbundle",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+        out = subprocess.run([readelf, "-s", "--wide", str(co)], check=True, capture_output=True, text=True).stdout
+        names += [ln.split()[-1] for ln in out.splitlines() if " FUNC " in ln]
+    assert names, "no gfx950 code object found"
+    return names
+
+
+def test_frame_encoders_are_inlined(tmp_path):
+    """The frame path's block encoders (k_encode, k_encode_p17, k_encode16,
+    k_encode_pub) run encode_block_v5 inlined: a second call site of one of
+    their instantiations (a debug kernel, say) makes LLVM outline it into a
+    called function, which cost k_encode ~8 % when it happened in round 4.
+    Only the -BD (LINK) instantiations are meant to be called functions."""
+    funcs = _device_functions(os.path.join(ROOT, "lz4mt_amd", "liblz4mt_amd.so"), tmp_path)
+    outlined = [f for f in funcs if "encode_block_v5" in f]
+    # template arguments <ST, U16, SPLIT, LINK, ...> mangle as ILb<ST>ELb<U16>ELb<SPLIT>ELb<LINK>E
+    bad = [f for f in outlined if not re.search(r"encode_block_v5ILb\dELb\dELb\dELb1E", f)]
+    assert not bad, f"frame encoders outlined: {bad}"
