@@ -3280,7 +3280,18 @@ __device__ __forceinline__ uint32_t xq_rounds(uint32_t v, const uint32_t (&w)[kX
 
 // XXH32 (seed 0) of [p, p+len) for the quad's block; every lane of the quad
 // returns the digest.  All 64 lanes must call it (DPP reads neighbours).
-__device__ uint32_t xxh32_quad(g_cu8* p, uint32_t len, g_cu8* safe /* any readable byte */) {
+// LZ4MT_XQ_INLINE=1: xxh32_quad inlined into its three kernels (LLVM outlines
+// it: three call sites).  Off: the decode it runs beside is 0.3 ms slower with
+// it inlined (30.9 -> 31.2 ms at 8 GiB; profiles/r04m_xxh32_quad_inline_ab.txt)
+#ifndef LZ4MT_XQ_INLINE
+#define LZ4MT_XQ_INLINE 0
+#endif
+#if LZ4MT_XQ_INLINE
+#define XQ_INLINE __forceinline__
+#else
+#define XQ_INLINE __noinline__
+#endif
+__device__ XQ_INLINE uint32_t xxh32_quad(g_cu8* p, uint32_t len, g_cu8* safe /* any readable byte */) {
     const uint32_t c = laneid() & 3u;
     const uint32_t ns = len >> 4;
     const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
