@@ -636,6 +636,14 @@ constexpr uint32_t kSRMirror = 64;    // ring[kSR .. kSR+64) mirrors ring[0 .. 6
 #define LZ4MT_RING_RT 0
 #endif
 constexpr bool kRingRT = LZ4MT_RING_RT != 0;
+// LZ4MT_CAND_PF (A/B): right after the table probe, every lane whose
+// candidate passed the tag test loads its candidate's word, so the stop's
+// round trip finds the candidate's line on chip (1: the candidate words; 2:
+// the other lanes also touch the first such candidate's line before it and
+// the line its forward count ends in)
+#ifndef LZ4MT_CAND_PF
+#define LZ4MT_CAND_PF 0
+#endif
 #ifndef LZ4MT_NOSTORE_TEST
 #define LZ4MT_NOSTORE_TEST 0
 #endif
@@ -990,6 +998,16 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         uint64_t mm = cokM & bal((told >> G::PB) == (mark >> G::PB));
         bool maybe = __builtin_amdgcn_inverse_ballot_w64(mm);
         uint64_t sm = mm | tmk;
+#if LZ4MT_CAND_PF
+        uint32_t pfw = 0;
+        if (!LINK && mm) {
+            const uint32_t c0 = rdlane(cand, (int)sff1(mm));
+            uint32_t a = c0;
+            if (LZ4MT_CAND_PF >= 2) a = (L & 1) ? c0 + 4 * kCountLanes + 4 : (c0 > 64 ? c0 - 64 : 0u);
+            a = maybe ? cand : a;
+            pfw = gld4u(s + (a < last4 ? a : last4));
+        }
+#endif
         STAMP_ADD(0, ts);
         // ---- resolve the first stop.  Exact in-window predecessors are
         // resolved (once) whenever a collision reaches the current stop
@@ -1095,6 +1113,9 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             havePe = false;
         }
         if (!twDone) table_writes(w, wTerm);
+#if LZ4MT_CAND_PF
+        asm volatile("" ::"v"(pfw));   // (the early loads retire before the window ends)
+#endif
         STAMP_ADD(1, ts);
         STAMP_ADD(2, ts);
         if (w == 64) {   // no stop: the search goes on
