@@ -27,6 +27,8 @@
 #include <cstdlib>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <atomic>
 #include <condition_variable>
 #include <deque>
@@ -433,8 +435,23 @@ thread_local SlotCache g_slots;
 // more input (S not launched) and sets *stop to end after a launched batch;
 // finish(S) returns false to stop the frame (later batches are drained
 // without writes).
+// LZ4MT_AMD_PIPE_TRACE=1: one stderr line per batch (ms since the call
+// began: fill start / launched, finish start / done) -- the e2e timeline
+bool pipe_trace() {
+    static const bool on = getenv("LZ4MT_AMD_PIPE_TRACE") && atoi(getenv("LZ4MT_AMD_PIPE_TRACE")) != 0;
+    return on;
+}
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 template <class Fill, class Finish>
 void run_slot_pipeline(Session& s, int nSlots, Fill fill, Finish finish) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const bool tr = pipe_trace();
+    std::vector<double> tFill0(kSlots), tFill1(kSlots);
+    int seqNo = 0;
+    std::vector<int> slotSeq(kSlots);
     SlotCache& C = g_slots;
     std::mutex mu;
     std::condition_variable cv;
@@ -455,8 +472,12 @@ void run_slot_pipeline(Session& s, int nSlots, Fill fill, Finish finish) {
             {
                 bool f;
                 { std::lock_guard<std::mutex> g(mu); f = failed; }
+                const double a = tr ? ms_since(t0) : 0;
                 if (f) { hipStreamSynchronize(S.st); okS = false; }
                 else okS = finish(S);
+                if (tr)
+                    fprintf(stderr, "pipe batch %d blocks %llu: fill %.1f-%.1f ms, finish %.1f-%.1f ms\n", slotSeq[i],
+                            (unsigned long long)S.nb, tFill0[i], tFill1[i], a, ms_since(t0));
             }
             {
                 std::lock_guard<std::mutex> g(mu);
@@ -476,7 +497,9 @@ void run_slot_pipeline(Session& s, int nSlots, Fill fill, Finish finish) {
         }
         if (s.error()) break;
         bool stop = false;
+        if (tr) tFill0[head] = ms_since(t0);
         if (!fill(S, &stop)) break;
+        if (tr) { tFill1[head] = ms_since(t0); slotSeq[head] = seqNo++; }
         {
             std::lock_guard<std::mutex> g(mu);
             S.busy = true;

@@ -10,6 +10,7 @@
 #include <cerrno>
 #include <fcntl.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -28,7 +29,15 @@
 
 namespace {
 constexpr size_t kParMin = 2u << 20;     // smaller transfers stay on the caller
-constexpr size_t kPiece = 1u << 20;      // at least 1 MiB per piece
+
+// LZ4MT_AMD_COPY_THREADS / LZ4MT_AMD_COPY_PIECE_KIB: the copy pool's width
+// (caller included) and the smallest piece a transfer is split into
+size_t env_size(const char* name, size_t dflt, size_t lo, size_t hi) {
+    const char* e = getenv(name);
+    const long long v = e ? atoll(e) : (long long)dflt;
+    return v < (long long)lo ? lo : ((size_t)v > hi ? hi : (size_t)v);
+}
+const size_t kPiece = env_size("LZ4MT_AMD_COPY_PIECE_KIB", 1024, 64, 1 << 20) << 10;
 
 // Persistent helper threads; run(n, f) calls f(0..n-1) on the helpers and
 // the caller and returns when all are done.  Safe for concurrent callers
@@ -59,7 +68,8 @@ class CopyPool {
 
     CopyPool() {
         const unsigned hw = std::thread::hardware_concurrency();
-        const unsigned nt = std::min(7u, hw > 1 ? hw - 1 : 0u);
+        const unsigned want = (unsigned)env_size("LZ4MT_AMD_COPY_THREADS", 8, 1, 64);
+        const unsigned nt = std::min(want - 1, hw > 1 ? hw - 1 : 0u);
         for (unsigned i = 0; i < nt; ++i) th_.emplace_back([this] { loop(); });
     }
     ~CopyPool() {

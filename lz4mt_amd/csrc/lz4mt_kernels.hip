@@ -644,6 +644,12 @@ constexpr bool kRingRT = LZ4MT_RING_RT != 0;
 #ifndef LZ4MT_CAND_PF
 #define LZ4MT_CAND_PF 0
 #endif
+// LZ4MT_IP_RING (A/B): the round trip's ip-side words and catch-up bytes from
+// the LDS source ring whenever they lie in it (only the candidate side goes
+// to global memory)
+#ifndef LZ4MT_IP_RING
+#define LZ4MT_IP_RING 0
+#endif
 #ifndef LZ4MT_NOSTORE_TEST
 #define LZ4MT_NOSTORE_TEST 0
 #endif
@@ -1082,6 +1088,11 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                         iw = *(const l_u32u*)(V.r + ((ii < last4 ? ii : last4) & (kSR - 1)));
                         bi = V.r[(bOn ? ip - L - 1 : ip - 1) & (kSR - 1)];
                         bc = V.r[(bOn ? cd - L - 1 : cd - 1) & (kSR - 1)];
+                    } else if (LZ4MT_IP_RING && ip >= V.B + kCatchLanes && ip + 4 * kCountLanes + 4 <= V.B + kSR) {
+                        cw = xld4(ci < last4 ? ci : last4);
+                        bc = xld1(bOn ? cd - L - 1 : o0);
+                        iw = *(const l_u32u*)(V.r + ((ii < last4 ? ii : last4) & (kSR - 1)));
+                        bi = V.r[(bOn ? ip - L - 1 : ip - 1) & (kSR - 1)];
                     } else {
                         cw = xld4(ci < last4 ? ci : last4);
                         iw = gld4u(s + (ii < last4 ? ii : last4));
