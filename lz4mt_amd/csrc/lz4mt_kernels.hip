@@ -3198,7 +3198,18 @@ hipError_t launch_decode(const uint8_t* frame, const BlockRec* recs, uint32_t nB
 __device__ __forceinline__ uint32_t xround(uint32_t acc, uint32_t w) { return rotl32(acc + w * kP2, 13) * kP1; }
 // a round on a word premultiplied by P2 (LLVM fuses the multiply with the
 // next round's add into one v_mad_u64_u32: the chain is alignbit + mad)
-__device__ __forceinline__ uint32_t xround_pm(uint32_t acc, uint32_t wp) { return rotl32(acc + wp, 13) * kP1; }
+// LZ4MT_XXH_NOFUSE (A/B): keep the multiply a v_mul_lo_u32 and the next add
+// a v_add_u32 instead of the fused 64-bit v_mad_u64_u32
+#ifndef LZ4MT_XXH_NOFUSE
+#define LZ4MT_XXH_NOFUSE 0
+#endif
+__device__ __forceinline__ uint32_t xround_pm(uint32_t acc, uint32_t wp) {
+    uint32_t m = rotl32(acc + wp, 13) * kP1;
+#if LZ4MT_XXH_NOFUSE
+    asm volatile("" : "+v"(m));
+#endif
+    return m;
+}
 // LZ4MT_XXH_FULL: a whole 1 KiB chunk's LDS reads in flight before its 64
 // rounds (k_xxh32_stored 4.05 -> 3.78 ms at 8 GiB; profiles/r03n_xxh32_ab.txt)
 #ifndef LZ4MT_XXH_FULL
