@@ -138,7 +138,7 @@ for step in "$@"; do
       done
       cat "$out/ab_bid.txt" ;;
     fuzz)   # time-boxed random differential campaign (seed 7) against the oracle / liblz4
-      timeout -k 10 420 python3 -u tools/fuzz_campaign.py 300 7 > "$out/fuzz.txt" 2>&1
+      timeout -k 10 420 python3 -u tools/fuzz_campaign.py 300 ${FUZZ_SEED:-7} > "$out/fuzz.txt" 2>&1
       tail -2 "$out/fuzz.txt" ;;
     sweep)   # secondary configs: block sizes, 32 GiB decompress-only, default flags, HC level 9, -BD B7
       for spec in "b4 --block-id 4 --steps 5 --warmup 2" "b5 --block-id 5 --steps 5 --warmup 2" \
