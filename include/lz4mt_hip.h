@@ -212,6 +212,11 @@ int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, 
  * points of a split parse, tools/occ_sweep.py).  d_slots: nb x blockSize +
  * 64 bytes, d_csize: nb int32.  Asynchronous; 0, or -1 on bad arguments. */
 int lz4mtHipDebugEncode(const void* d_src, uint64_t n, uint32_t blockSize, void* d_slots, void* d_csize, void* stream);
+/* 1 when the current device applies one wave's same-address LDS exchanges
+ * in ascending lane order (what the block encoder's table probe relies on;
+ * checked once per device before the first encode, which fails with an
+ * error when it does not hold), 0 when it does not, -1 without a device. */
+int lz4mtHipCheckEncoderOrder(void);
 /* The parse work of a split parse: n bytes in streams of S bytes, stream b
  * parsed from ov bytes before its start (the overlap a join needs), S + ov
  * <= 4 MiB, into d_slots (nb x (S + ov) + 64 bytes), sizes into d_csize;

@@ -131,6 +131,7 @@ PROTOTYPES = {
     "lz4mtHipShardBodyBytes": (c_uint64, [c_uint64, SD_P, c_void_p, c_uint64, c_void_p]),
     "lz4mtHipDebugEncodeStats": (c_int, [c_void_p, c_uint64, c_uint32, ctypes.POINTER(c_uint64), c_void_p]),
     "lz4mtHipDebugEncode": (c_int, [c_void_p, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p]),
+    "lz4mtHipCheckEncoderOrder": (c_int, []),
     "lz4mtHipDebugEncodeOverlap": (c_int, [c_void_p, c_uint64, c_uint32, c_uint32, c_int, c_void_p, c_void_p, c_void_p]),
     "lz4mtDebugBdPlan": (c_int, [c_int, c_int, c_void_p, c_uint64, c_void_p]),
     "lz4mtHipDebugFetchCal": (c_int, [c_void_p, c_uint64, c_int, c_void_p, c_void_p]),

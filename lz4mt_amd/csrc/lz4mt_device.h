@@ -81,6 +81,9 @@ struct AuxStream {
 };
 
 // ---- kernel launchers (lz4mt_kernels.hip) ----
+// once per device, before the first block-encoder launch: the LDS exchange
+// order the encoder's table probe relies on (k_xchg_order)
+hipError_t encoder_ready(hipStream_t st);
 hipError_t launch_encode_overlap(const uint8_t* src, uint64_t srcSize, uint32_t S, uint32_t ov, bool p17,
                                  uint8_t* slots, int32_t* csize, hipStream_t st);
 hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,

@@ -20,9 +20,12 @@
 // while the parse state lives in wave-uniform registers.  The hash table
 // (16 KiB) and the decoder's history ring (16 KiB) sit in LDS.
 #include "lz4mt_device.h"
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 
 // LZ4MT_PART splits this file into two objects so each half gets its own
 // scheduler flags (Makefile): 1 = everything but the decoder kernels,
@@ -650,6 +653,15 @@ constexpr bool kRingRT = LZ4MT_RING_RT != 0;
 #ifndef LZ4MT_IP_RING
 #define LZ4MT_IP_RING 0
 #endif
+// LZ4MT_ENC_XCHG: the u32 table probe as ONE LDS exchange per lane
+// (ds_wrxchg_rtn_b32).  A wave's same-address exchanges take effect in
+// ascending lane order (tools/probe/lds_xchg_order.hip: 6.4 M lanes, every
+// one), lanes are in position order, so each lane gets exactly the entry
+// LZ4's sequential inserts leave for it -- its in-window predecessor's mark,
+// or the table's entry -- with no readback and no predecessor resolution.
+#ifndef LZ4MT_ENC_XCHG
+#define LZ4MT_ENC_XCHG 1
+#endif
 #ifndef LZ4MT_NOSTORE_TEST
 #define LZ4MT_NOSTORE_TEST 0
 #endif
@@ -754,6 +766,10 @@ template <bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false> str
         if (SP) { T16()[i] = (uint16_t)e; TG()[i] = (uint8_t)(e >> 16); } else T[i] = e;
     }
     __device__ __forceinline__ uint32_t rb(uint32_t i) const { return SP ? (uint32_t)T16()[i] : T[i]; }
+    // (u32 entries only) store e, return the entry it replaced
+    __device__ __forceinline__ uint32_t xchg(uint32_t i, uint32_t e) const {
+        return __hip_atomic_exchange(T + i, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
     static constexpr uint32_t kRbMask = SP ? 0xFFFFu : 0xFFFFFFFFu;
     // P17: at T (a multiple of 32 KiB, every table write so far below T +
     // 32 KiB, every live entry at or above T - 96 KiB): entries more than
@@ -857,7 +873,7 @@ __device__ __forceinline__ void store_pend(const PendSeq& p, const SrcRing& V, g
 constexpr uint32_t kPubShift = 16;   // publish every 64 KiB of output
 // pub[b] at the end of block b: the stored size | kPubDone, or kPubDone |
 // kPubRaw when the block is stored raw (its source bytes are the payload)
-constexpr uint32_t kPubDone = 0x80000000u, kPubRaw = 0x40000000u, kPubLen = 0x3FFFFFFFu;
+[[maybe_unused]] constexpr uint32_t kPubDone = 0x80000000u, kPubRaw = 0x40000000u, kPubLen = 0x3FFFFFFFu;
 __device__ __forceinline__ void publish_progress(uint32_t* pub, uint32_t v) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -877,6 +893,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                                    LinkArgs lk = LinkArgs{0, 0, 0, true}, uint32_t* pub = nullptr) {
     using G = V5Geo<U16, SPLIT, LINK, P17>;
     const G tab{T};
+    constexpr bool XCHG = LZ4MT_ENC_XCHG != 0 && !G::SP;
     const uint32_t L = laneid();
     uint64_t ts = STAMP_T();
     const uint32_t o0 = LINK ? kLinkO0 : 0u;   // position of the block's first byte
@@ -992,11 +1009,17 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         const uint32_t mark = (P17 ? p & G::PM : p) | (G::tag(w0) << G::PB);   // the lane's final table entry
         // ---- table probe: read, write the marker, read back (LDS ops of a wave run in order)
         const uint32_t ti = live ? h : dumIdx;
-        const uint32_t told = tab.ld(ti);
-        tab.st(ti, mark);
-        WAVE_SYNC();
-        const uint32_t sv = tab.rb(ti);
-        const uint64_t pend = bal(sv != (mark & G::kRbMask));   // same-bucket collision inside the window
+        uint32_t told;
+        uint64_t pend = 0;   // same-bucket collisions inside the window (XCHG: none to resolve)
+        if constexpr (XCHG) {
+            told = tab.xchg(ti, mark);
+        } else {
+            told = tab.ld(ti);
+            tab.st(ti, mark);
+            WAVE_SYNC();
+            const uint32_t sv = tab.rb(ti);
+            pend = bal(sv != (mark & G::kRbMask));
+        }
         const uint32_t dq = (p - told) & G::PM;   // P17: the distance, exact below 2^17
         uint32_t cand = P17 ? p - dq : told & G::PM;
         const uint64_t cokM = bal((P17 ? dq <= kDistMax : cand + kDistMax >= p) && (!LINK || cand >= lk.candLow)) &
@@ -1029,11 +1052,23 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         auto table_writes = [&](uint32_t ws, bool wsTerm) {
             const int wlim = (ws == 64) ? 63 : (wsTerm ? (int)ws - 1 : (int)ws);
             const bool le = (int)L <= wlim;
-            tab.st((live && !le) ? h : dumIdx, told);
-            if (pend || twRedo) {
-                const uint64_t upto = wlim < 0 ? 0ull : mask_le((uint32_t)wlim);
-                const bool lastM = !dd || !(gmask & ~mask_le(L) & upto);
-                tab.st((live && le && lastM) ? h : dumIdx, mark);
+            if constexpr (XCHG) {
+                // after an alias moved the stop: the lanes up to it insert again
+                // (exchanges, so the last of each bucket wins)
+                if (twRedo) (void)tab.xchg((live && le) ? h : dumIdx, mark);
+                // lanes past the stop: the first of each bucket puts back the
+                // entry it displaced (the last mark up to the stop, or the
+                // table's entry); a later one displaced a lane past the stop
+                const uint64_t past = liveM & ~(wlim < 0 ? 0ull : mask_le((uint32_t)wlim));
+                const uint32_t pfl = rdlane(p, (int)sff1(past | (1ull << 63)));
+                tab.st((live && !le && (told & G::PM) < pfl) ? h : dumIdx, told);
+            } else {
+                tab.st((live && !le) ? h : dumIdx, told);
+                if (pend || twRedo) {
+                    const uint64_t upto = wlim < 0 ? 0ull : mask_le((uint32_t)wlim);
+                    const bool lastM = !dd || !(gmask & ~mask_le(L) & upto);
+                    tab.st((live && le && lastM) ? h : dumIdx, mark);
+                }
             }
             WAVE_SYNC();
         };
@@ -1299,8 +1334,80 @@ __global__ void __launch_bounds__(64) k_encode_pub(const uint8_t* __restrict__ s
     publish_progress(pub + b, kPubDone | (r > 0 ? (uint32_t)r : kPubRaw));   // the block is final
 }
 
+// The XCHG table probe relies on one wave's same-address LDS exchanges
+// taking effect in ascending lane order.  k_xchg_order checks it on the
+// device in use (three address patterns, one wave): *ok = 1 when every
+// lane got its lower same-address neighbour's value (or the initial one)
+// and every word ends with its highest lane's value.
+__global__ void __launch_bounds__(64) k_xchg_order(uint32_t* ok) {
+    __shared__ uint32_t W[64];
+    const uint32_t L = laneid();
+    bool good = true;
+    for (uint32_t pat = 0; pat < 3; ++pat) {
+        W[L] = 0xFFFF0000u | L;
+        WAVE_SYNC();
+        const uint32_t a = pat == 0 ? 0u : pat == 1 ? (L & 3u) : (L * 37u) % 7u;
+        const uint32_t got = __hip_atomic_exchange((l_u32*)W + a, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        WAVE_SYNC();
+        uint32_t want = 0xFFFF0000u | a, last = 64;
+        for (uint32_t j = 0; j < 64; ++j) {   // (uniform loop: every lane walks the pattern)
+            const uint32_t aj = pat == 0 ? 0u : pat == 1 ? (j & 3u) : (j * 37u) % 7u;
+            if (aj == a && j < L) want = j;
+            if (aj == L) last = j;
+        }
+        good = good && got == want && (last == 64 || W[L] == last);
+        WAVE_SYNC();
+    }
+    const bool all = __builtin_amdgcn_ballot_w64(!good) == 0;
+    if (L == 0) *ok = all ? 1u : 0u;
+}
+
+// once per device: hipSuccess when the check passed (or the encoder does not
+// use exchanges), hipErrorNotSupported (and one stderr line) when it failed.
+// A call whose stream is being captured into a graph skips the check until
+// an uncaptured call runs it.
+hipError_t encoder_ready(hipStream_t st) {
+    if (!LZ4MT_ENC_XCHG) return hipSuccess;
+    static std::atomic<int> state[64];   // 0 unchecked, 1 passed, -1 failed
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    const int v = state[dev].load(std::memory_order_acquire);
+    if (v) return v > 0 ? hipSuccess : hipErrorNotSupported;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (st && hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return hipSuccess;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> g(mu);
+    if (state[dev].load()) return state[dev].load() > 0 ? hipSuccess : hipErrorNotSupported;
+    hipStream_t ps = nullptr;
+    uint32_t* d = nullptr;
+    uint32_t h = 0;
+    hipError_t e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&d, 4);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_xchg_order, dim3(1), dim3(64), 0, ps, d);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, d, 4, hipMemcpyDeviceToHost, ps);
+    if (e == hipSuccess) e = hipStreamSynchronize(ps);
+    if (d) hipFree(d);
+    if (ps) hipStreamDestroy(ps);
+    if (e != hipSuccess) return e;
+    state[dev].store(h == 1 ? 1 : -1, std::memory_order_release);
+    if (h != 1)
+        fprintf(stderr, "lz4mt_amd: device %d does not apply a wave's same-address LDS exchanges in lane order; "
+                        "the block encoder (LZ4MT_ENC_XCHG) cannot run here\n", dev);
+    return h == 1 ? hipSuccess : hipErrorNotSupported;
+}
+
+extern "C" int lz4mtHipCheckEncoderOrder(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -1;
+    return encoder_ready(nullptr) == hipSuccess ? 1 : 0;
+}
+
 hipError_t launch_encode_pub(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                              uint8_t* slots, int32_t* csize, uint32_t* pub, hipStream_t st) {
+    if (const hipError_t r = encoder_ready(st); r != hipSuccess) return r;
     if (nBlocks == 0) return hipSuccess;
     hipLaunchKernelGGL(k_encode_pub, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots,
                        (uint64_t)blockSize, csize, pub);
@@ -1441,6 +1548,7 @@ __global__ void __launch_bounds__(64) k_encode_linked(const uint8_t* __restrict_
 hipError_t launch_encode_linked(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                                 uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh, bool xh,
                                 int32_t* csize, hipStream_t st) {
+    if (const hipError_t r = encoder_ready(st); r != hipSuccess) return r;
     if (nBlocks == 0) return hipSuccess;
     hipLaunchKernelGGL(xh ? k_encode_linked<true> : k_encode_linked<false>, dim3(1), dim3(64), 0, st, src, srcSize,
                        blockSize, nBlocks, slots, plan, table, fresh ? 1 : 0, csize, (const uint32_t*)nullptr,
@@ -1687,6 +1795,7 @@ uint64_t link_round_bytes(uint64_t nBlocks) {
 hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                                     uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh, bool xh,
                                     uint32_t* scratch, int32_t* csize, int rounds, hipStream_t st) {
+    if (const hipError_t r = encoder_ready(st); r != hipSuccess) return r;
     if (nBlocks == 0) return hipSuccess;
     if (rounds < 1 || rounds > kLinkRounds) rounds = kLinkRounds;
     uint32_t* entry = scratch;
@@ -1737,15 +1846,17 @@ hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32
     return hipGetLastError();
 }
 
-// k_encode_p17 for 256 KiB blocks (11 waves per CU pay for the split table
-// there: 161 -> 151 ms at 8 GiB; at 1 / 4 MiB blocks the 7-bit tags' extra
-// round trips cost more than the occupancy gains, profiles/r02_p17_ab.txt);
-// LZ4MT_AMD_ENC=p17 / base forces one (A/B)
+// k_encode_p17 (the 3-byte table, 11 waves per CU) paid for 256 KiB blocks
+// while k_encode resolved in-window collisions by readback (161 -> 151 ms at
+// 8 GiB, profiles/r02_p17_ab.txt); k_encode's exchange probe (XCHG, which
+// the split u16 + u8 table cannot use) is faster at every block size now:
+// B5 8 GiB 45.6 vs 43.3 GiB/s (profiles/r04y_xchg_sweep/).  LZ4MT_AMD_ENC=p17
+// / base forces one (A/B)
 static bool enc_p17(uint32_t blockSize) {
     const char* e = getenv("LZ4MT_AMD_ENC");
     if (e && !strcmp(e, "p17")) return true;
     if (e && !strcmp(e, "base")) return false;
-    return blockSize <= (256u << 10);
+    return !LZ4MT_ENC_XCHG && blockSize <= (256u << 10);
 }
 
 // The parse work of a split parse (timing only): stream b of S
@@ -1777,6 +1888,7 @@ __global__ void __launch_bounds__(64) k_encode_overlap(const uint8_t* __restrict
 
 hipError_t launch_encode_overlap(const uint8_t* src, uint64_t srcSize, uint32_t S, uint32_t ov, bool p17,
                                  uint8_t* slots, int32_t* csize, hipStream_t st) {
+    if (const hipError_t r = encoder_ready(st); r != hipSuccess) return r;
     const uint32_t nb = (uint32_t)((srcSize + S - 1) / S);
     if (nb == 0) return hipSuccess;
     if (p17) hipLaunchKernelGGL(k_encode_overlap<true>, dim3(nb), dim3(64), 0, st, src, srcSize, S, ov, slots, csize);
@@ -1794,6 +1906,7 @@ static uint32_t enc_lds_pad() {
 
 hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks, uint8_t* slots,
                          uint64_t slotStride, uint32_t capOverride, int32_t* csize, hipStream_t st) {
+    if (const hipError_t r = encoder_ready(st); r != hipSuccess) return r;
     if (nBlocks == 0) return hipSuccess;
     const uint32_t pad = enc_lds_pad();
     if (blockSize < (uint32_t)kLimit64K)
@@ -3174,6 +3287,7 @@ hipError_t launch_decode_stats(const uint8_t* frame, const BlockRec* recs, uint3
 #if LZ4MT_PART != 2
 hipError_t launch_encode_stats(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                                uint8_t* slots, int32_t* csize, uint64_t* stats, hipStream_t st) {
+    if (const hipError_t r = encoder_ready(st); r != hipSuccess) return r;
     hipLaunchKernelGGL(k_encode_stats, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots,
                        (uint64_t)blockSize, csize, stats);
     return hipGetLastError();

@@ -45,6 +45,31 @@ def host(t):
     return bytes(t.cpu().numpy().tobytes())
 
 
+def test_p17_encoder_forced_matches_default(monkeypatch):
+    """k_encode_p17 (the 3-byte table) is no longer the default at any block
+    size but stays selectable (LZ4MT_AMD_ENC=p17): forced, it writes the
+    frame the default k_encode writes, byte for byte (B5 and B6)."""
+    src = L.gen_synthetic(12 << 20, seed=5, device="cuda")
+    for bid in (5, 6):
+        sd = L.make_sd(bid, stream_checksum=False, block_checksum=True)
+        want = host(L.compress_frame(src, sd))
+        monkeypatch.setenv("LZ4MT_AMD_ENC", "p17")
+        got = host(L.compress_frame(src, sd))
+        monkeypatch.delenv("LZ4MT_AMD_ENC")
+        assert got == want, bid
+    data = host(src[:(3 << 20) + 12345])
+    sd = L.make_sd(5, stream_checksum=True, block_checksum=True)
+    assert host(L.compress_frame(dev(data), sd)) == oracle.compress_frame(data, oracle.params(5, True, True))
+
+
+def test_encoder_lds_exchange_order():
+    """The block encoder's table probe (LZ4MT_ENC_XCHG) takes each lane's
+    candidate from one LDS exchange, which is LZ4's sequential insert order
+    only if a wave's same-address exchanges apply in ascending lane order;
+    the library checks that once per device before the first encode."""
+    assert L.lib.lz4mtHipCheckEncoderOrder() == 1
+
+
 # ---------------------------------------------------------------------------
 # block operators (reference plugin signatures)
 # ---------------------------------------------------------------------------
