@@ -662,6 +662,13 @@ constexpr bool kRingRT = LZ4MT_RING_RT != 0;
 #ifndef LZ4MT_ENC_XCHG
 #define LZ4MT_ENC_XCHG 1
 #endif
+// LZ4MT_ENC_LATE (A/B): a sequence's layout (extension lengths, the output
+// offset, limitedOutput's margin checks) is worked out in the NEXT window's
+// round-trip shadow, just before its bytes are stored, instead of between
+// the forward count and the next window's probe
+#ifndef LZ4MT_ENC_LATE
+#define LZ4MT_ENC_LATE 0
+#endif
 #ifndef LZ4MT_NOSTORE_TEST
 #define LZ4MT_NOSTORE_TEST 0
 #endif
@@ -802,6 +809,7 @@ template <bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false> str
 // (few loop-carried fields; the layout is derived at store time)
 struct PendSeq {
     uint32_t op, lit, mcf, off, anchor;
+    bool test;   // (LZ4MT_ENC_LATE) the match was found by the TEST lane: no literal margin check
 };
 struct SeqLayout {
     uint32_t total, a1, a2, token, litRem, mlRem, off;
@@ -948,6 +956,28 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     uint32_t anchor = o0, op = 0;
     PendSeq pe{};
     bool havePe = false;
+    bool done = false, fail = false;
+    // LZ4MT_ENC_LATE: the pending sequence's layout, right before its store;
+    // false when limitedOutput's margins fail (the block is then stored raw)
+    auto settle = [&]() -> bool {
+        const uint32_t litExt = ext_len(pe.lit), mlExt = ext_len(pe.mcf);
+        if (op + 2 * (pe.lit + pe.mcf) + 16 > capL) {
+            if ((!pe.test && op + 1 + pe.lit + 8 + pe.lit / 255 > cap) ||
+                (op + 1 + litExt + pe.lit + 2 + 6 + (pe.mcf + 240) / 255 > cap))
+                return false;
+        }
+        pe.op = op;
+        if constexpr (PUB) {   // every sequence before this one has been stored: [0, op) is final
+            if ((op ^ (op + 1 + litExt + pe.lit + 2 + mlExt)) >> kPubShift) publish_progress(pub, op);
+        }
+        op += 1 + litExt + pe.lit + 2 + mlExt;
+        return true;
+    };
+    auto store_pending = [&]() {
+        if (!LZ4MT_ENC_LATE || settle()) store_pend(pe, V, s, d);
+        else fail = true;
+        havePe = false;
+    };
     // window: lane 0 INSERT insPos, lane 1 TEST testPos, lane L >= 2 SEARCH
     // probe k0 + L - 2 (at sBase + F(k) - F(k0), sBase = first search position)
     // window state: sBase, k0 (+ s0, j1 derived from it) and the mode
@@ -957,7 +987,6 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     uint32_t nextSweep = 32768;   // P17
     // ONE exit and no continue: the structurizer then needs no flow
     // variables and the loop-carried state stays in place across windows
-    bool done = false, fail = false;
     while (!done) {
       // windows without a stop (continuations) loop here, inside: the
       // match-path state (anchor, op, pe) is not touched by them
@@ -1134,10 +1163,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                         bi = s[bOn ? ip - L - 1 : o0];   // (o0: a byte of the block itself)
                         bc = xld1(bOn ? cd - L - 1 : o0);
                     }
-                    if (havePe) {
-                        store_pend(pe, V, s, d);
-                        havePe = false;
-                    }
+                    if (havePe) store_pending();
                     table_writes(w, false);   // in the round trip's shadow; redone if w moves
                     twDone = true;
                     if (((mm >> w) & 1) && rdlane(cw, 0) != rdlane(w0, (int)w)) {   // tag alias: no match here
@@ -1154,10 +1180,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                 }
             }
         }
-        if (havePe) {
-            store_pend(pe, V, s, d);
-            havePe = false;
-        }
+        if (havePe) store_pending();
         if (!twDone) table_writes(w, wTerm);
 #if LZ4MT_CAND_PF
         asm volatile("" ::"v"(pfw));   // (the early loads retire before the window ends)
@@ -1171,8 +1194,8 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             j1 = (k0 < 65 ? 65u : ((k0 - 1) & ~63u) + 65) - k0;
             mode = 0;
         }
-      } while (w == 64);
-        if (wTerm) {
+      } while (w == 64 && !(LZ4MT_ENC_LATE && fail));
+        if (wTerm || (LZ4MT_ENC_LATE && fail)) {
             done = true;
         } else {
             // ---- catch-up (backwards) and LZ4_count (forwards from ip + 4).
@@ -1223,23 +1246,28 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             STAMP_ADD(3, ts);
             // ---- sequence layout (stored during the next round trip)
             const uint32_t lit = ip - anchor - back, mcf = mc + back;
-            const uint32_t litExt = ext_len(lit), mlExt = ext_len(mcf);
-            // 1.9.3's limitedOutput margins; both hold whenever
-            // op + 2 (lit + mcf) + 16 <= cap, so the exact test runs rarely
-            if (op + 2 * (lit + mcf) + 16 > capL) {
-                fail = (w != 1 && op + 1 + lit + 8 + lit / 255 > cap) ||
-                       (op + 1 + litExt + lit + 2 + 6 + (mcf + 240) / 255 > cap);
-            }
-            pe.op = op;
             pe.lit = lit;
             pe.mcf = mcf;
             pe.off = ip - cd;
             pe.anchor = anchor;
-            havePe = !fail;
-            if constexpr (PUB) {   // every sequence before this one has been stored: [0, op) is final
-                if ((op ^ (op + 1 + litExt + lit + 2 + mlExt)) >> kPubShift) publish_progress(pub, op);
+            pe.test = w == 1;
+            if (LZ4MT_ENC_LATE) {
+                havePe = true;
+            } else {
+                const uint32_t litExt = ext_len(lit), mlExt = ext_len(mcf);
+                // 1.9.3's limitedOutput margins; both hold whenever
+                // op + 2 (lit + mcf) + 16 <= cap, so the exact test runs rarely
+                if (op + 2 * (lit + mcf) + 16 > capL) {
+                    fail = (w != 1 && op + 1 + lit + 8 + lit / 255 > cap) ||
+                           (op + 1 + litExt + lit + 2 + 6 + (mcf + 240) / 255 > cap);
+                }
+                pe.op = op;
+                havePe = !fail;
+                if constexpr (PUB) {   // every sequence before this one has been stored: [0, op) is final
+                    if ((op ^ (op + 1 + litExt + lit + 2 + mlExt)) >> kPubShift) publish_progress(pub, op);
+                }
+                op += 1 + litExt + lit + 2 + mlExt;
             }
-            op += 1 + litExt + lit + 2 + mlExt;
             const uint32_t ipe = ip + kMinMatch + mc;
             anchor = ipe;
             done = fail || ipe >= mflimitP1;
@@ -1252,7 +1280,10 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         }
     }
     if (fail) return 0;
-    if (havePe) store_pend(pe, V, s, d);
+    if (havePe) {
+        store_pending();
+        if (fail) return 0;
+    }
     // ---- last literals
     {
         const uint32_t run = n - anchor;
