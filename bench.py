@@ -234,11 +234,12 @@ def pmc_traffic(kernel, n, bm, flg):
 
 def frame_encoder(bm):
     """The kernel lz4mtHipCompressFrameAsyncEx runs for bm-byte blocks
-    (launch_encode, lz4mt_kernels.hip): the byU16 table below 65 547 B, else
-    k_encode (LZ4MT_AMD_ENC=p17 forces the 3-byte table)."""
+    (launch_encode, lz4mt_kernels.hip): the byU16 table below 65 547 B, the
+    3-byte table at 256 KiB (LZ4MT_AMD_ENC overrides), else k_encode."""
+    enc = os.environ.get("LZ4MT_AMD_ENC", "")
     if bm < 65547:
         return "k_encode16"
-    if os.environ.get("LZ4MT_AMD_ENC", "") == "p17":
+    if enc == "p17" or (enc != "base" and bm <= (256 << 10)):
         return "k_encode_p17"
     return "k_encode"
 

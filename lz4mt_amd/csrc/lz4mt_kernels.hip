@@ -669,6 +669,25 @@ constexpr bool kRingRT = LZ4MT_RING_RT != 0;
 #ifndef LZ4MT_ENC_LATE
 #define LZ4MT_ENC_LATE 0
 #endif
+// LZ4MT_ENC_XCHG_SP (A/B): the same exchange probe on the split u16 + u8
+// tables (k_encode16, k_encode_p17): a masked OR with return
+// (ds_mskor_rtn_b32) replaces just the lane's 16-bit position and its tag
+// byte, and is lane-ordered the same way (tools/probe/lds_mskor_order.hip)
+#ifndef LZ4MT_ENC_XCHG_SP
+#define LZ4MT_ENC_XCHG_SP 1
+#endif
+
+// ds_mskor_rtn_b32 on two LDS dwords (one position half, one tag byte): each
+// word becomes (word & ~mask) | data; returns the old words
+__device__ __forceinline__ void mskor2_rtn(l_u32* w16, uint32_t m16, uint32_t d16, l_u32* w8, uint32_t m8,
+                                           uint32_t d8, uint32_t& o16, uint32_t& o8) {
+    asm volatile("ds_mskor_rtn_b32 %0, %2, %3, %4\n\t"
+                 "ds_mskor_rtn_b32 %1, %5, %6, %7\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(o16), "=&v"(o8)
+                 : "v"((uint32_t)(uintptr_t)w16), "v"(m16), "v"(d16), "v"((uint32_t)(uintptr_t)w8), "v"(m8), "v"(d8)
+                 : "memory");
+}
 #ifndef LZ4MT_NOSTORE_TEST
 #define LZ4MT_NOSTORE_TEST 0
 #endif
@@ -773,9 +792,17 @@ template <bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false> str
         if (SP) { T16()[i] = (uint16_t)e; TG()[i] = (uint8_t)(e >> 16); } else T[i] = e;
     }
     __device__ __forceinline__ uint32_t rb(uint32_t i) const { return SP ? (uint32_t)T16()[i] : T[i]; }
-    // (u32 entries only) store e, return the entry it replaced
+    // store e, return the entry it replaced (lane-ordered within a wave)
     __device__ __forceinline__ uint32_t xchg(uint32_t i, uint32_t e) const {
-        return __hip_atomic_exchange(T + i, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        if constexpr (SP) {
+            const uint32_t s16 = (i & 1u) * 16u, s8 = (i & 3u) * 8u;
+            uint32_t o16, o8;
+            mskor2_rtn((l_u32*)T16() + (i >> 1), 0xFFFFu << s16, (e & 0xFFFFu) << s16, (l_u32*)TG() + (i >> 2),
+                       0xFFu << s8, ((e >> 16) & 0xFFu) << s8, o16, o8);
+            return ((o16 >> s16) & 0xFFFFu) | (((o8 >> s8) & 0xFFu) << 16);
+        } else {
+            return __hip_atomic_exchange(T + i, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
     }
     static constexpr uint32_t kRbMask = SP ? 0xFFFFu : 0xFFFFFFFFu;
     // P17: at T (a multiple of 32 KiB, every table write so far below T +
@@ -901,7 +928,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                                    LinkArgs lk = LinkArgs{0, 0, 0, true}, uint32_t* pub = nullptr) {
     using G = V5Geo<U16, SPLIT, LINK, P17>;
     const G tab{T};
-    constexpr bool XCHG = LZ4MT_ENC_XCHG != 0 && !G::SP;
+    constexpr bool XCHG = LZ4MT_ENC_XCHG != 0 && (!G::SP || LZ4MT_ENC_XCHG_SP != 0);
     const uint32_t L = laneid();
     uint64_t ts = STAMP_T();
     const uint32_t o0 = LINK ? kLinkO0 : 0u;   // position of the block's first byte
@@ -1090,7 +1117,9 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                 // table's entry); a later one displaced a lane past the stop
                 const uint64_t past = liveM & ~(wlim < 0 ? 0ull : mask_le((uint32_t)wlim));
                 const uint32_t pfl = rdlane(p, (int)sff1(past | (1ull << 63)));
-                tab.st((live && !le && (told & G::PM) < pfl) ? h : dumIdx, told);
+                // (P17 keeps positions mod 2^17: compare distances from p)
+                const bool first = P17 ? dq > p - pfl : (told & G::PM) < pfl;
+                tab.st((live && !le && first) ? h : dumIdx, told);
             } else {
                 tab.st((live && !le) ? h : dumIdx, told);
                 if (pend || twRedo) {
@@ -1365,11 +1394,12 @@ __global__ void __launch_bounds__(64) k_encode_pub(const uint8_t* __restrict__ s
     publish_progress(pub + b, kPubDone | (r > 0 ? (uint32_t)r : kPubRaw));   // the block is final
 }
 
-// The XCHG table probe relies on one wave's same-address LDS exchanges
-// taking effect in ascending lane order.  k_xchg_order checks it on the
-// device in use (three address patterns, one wave): *ok = 1 when every
-// lane got its lower same-address neighbour's value (or the initial one)
-// and every word ends with its highest lane's value.
+// The exchange table probes rely on one wave's same-address LDS exchanges
+// (ds_wrxchg_rtn_b32) and masked ORs (ds_mskor_rtn_b32) taking effect in
+// ascending lane order.  k_xchg_order checks it on the device in use (one
+// wave; three exchange address patterns, masked ORs on 16- and 8-bit
+// fields): *ok = 1 when every lane got its lower same-address neighbour's
+// value (or the initial one) and every word ends with its highest lane's.
 __global__ void __launch_bounds__(64) k_xchg_order(uint32_t* ok) {
     __shared__ uint32_t W[64];
     const uint32_t L = laneid();
@@ -1389,6 +1419,24 @@ __global__ void __launch_bounds__(64) k_xchg_order(uint32_t* ok) {
         good = good && got == want && (last == 64 || W[L] == last);
         WAVE_SYNC();
     }
+    // the split tables' masked ORs (16-bit and 8-bit fields of shared dwords)
+    for (uint32_t fb = 16; fb >= 8; fb -= 8) {
+        const uint32_t nf = 32u / fb, fm = (1u << fb) - 1u;
+        W[L] = 0xA5A5A5A5u ^ L;
+        WAVE_SYNC();
+        const uint32_t sel = (L * 5u) % (4u * nf), a = sel / nf, sh = (sel % nf) * fb;
+        uint32_t o16, o8;   // (the second op hits a word no lane reads back)
+        mskor2_rtn((l_u32*)W + a, fm << sh, ((L + 1u) & fm) << sh, (l_u32*)W + 63, 0u, 0u, o16, o8);
+        WAVE_SYNC();
+        uint32_t want = ((0xA5A5A5A5u ^ a) >> sh) & fm, fin = 0xA5A5A5A5u ^ L;
+        for (uint32_t j = 0; j < 64; ++j) {
+            const uint32_t sj = (j * 5u) % (4u * nf), shj = (sj % nf) * fb;
+            if (sj == sel && j < L) want = (j + 1u) & fm;
+            if (sj / nf == L) fin = (fin & ~(fm << shj)) | (((j + 1u) & fm) << shj);
+        }
+        good = good && ((o16 >> sh) & fm) == want && (L >= 4 || W[L] == fin);
+        WAVE_SYNC();
+    }
     const bool all = __builtin_amdgcn_ballot_w64(!good) == 0;
     if (L == 0) *ok = all ? 1u : 0u;
 }
@@ -1398,7 +1446,7 @@ __global__ void __launch_bounds__(64) k_xchg_order(uint32_t* ok) {
 // A call whose stream is being captured into a graph skips the check until
 // an uncaptured call runs it.
 hipError_t encoder_ready(hipStream_t st) {
-    if (!LZ4MT_ENC_XCHG) return hipSuccess;
+    if (!LZ4MT_ENC_XCHG && !LZ4MT_ENC_XCHG_SP) return hipSuccess;
     static std::atomic<int> state[64];   // 0 unchecked, 1 passed, -1 failed
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
@@ -1877,17 +1925,17 @@ hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32
     return hipGetLastError();
 }
 
-// k_encode_p17 (the 3-byte table, 11 waves per CU) paid for 256 KiB blocks
-// while k_encode resolved in-window collisions by readback (161 -> 151 ms at
-// 8 GiB, profiles/r02_p17_ab.txt); k_encode's exchange probe (XCHG, which
-// the split u16 + u8 table cannot use) is faster at every block size now:
-// B5 8 GiB 45.6 vs 43.3 GiB/s (profiles/r04y_xchg_sweep/).  LZ4MT_AMD_ENC=p17
-// / base forces one (A/B)
+// k_encode_p17 (the 3-byte table, 11 waves per CU) for 256 KiB blocks: with
+// the exchange probe on both tables (XCHG, XCHG_SP) it is 134.7 ms per 8 GiB
+// there against k_encode's 141.4; at 1 / 4 MiB blocks k_encode wins (150.2 /
+// 161.5 vs 154.6 / 175.9: the 7-bit tags' extra round trips, and 4 MiB blocks
+// fill only 8 waves per CU anyway; profiles/r04xsp_encoder_split_xchg_ab.txt).
+// LZ4MT_AMD_ENC=p17 / base forces one (A/B)
 static bool enc_p17(uint32_t blockSize) {
     const char* e = getenv("LZ4MT_AMD_ENC");
     if (e && !strcmp(e, "p17")) return true;
     if (e && !strcmp(e, "base")) return false;
-    return !LZ4MT_ENC_XCHG && blockSize <= (256u << 10);
+    return blockSize <= (256u << 10);
 }
 
 // The parse work of a split parse (timing only): stream b of S

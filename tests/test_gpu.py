@@ -45,18 +45,19 @@ def host(t):
     return bytes(t.cpu().numpy().tobytes())
 
 
-def test_p17_encoder_forced_matches_default(monkeypatch):
-    """k_encode_p17 (the 3-byte table) is no longer the default at any block
-    size but stays selectable (LZ4MT_AMD_ENC=p17): forced, it writes the
-    frame the default k_encode writes, byte for byte (B5 and B6)."""
+def test_p17_and_base_encoders_agree(monkeypatch):
+    """k_encode_p17 (the 3-byte table; the default at 256 KiB blocks) and
+    k_encode (the default above) forced either way write the same frames,
+    byte for byte (B5 and B6)."""
     src = L.gen_synthetic(12 << 20, seed=5, device="cuda")
     for bid in (5, 6):
         sd = L.make_sd(bid, stream_checksum=False, block_checksum=True)
         want = host(L.compress_frame(src, sd))
-        monkeypatch.setenv("LZ4MT_AMD_ENC", "p17")
-        got = host(L.compress_frame(src, sd))
-        monkeypatch.delenv("LZ4MT_AMD_ENC")
-        assert got == want, bid
+        for enc in ("p17", "base"):
+            monkeypatch.setenv("LZ4MT_AMD_ENC", enc)
+            got = host(L.compress_frame(src, sd))
+            monkeypatch.delenv("LZ4MT_AMD_ENC")
+            assert got == want, (bid, enc)
     data = host(src[:(3 << 20) + 12345])
     sd = L.make_sd(5, stream_checksum=True, block_checksum=True)
     assert host(L.compress_frame(dev(data), sd)) == oracle.compress_frame(data, oracle.params(5, True, True))
