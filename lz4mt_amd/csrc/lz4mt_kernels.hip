@@ -676,6 +676,13 @@ constexpr bool kRingRT = LZ4MT_RING_RT != 0;
 #ifndef LZ4MT_ENC_XCHG_SP
 #define LZ4MT_ENC_XCHG_SP 1
 #endif
+// LZ4MT_ENC_TIDY (A/B): the window's last-probe offset carried as loop state
+// (61 after every match) instead of recomputed with a saturating VALU
+// subtract + readfirstlane each window; catch-up byte indices materialised
+// as 32-bit offsets (SGPR-base loads, no 64-bit address adds)
+#ifndef LZ4MT_ENC_TIDY
+#define LZ4MT_ENC_TIDY 1
+#endif
 
 // ds_mskor_rtn_b32 on two LDS dwords (one position half, one tag byte): each
 // word becomes (word & ~mask) | data; returns the old words
@@ -1011,6 +1018,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     // (0 continuation: search only; 1 after a match ending at sBase - 1:
     // INSERT sBase - 3, TEST sBase - 1; 2 first window: INSERT 0)
     uint32_t sBase = o0 + 1, k0 = 0, s0 = 1, j1 = 65, mode = 2;
+    uint32_t spanHi = 61;   // (TIDY) 61 * s0 + max(0, 61 - j1): the last SEARCH probe's offset from sBase
     uint32_t nextSweep = 32768;   // P17
     // ONE exit and no continue: the structurizer then needs no flow
     // variables and the loop-carried state stays in place across windows
@@ -1036,14 +1044,17 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         // and 1 wrap j, but take the INSERT / TEST position below)
         uint32_t p = sBase + __umul24(j, s0) + (uint32_t)max(jx, 0);
         const uint32_t step = s0 + (jx >= 0 ? 1u : 0u);
-        const uint32_t sHi = sBase + 61 * s0 + (61 > j1 ? 61 - j1 : 0u);
+        const uint32_t sHi = LZ4MT_ENC_TIDY ? sBase + spanHi : sBase + 61 * s0 + (61 > j1 ? 61 - j1 : 0u);
         const bool insOn = mode != 0, testOn = mode == 1;
         const uint32_t insPos = mode == 2 ? o0 : sBase - 3, testPos = sBase - 1;
         p = L == 0 ? insPos : (L == 1 ? testPos : p);
         // lane predicates as wave masks (SALU), turned back into per-lane
         // conditions with inverse_ballot (the mask is the select's condition):
         // no 0/1 materialisation chains
-        const uint64_t liveM = (bal(p <= mflimitP1) & ~3ull) | (insOn ? 1ull : 0ull) | (testOn ? 2ull : 0ull);
+        // (TIDY: lane 0 / 1's bits straight from the mode -- 2: INSERT only, 1: both)
+        const uint64_t roleM = LZ4MT_ENC_TIDY ? (uint64_t)((0x130u >> (4 * mode)) & 3u)
+                                              : (insOn ? 1ull : 0ull) | (testOn ? 2ull : 0ull);
+        const uint64_t liveM = (bal(p <= mflimitP1) & ~3ull) | roleM;
         const uint64_t tmk = bal(p + step > mflimitP1) & liveM & ~3ull;
         const bool live = __builtin_amdgcn_inverse_ballot_w64(liveM);
         const bool term = __builtin_amdgcn_inverse_ballot_w64(tmk);
@@ -1106,6 +1117,9 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         // back; on a collision (or when redone after a tag alias moved the
         // stop) the lanes up to the stop re-insert (last member of each group)
         auto table_writes = [&](uint32_t ws, bool wsTerm) {
+            // (an SGPR-pinned version of this, w - ((tmk >> w) & 1) under an
+            // asm "+s" constraint, drops a v_readfirstlane but costs 1 ms:
+            // profiles/r04tidy_encoder_ab.txt)
             const int wlim = (ws == 64) ? 63 : (wsTerm ? (int)ws - 1 : (int)ws);
             const bool le = (int)L <= wlim;
             if constexpr (XCHG) {
@@ -1189,8 +1203,10 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                     } else {
                         cw = xld4(ci < last4 ? ci : last4);
                         iw = gld4u(s + (ii < last4 ? ii : last4));
-                        bi = s[bOn ? ip - L - 1 : o0];   // (o0: a byte of the block itself)
-                        bc = xld1(bOn ? cd - L - 1 : o0);
+                        uint32_t bix = bOn ? ip - L - 1 : o0, bcx = bOn ? cd - L - 1 : o0;   // (o0: a byte of the block itself)
+                        if (LZ4MT_ENC_TIDY) asm volatile("" : "+v"(bix), "+v"(bcx));
+                        bi = s[bix];
+                        bc = xld1(bcx);
                     }
                     if (havePe) store_pending();
                     table_writes(w, false);   // in the round trip's shadow; redone if w moves
@@ -1222,6 +1238,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             s0 = (63 + k0) >> 6;   // k0 >= 62: no max(1, .) needed
             j1 = (k0 < 65 ? 65u : ((k0 - 1) & ~63u) + 65) - k0;
             mode = 0;
+            if (LZ4MT_ENC_TIDY) spanHi = 61 * s0 + (61 > j1 ? 61 - j1 : 0u);
         }
       } while (w == 64 && !(LZ4MT_ENC_LATE && fail));
         if (wTerm || (LZ4MT_ENC_LATE && fail)) {
@@ -1305,6 +1322,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             k0 = 0;
             s0 = 1;
             j1 = 65;
+            spanHi = 61;
             STAMP_ADD(4, ts);
         }
     }
