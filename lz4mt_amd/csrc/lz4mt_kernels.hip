@@ -683,6 +683,12 @@ constexpr bool kRingRT = LZ4MT_RING_RT != 0;
 #ifndef LZ4MT_ENC_TIDY
 #define LZ4MT_ENC_TIDY 1
 #endif
+// LZ4MT_ENC_PFR (A/B): the first window after a match gets its hash inputs
+// from a ring read issued at the end of the previous sequence (its positions
+// are known once the match end is), so the LDS latency overlaps the layout
+#ifndef LZ4MT_ENC_PFR
+#define LZ4MT_ENC_PFR 0
+#endif
 
 // ds_mskor_rtn_b32 on two LDS dwords (one position half, one tag byte): each
 // word becomes (word & ~mask) | data; returns the old words
@@ -1019,6 +1025,8 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     // INSERT sBase - 3, TEST sBase - 1; 2 first window: INSERT 0)
     uint32_t sBase = o0 + 1, k0 = 0, s0 = 1, j1 = 65, mode = 2;
     uint32_t spanHi = 61;   // (TIDY) 61 * s0 + max(0, 61 - j1): the last SEARCH probe's offset from sBase
+    uint64_t v8pf = 0;      // (PFR) the next window's hash inputs, read ahead
+    bool pfOk = false;
     uint32_t nextSweep = 32768;   // P17
     // ONE exit and no continue: the structurizer then needs no flow
     // variables and the loop-carried state stays in place across windows
@@ -1061,7 +1069,10 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         const uint32_t lo = insOn ? insPos : sBase;
         const uint32_t hi = (sHi < mflimitP1 ? sHi : mflimitP1) + 8;
         uint64_t v8;
-        if (hi - lo <= 1024) {
+        if (LZ4MT_ENC_PFR && pfOk) {   // read at the end of the previous sequence, the ring unchanged since
+            v8 = v8pf;
+            pfOk = false;
+        } else if (hi - lo <= 1024) {
             V.cover(hi);
             v8 = V.rd8(p);
         } else {   // wide window (long searches): hash inputs straight from global
@@ -1323,6 +1334,13 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             s0 = 1;
             j1 = 65;
             spanHi = 61;
+            if (LZ4MT_ENC_PFR && !done) {   // the next window (mode 1): INSERT, TEST, then sBase + j
+                const uint32_t hiN = (sBase + 61 < mflimitP1 ? sBase + 61 : mflimitP1) + 8;
+                if (hiN <= V.B + kSR) {
+                    v8pf = V.rd8(L == 0 ? sBase - 3 : (L == 1 ? sBase - 1 : sBase + (L - 2)));
+                    pfOk = true;
+                }
+            }
             STAMP_ADD(4, ts);
         }
     }
