@@ -689,6 +689,14 @@ constexpr bool kRingRT = LZ4MT_RING_RT != 0;
 #ifndef LZ4MT_ENC_PFR
 #define LZ4MT_ENC_PFR 0
 #endif
+// LZ4MT_ENC_HTAG (A/B): the u32 table's tag taken from the hash product's
+// bits 42..51 (bits 52..63 are the hash) instead of a second multiply.  Those
+// bits depend on the first 28 bits of the 4 bytes only, so equal words still
+// have equal tags; and within one bucket, equal low 28 bits force equal
+// words (the remaining bits would move the hash), so the filter is as sharp
+#ifndef LZ4MT_ENC_HTAG
+#define LZ4MT_ENC_HTAG 1
+#endif
 
 // ds_mskor_rtn_b32 on two LDS dwords (one position half, one tag byte): each
 // word becomes (word & ~mask) | data; returns the old words
@@ -794,7 +802,11 @@ template <bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false> str
     static constexpr uint32_t PM = (1u << PB) - 1u;
     static constexpr bool SP = SPLIT || P17;                  // u16 + u8 storage
     static constexpr uint32_t TB = P17 ? 7u : SPLIT ? 8u : 32u - PB;   // tag bits
-    static __device__ __forceinline__ uint32_t tag(uint32_t w0) { return (w0 * 0x85EBCA77u) >> (32 - TB); }
+    static constexpr bool HT = LZ4MT_ENC_HTAG != 0 && !U16 && !SP;   // tag from the hash5 product
+    static __device__ __forceinline__ uint32_t tag(uint32_t w0) {
+        if constexpr (HT) return (uint32_t)(((uint64_t)w0 << 24) * 889523592379ull >> (52 - TB)) & ((1u << TB) - 1u);
+        else return (w0 * 0x85EBCA77u) >> (32 - TB);
+    }
     l_u32* T;
     __device__ __forceinline__ l_u16* T16() const { return (l_u16*)T; }
     __device__ __forceinline__ l_u8* TG() const { return (l_u8*)T + 2 * (kTE + 64); }
@@ -1083,8 +1095,16 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             v8 = ((uint64_t)b << 32) | a;
         }
         const uint32_t w0 = (uint32_t)v8;
-        const uint32_t h = lz4_hash<U16>(w0, (uint32_t)(v8 >> 32));
-        const uint32_t mark = (P17 ? p & G::PM : p) | (G::tag(w0) << G::PB);   // the lane's final table entry
+        uint32_t h, tg;
+        if constexpr (G::HT) {   // one product: hash = bits 52..63, tag = the TB bits below
+            const uint64_t P = (v8 << 24) * 889523592379ull;
+            h = (uint32_t)(P >> 52);
+            tg = (uint32_t)(P >> (52 - G::TB)) & ((1u << G::TB) - 1u);
+        } else {
+            h = lz4_hash<U16>(w0, (uint32_t)(v8 >> 32));
+            tg = G::tag(w0);
+        }
+        const uint32_t mark = (P17 ? p & G::PM : p) | (tg << G::PB);   // the lane's final table entry
         // ---- table probe: read, write the marker, read back (LDS ops of a wave run in order)
         const uint32_t ti = live ? h : dumIdx;
         uint32_t told;
