@@ -697,6 +697,9 @@ constexpr bool kRingRT = LZ4MT_RING_RT != 0;
 #ifndef LZ4MT_ENC_HTAG
 #define LZ4MT_ENC_HTAG 1
 #endif
+#ifndef LZ4MT_ENC_HTAG_SP
+#define LZ4MT_ENC_HTAG_SP 1
+#endif
 
 // ds_mskor_rtn_b32 on two LDS dwords (one position half, one tag byte): each
 // word becomes (word & ~mask) | data; returns the old words
@@ -802,9 +805,14 @@ template <bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false> str
     static constexpr uint32_t PM = (1u << PB) - 1u;
     static constexpr bool SP = SPLIT || P17;                  // u16 + u8 storage
     static constexpr uint32_t TB = P17 ? 7u : SPLIT ? 8u : 32u - PB;   // tag bits
-    static constexpr bool HT = LZ4MT_ENC_HTAG != 0 && !U16 && !SP;   // tag from the hash5 product
+    // tag from the hash product: u32 tables, and with LZ4MT_ENC_HTAG_SP the
+    // byU16 split table (its hash4 product's bits 19 - TB .. 18; B4 218.0 ->
+    // 216.3 ms) -- not P17, whose 7 bits from the hash5 product filter a
+    // little worse (132.0 -> 132.3 ms at B5; profiles/r04htsp_encoder_ab.txt)
+    static constexpr bool HT = LZ4MT_ENC_HTAG != 0 && (!SP || (U16 && LZ4MT_ENC_HTAG_SP != 0));
     static __device__ __forceinline__ uint32_t tag(uint32_t w0) {
-        if constexpr (HT) return (uint32_t)(((uint64_t)w0 << 24) * 889523592379ull >> (52 - TB)) & ((1u << TB) - 1u);
+        if constexpr (HT && U16) return ((w0 * 2654435761u) >> (19 - TB)) & ((1u << TB) - 1u);
+        else if constexpr (HT) return (uint32_t)(((uint64_t)w0 << 24) * 889523592379ull >> (52 - TB)) & ((1u << TB) - 1u);
         else return (w0 * 0x85EBCA77u) >> (32 - TB);
     }
     l_u32* T;
@@ -1096,7 +1104,11 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         }
         const uint32_t w0 = (uint32_t)v8;
         uint32_t h, tg;
-        if constexpr (G::HT) {   // one product: hash = bits 52..63, tag = the TB bits below
+        if constexpr (G::HT && U16) {   // one product: hash4 = bits 19..31, tag = the TB bits below
+            const uint32_t P = w0 * 2654435761u;
+            h = P >> 19;
+            tg = (P >> (19 - G::TB)) & ((1u << G::TB) - 1u);
+        } else if constexpr (G::HT) {   // one product: hash5 = bits 52..63, tag = the TB bits below
             const uint64_t P = (v8 << 24) * 889523592379ull;
             h = (uint32_t)(P >> 52);
             tg = (uint32_t)(P >> (52 - G::TB)) & ((1u << G::TB) - 1u);
