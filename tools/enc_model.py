@@ -42,7 +42,14 @@ def ext_len(v):
     return (v - 15) // 255 + 1 if v >= 15 else 0
 
 
-def encode(s, cap, last_lane_wins=True):
+def encode(s, cap, last_lane_wins=True, xchg=False):
+    """xchg=True: the exchange probe of encode_block_v5 (LZ4MT_ENC_XCHG):
+    lanes exchange their entries in ascending lane order, so each gets its
+    in-window predecessor's entry or the table's; no read-back, no
+    predecessor resolution; lanes past the stop undo their inserts (the
+    first of each bucket puts back what it displaced)."""
+    if xchg:
+        return encode_xchg(s, cap)
     n = len(s)
     assert 65547 <= n <= 1 << 22
     bound = n + n // 255 + 16
@@ -173,6 +180,119 @@ def encode(s, cap, last_lane_wins=True):
     return bytes(out)
 
 
+def tag_ht(w0):
+    """the hash-product tag (LZ4MT_ENC_HTAG): bits 42..51 of hash5's product"""
+    return ((((w0 << 24) * 889523592379) & 0xFFFFFFFFFFFFFFFF) >> (52 - (32 - POSB))) & ((1 << (32 - POSB)) - 1)
+
+
+def encode_xchg(s, cap):
+    n = len(s)
+    assert 65547 <= n <= 1 << 22
+    bound = n + n // 255 + 16
+    limited = cap < bound
+    T = [(tag_ht(rd32(s, 0)) << POSB)] * 4096 + [0] * 64
+    mfl = n - 12 + 1
+    matchlimit = n - 5
+    anchor = op = 0
+    out = bytearray()
+    mode = 2            # 2: INSERT 0 only; 1: INSERT + TEST after a match; 0: continuation
+    sPos, k0 = 1, 0
+    while True:
+        p, step = [0] * 64, [1] * 64
+        for L in range(2, 64):
+            k = k0 + L - 2
+            p[L] = sPos + poff(k)
+            step[L] = 1 if k == 0 else (63 + k) >> 6
+        p[0] = 0 if mode == 2 else sPos - 3
+        p[1] = sPos - 1
+        live = [p[L] <= mfl if L >= 2 else (mode != 0 if L == 0 else mode == 1) for L in range(64)]
+        term = [L >= 2 and live[L] and p[L] + step[L] > mfl for L in range(64)]
+        w0 = [rd32(s, min(p[L], n - 8)) for L in range(64)]
+        h = [h5(rd64(s, min(p[L], n - 8))) for L in range(64)]
+        mark = [(p[L] | (tag_ht(w0[L]) << POSB)) & 0xFFFFFFFF for L in range(64)]
+        told = [0] * 64
+        for L in range(64):   # the exchanges, in ascending lane order
+            i = h[L] if live[L] else 4096 + L
+            told[L] = T[i]
+            T[i] = mark[L]
+        cand = [told[L] & MASK for L in range(64)]
+        maybe = [live[L] and L != 0 and not term[L] and cand[L] + 65535 >= p[L] and
+                 (told[L] >> POSB) == (mark[L] >> POSB) for L in range(64)]
+        aliased = set()
+        redo = False
+
+        def table_writes(wlim):
+            if redo:   # re-insert the lanes up to the stop, in lane order
+                for L in range(64):
+                    if live[L] and L <= wlim:
+                        T[h[L]] = mark[L]
+            past = [L for L in range(64) if live[L] and L > wlim]
+            pfl = p[past[0]] if past else p[63]
+            for L in past:   # the first lane of each bucket past the stop restores
+                if (told[L] & MASK) < pfl:
+                    T[h[L]] = told[L]
+
+        while True:
+            w = next((L for L in range(64) if (maybe[L] or term[L]) and L not in aliased), 64)
+            wTerm = w < 64 and term[w]
+            if w < 64 and not wTerm and rd32(s, cand[w]) != w0[w]:
+                aliased.add(w)     # tag alias: the stop moves on
+                table_writes(w)    # (the kernel writes in the round trip's shadow, then redoes)
+                redo = True
+                continue
+            break
+        wlim = 63 if w == 64 else (w - 1 if wTerm else w)
+        table_writes(wlim)
+        if w == 64:   # (probe offsets poff(k) count from the sequence's first search position)
+            k0 += 62
+            mode = 0
+            continue
+        if wTerm:
+            break
+        ip, cd = p[w], cand[w]
+        maxb = 0 if w == 1 else min(ip - anchor, cd)
+        back = 0
+        while back < maxb and s[ip - back - 1] == s[cd - back - 1]:
+            back += 1
+        lim = matchlimit - (ip + 4)
+        mc = 0
+        while mc < lim and s[ip + 4 + mc] == s[cd + 4 + mc]:
+            mc += 1
+        lit = ip - anchor - back
+        mcf = mc + back
+        litExt, mlExt = ext_len(lit), ext_len(mcf)
+        if limited:
+            if w != 1 and op + 1 + lit + 8 + lit // 255 > cap:
+                return b""
+            if op + 1 + litExt + lit + 2 + 6 + (mcf + 240) // 255 > cap:
+                return b""
+        tok = (min(lit, 15) << 4) | min(mcf, 15)
+        seq = bytearray([tok])
+        if lit >= 15:
+            seq += b"\xff" * (litExt - 1) + bytes([(lit - 15) % 255])
+        seq += s[anchor:anchor + lit]
+        off = ip - cd
+        seq += bytes([off & 255, off >> 8])
+        if mcf >= 15:
+            seq += b"\xff" * (mlExt - 1) + bytes([(mcf - 15) % 255])
+        out += seq
+        op += len(seq)
+        ipe = ip + 4 + mc
+        anchor = ipe
+        if ipe >= mfl:
+            break
+        mode = 1
+        sPos, k0 = ipe + 1, 0
+    run = n - anchor
+    if limited and op + run + 1 + (run + 240) // 255 > cap:
+        return b""
+    out.append(min(run, 15) << 4)
+    if run >= 15:
+        out += b"\xff" * (ext_len(run) - 1) + bytes([(run - 15) % 255])
+    out += s[anchor:]
+    return bytes(out)
+
+
 def fuzz_cases():
     rnd = random.Random(3)
     syn = oracle.gen_synthetic(1 << 20)
@@ -197,8 +317,9 @@ if __name__ == "__main__":
         if len(d) < 65547:
             continue
         for cap in (len(d), len(d) + len(d) // 255 + 16):
-            for llw in (True, False):
-                got, want = encode(d, cap, llw), oracle.compress_block(d, cap)
+            for llw in (True, False, "xchg"):
+                got = encode(d, cap, xchg=True) if llw == "xchg" else encode(d, cap, llw)
+                want = oracle.compress_block(d, cap)
                 if got != want:
                     i = next((i for i in range(min(len(got), len(want))) if got[i] != want[i]), None)
                     print(f"MISMATCH t={t} n={len(d)} cap={cap} lastLaneWins={llw} first diff at {i}")
