@@ -31,6 +31,7 @@ committed PMC profile of this same configuration, calibrated) and the CPU
 baseline (lz4mt-shaped pipeline on the host cores over liblz4 when present).
 """
 import argparse
+import contextlib
 import ctypes
 import json
 import os
@@ -232,6 +233,23 @@ def pmc_traffic(kernel, n, bm, flg):
             "source": "profiles/pmc_current.json (" + prof.get("tag", "?") + ")"}, None
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """gloo prints '[Gloo] Rank r is connected to k peer ranks' on file
+    descriptor 1 when a group connects (the gloo control group of every N > 1
+    run too); the driver reads stdout for rank 0's one JSON line, so group
+    set-up writes to stderr instead."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def frame_encoder(bm):
     """The kernel lz4mtHipCompressFrameAsyncEx runs for bm-byte blocks
     (launch_encode, lz4mt_kernels.hip): the byU16 table below 65 547 B, the
@@ -294,10 +312,12 @@ def main():
     local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
     torch.cuda.set_device(local)
     if distributed:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        with stdout_to_stderr():
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group(backend)
+                dist.barrier()   # (gloo connects its mesh here at the latest)
     dev = torch.device("cuda", local)
     stream = torch.cuda.current_stream()
 
@@ -364,7 +384,9 @@ def main():
     if streamed:   # the shard engine's streams and workspace, the control group and transport, made once
         eng = D.HipShardEngine(dev)
         shard_ws = L.shard_workspace(n, sd, device=dev)
-        ctrl = D.control_group()
+        with stdout_to_stderr():
+            ctrl = D.control_group()
+            dist.barrier(group=ctrl)   # (connected inside the redirect)
         transport = D.IpcPushTransport(dev) if a.transport == "ipc" else D.RcclTransport()
         transport_name = a.transport
         peers = D.peer_access_matrix() if rank == 0 else None
