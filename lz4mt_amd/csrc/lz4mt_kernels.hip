@@ -2045,7 +2045,7 @@ hipError_t launch_encode_overlap(const uint8_t* src, uint64_t srcSize, uint32_t 
 
 // LZ4MT_AMD_ENC_LDS_PAD=<bytes>: dynamic LDS added to the frame encoder's
 // launch, i.e. fewer resident waves per CU (occupancy sweeps, timing only;
-// profiles/r04_occupancy_sweep.txt)
+// profiles/r04a_occupancy_sweep.txt)
 static uint32_t enc_lds_pad() {
     const char* e = getenv("LZ4MT_AMD_ENC_LDS_PAD");
     return e ? (uint32_t)atoi(e) : 0u;
