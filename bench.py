@@ -204,8 +204,9 @@ def pmc_traffic(kernel, n, bm, flg):
     byte count (MI355X_MICROARCH.md: gfx950 FETCH_SIZE is ~1/2 of wide
     streaming reads; other widths need their own calibration)."""
     import glob
-    prof, seen = None, []
-    for path in [PMC_PROFILE] + sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_b*.json"))):
+    prof, seen, used = None, [], None
+    for path in [PMC_PROFILE] + sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_b*.json"))
+                                       + glob.glob(os.path.join(ROOT, "profiles", "pmc_dec*.json"))):
         try:
             p = json.load(open(path))
         except (OSError, ValueError):
@@ -213,7 +214,7 @@ def pmc_traffic(kernel, n, bm, flg):
         cfg = p.get("config", {})
         seen.append(cfg.get("workload", os.path.basename(path)))
         if (cfg.get("bytes"), cfg.get("block_bytes"), cfg.get("flg")) == (n, bm, flg):
-            prof = p
+            prof, used = p, os.path.relpath(path, ROOT)
             break
     if prof is None:
         return None, f"no PMC profile of this configuration (have: {seen})"
@@ -230,7 +231,7 @@ def pmc_traffic(kernel, n, bm, flg):
     return {"bytes": fetch + k["write_bytes"], "raw_bytes": fr + k["write_bytes"], "fetch_raw": fr,
             "fetch_calibrated": round(fetch),
             "write": k["write_bytes"], "calibration": cal.get("how", "guide x2 (uncalibrated)"),
-            "source": "profiles/pmc_current.json (" + prof.get("tag", "?") + ")"}, None
+            "source": f"{used} ({prof.get('tag', '?')})"}, None
 
 
 @contextlib.contextmanager
@@ -262,9 +263,15 @@ def frame_encoder(bm):
     return "k_encode"
 
 
-def workload_id(world, block_id):
-    """configs[1] is the 4 MiB headline; other block sizes are the configs[4]
-    sweep; N > 1 is configs[3]."""
+def workload_id(world, block_id, sck=False, level=0, bd=False):
+    """configs[1] is the 4 MiB -Sx -BX headline; other block sizes are the
+    configs[4] sweep; N > 1 is configs[3].  The content checksum (default
+    flags), LZ4-HC levels and -BD are modes BASELINE.json names no config
+    for: labelled as such, never as configs[1]."""
+    if sck or level >= 3 or bd:
+        mode = ", ".join(m for m, on in (("default flags (FLG.2 content checksum)", sck),
+                                         (f"LZ4-HC level {level}", level >= 3), ("-BD", bd)) if on)
+        return f"off-baseline mode ({mode}; not a BASELINE.json config)"
     if world > 1:
         return "configs[3]"
     return "configs[1]" if block_id == 7 else "configs[4] (block-size sweep)"
@@ -313,10 +320,12 @@ def main():
     torch.cuda.set_device(local)
     if distributed:
         with stdout_to_stderr():
+            # an explicit timeout: a rank that stops answering ends the run
+            # non-zero instead of stalling it for torch's 30 min default
             if backend == "nccl":
-                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=D.dist_timeout())
             else:
-                dist.init_process_group(backend)
+                dist.init_process_group(backend, timeout=D.dist_timeout())
                 dist.barrier()   # (gloo connects its mesh here at the latest)
     dev = torch.device("cuda", local)
     stream = torch.cuda.current_stream()
@@ -381,6 +390,7 @@ def main():
         compress()
         torch.cuda.synchronize()
     own_body = 0
+    transport = transport_name = None
     if streamed:   # the shard engine's streams and workspace, the control group and transport, made once
         eng = D.HipShardEngine(dev)
         shard_ws = L.shard_workspace(n, sd, device=dev)
@@ -390,77 +400,97 @@ def main():
         transport = D.IpcPushTransport(dev) if a.transport == "ipc" else D.RcclTransport()
         transport_name = a.transport
         peers = D.peer_access_matrix() if rank == 0 else None
-    L.lib.lz4mtHipSetTiming(1)
-    tc = td = ts = tg = 0.0
-    enc_ms, dec_ms, frame_len, exposed_ms, rounds, tails, scat = [], [], 0, [], [], [], []
-    full = piece = None
-    for it in range(a.warmup + a.steps):
-        timed = it >= a.warmup
-        t0 = sync_all()
-        tm = None
-        tgr = 0.0
-        if streamed:   # encode + streamed gather: ONE frame on rank 0
-            st_ = {}
-            try:
-                full = D.compress_gather_streamed(src, sd, dst=0, engine=eng, ws=shard_ws, stats=st_,
-                                                  transport=transport, ctrl=ctrl)
-            except D.IpcSetupError as e:   # raised on every rank together: all switch to RCCL
-                print(f"bench.py: IPC PUSH UNAVAILABLE ({e}); streamed gather falls back to RCCL point-to-point",
-                      file=sys.stderr, flush=True)
-                transport, transport_name = D.RcclTransport(), f"rccl (IPC setup failed: {e})"
-                full = D.compress_gather_streamed(src, sd, dst=0, engine=eng, ws=shard_ws, stats=st_,
-                                                  transport=transport, ctrl=ctrl)
-            end_ev = torch.cuda.Event(enable_timing=True)
-            end_ev.record()
-            torch.cuda.synchronize()
-            t1 = sync_all()
-            tm = [eng.enc_start.elapsed_time(eng.enc_done)]
-            exposed_ms.append(eng.enc_done.elapsed_time(end_ev) if rank == 0 else 0.0)
-            tgr = exposed_ms[-1] * 1e-3
-            rounds.append(st_.get("rounds", 0))
-            tails.append((st_.get("tail_rounds_s") or 0.0, st_.get("rounds_after_encode", 0)))
-            frame_len = full.numel() if rank == 0 else 0
-            own_body = st_.get("own_body_bytes", 0)
-        else:
-            if not a.decompress_only:
-                compress()
-            frame_len = int(fsz[0].item())          # synchronises the stream
-            if not a.decompress_only:
-                tm = timings()
-            tl = time.perf_counter()
-            if distributed:   # the gather belongs to compress
-                full = D.gather_frame(frame_buf, frame_len, dst=0)
-                torch.cuda.synchronize()
-            t1 = sync_all()
-            tgr = time.perf_counter() - tl if distributed else 0.0
-        if distributed:
-            sst = {}
-            piece = D.scatter_frame(full if rank == 0 else None, full.numel() if rank == 0 else 0, src=0,
-                                    device=dev, stats=sst)
-            if timed:
-                scat.append(sst)
-            torch.cuda.synchronize()
-            t2 = sync_all()
-        else:
-            piece, t2 = frame_buf, t1
-        decompress(piece, piece.numel() if distributed else frame_len)
-        tmd = timings()
-        t3 = sync_all()
-        if timed:
-            tc += t1 - t0
-            ts += t2 - t1
-            td += t3 - t2
-            tg += tgr
-            if tm:
-                enc_ms.append(tm[0])
-            if tmd:
-                dec_ms.append(tmd[1])
-    L.lib.lz4mtHipSetTiming(0)
+        # the transport's set-up (IPC buffers, maps, the pattern check) before
+        # any step: collective, and on failure every rank falls back together
+        try:
+            D.prepare_transport(transport, eng, n, sd, ctrl=ctrl)
+        except D.IpcSetupError as e:
+            print(f"bench.py: IPC PUSH UNAVAILABLE ({e}); streamed gather falls back to RCCL point-to-point",
+                  file=sys.stderr, flush=True)
+            transport, transport_name = D.RcclTransport(), f"rccl (IPC setup failed: {e})"
+            D.prepare_transport(transport, eng, n, sd, ctrl=ctrl)
 
-    # correctness (not timed): this rank's decoded piece == its source; at
-    # N > 1 the root decodes the stitched frame and checks every shard
-    ok = bool(torch.equal(out[:n], src))
-    stitched_ok = None
+    def run_steps(transport):
+        """W untimed + K timed steps; returns the accumulated timings and the last step's frames."""
+        R = dict(tc=0.0, td=0.0, ts=0.0, tg=0.0, enc_ms=[], dec_ms=[], frame_len=0, exposed_ms=[], rounds=[],
+                 tails=[], scat=[], full=None, piece=None, own_body=0)
+        L.lib.lz4mtHipSetTiming(1)
+        for it in range(a.warmup + a.steps):
+            timed = it >= a.warmup
+            t0 = sync_all()
+            tm = None
+            tgr = 0.0
+            if streamed:   # encode + streamed gather: ONE frame on rank 0 (SURVEY.md §8(d)/(e))
+                st_ = {}
+                R["full"] = D.compress_gather_streamed(src, sd, dst=0, engine=eng, ws=shard_ws, stats=st_,
+                                                       transport=transport, ctrl=ctrl)
+                end_ev = torch.cuda.Event(enable_timing=True)
+                end_ev.record()
+                torch.cuda.synchronize()
+                t1 = sync_all()
+                tm = [eng.enc_start.elapsed_time(eng.enc_done)]
+                R["exposed_ms"].append(eng.enc_done.elapsed_time(end_ev) if rank == 0 else 0.0)
+                tgr = R["exposed_ms"][-1] * 1e-3
+                R["rounds"].append(st_.get("rounds", 0))
+                R["tails"].append((st_.get("tail_rounds_s") or 0.0, st_.get("rounds_after_encode", 0)))
+                R["frame_len"] = R["full"].numel() if rank == 0 else 0
+                R["own_body"] = st_.get("own_body_bytes", 0)
+            else:
+                if not a.decompress_only:
+                    compress()
+                R["frame_len"] = int(fsz[0].item())          # synchronises the stream
+                if not a.decompress_only:
+                    tm = timings()
+                tl = time.perf_counter()
+                if distributed:   # the gather belongs to compress (SURVEY.md §8(d))
+                    R["full"] = D.gather_frame(frame_buf, R["frame_len"], dst=0)
+                    torch.cuda.synchronize()
+                t1 = sync_all()
+                tgr = time.perf_counter() - tl if distributed else 0.0
+            full = R["full"]
+            if distributed:
+                sst = {}
+                R["piece"] = D.scatter_frame(full if rank == 0 else None, full.numel() if rank == 0 else 0, src=0,
+                                             device=dev, stats=sst)
+                if timed:
+                    R["scat"].append(sst)
+                torch.cuda.synchronize()
+                t2 = sync_all()
+            else:
+                R["piece"], t2 = frame_buf, t1
+            piece = R["piece"]
+            decompress(piece, piece.numel() if distributed else R["frame_len"])
+            tmd = timings()
+            t3 = sync_all()
+            if timed:
+                R["tc"] += t1 - t0
+                R["ts"] += t2 - t1
+                R["td"] += t3 - t2
+                R["tg"] += tgr
+                if tm:
+                    R["enc_ms"].append(tm[0])
+                if tmd:
+                    R["dec_ms"].append(tmd[1])
+        L.lib.lz4mtHipSetTiming(0)
+        return R
+
+    def check(R):
+        """Correctness (not timed): this rank's decoded piece == its source; at
+        N > 1 the root decodes the stitched frame and checks every shard.
+        Returns (this rank's ok, stitched ok (same on every rank) or None)."""
+        ok = bool(torch.equal(out[:n], src))
+        if not distributed:
+            return ok, None
+
+        def digests(t):
+            return L.xxh32_chunks(t, 16 << 20).to(torch.int64)
+
+        def decode_full(f):
+            o, r = L.decompress_frame(f)
+            return o if r == 0 else o[:0]
+        return ok, D.verify_stitched(R["full"] if rank == 0 else None, src, decode_full, digests)
+
+    R = run_steps(transport)
     mem = None
     if distributed:
         # the root's device memory at its peak: torch's allocator (sources,
@@ -469,14 +499,22 @@ def main():
         free_b, total_b = torch.cuda.mem_get_info(dev)
         mem = {"max_allocated_GiB": round(torch.cuda.max_memory_allocated(dev) / GiB, 2),
                "device_used_GiB": round((total_b - free_b) / GiB, 2), "device_total_GiB": round(total_b / GiB, 2)}
-
-        def digests(t):
-            return L.xxh32_chunks(t, 16 << 20).to(torch.int64)
-
-        def decode_full(f):
-            o, r = L.decompress_frame(f)
-            return o if r == 0 else o[:0]
-        stitched_ok = D.verify_stitched(full if rank == 0 else None, src, decode_full, digests)
+    ok, stitched_ok = check(R)
+    if streamed and stitched_ok is False and isinstance(transport, D.IpcPushTransport):
+        # the IPC push delivered a wrong frame although its set-up check
+        # passed: measure again over RCCL (every rank sees the same verdict)
+        # and say so in the line -- the first measurement is discarded
+        print("bench.py: THE STITCHED FRAME OVER THE IPC PUSH FAILED ITS CHECK; steps re-run over RCCL point-to-point",
+              file=sys.stderr, flush=True)
+        transport.close()
+        transport, transport_name = D.RcclTransport(), "rccl (IPC push gave a wrong stitched frame; re-run)"
+        D.prepare_transport(transport, eng, n, sd, ctrl=ctrl)
+        R = run_steps(transport)
+        ok, stitched_ok = check(R)
+    tc, td, ts, tg = R["tc"], R["td"], R["ts"], R["tg"]
+    enc_ms, dec_ms, frame_len, exposed_ms = R["enc_ms"], R["dec_ms"], R["frame_len"], R["exposed_ms"]
+    rounds, tails, scat, full, own_body = R["rounds"], R["tails"], R["scat"], R["full"], R["own_body"]
+    if distributed:
         mem["after_verify_max_allocated_GiB"] = round(torch.cuda.max_memory_allocated(dev) / GiB, 2)
         t = torch.tensor([tc, td, ts, tg, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -537,7 +575,7 @@ def main():
                                     f"{world} GPU(s), {bm >> 10} KiB independent blocks, {flags} frame, "
                                     f"compress+decompress+XXH32, device-resident")
                                    if a.total_gib is not None else
-                                   (f"{workload_id(world, a.block_id)}: {a.gib:g} GiB/GPU synthetic, {bm >> 10} KiB "
+                                   (f"{workload_id(world, a.block_id, sck, a.level, a.block_dependent)}: {a.gib:g} GiB/GPU synthetic, {bm >> 10} KiB "
                                     f"independent blocks, {flags} frame, compress+decompress+XXH32, device-resident"),
                        "bytes_per_gpu": n, "bytes_total": n_total, "block_bytes": bm,
                        "parallelism": f"block-sharded x{world}" + (", RCCL gather to one frame on rank 0 (in compress)"
@@ -549,6 +587,7 @@ def main():
         }
         if streamed:   # root's GPU time from its own encode's end to the assembled frame
             line.update({"gather": f"streamed beside the encode (dist.compress_gather_streamed, {transport_name})",
+                         "ipc_buffers": getattr(transport, "kind", None),
                          "gather_exposed_ms": round(sum(exposed_ms[a.warmup:]) / max(1, K), 3),
                          "gather_rounds": round(sum(rounds[a.warmup:]) / max(1, K), 1),
                          "gather_tail_rounds": round(sum(t[1] for t in tails[a.warmup:]) / max(1, K), 1),

@@ -189,6 +189,20 @@ Lz4MtResult lz4mtHipShardAssemble(const void* d_src, uint64_t n, const Lz4MtStre
  * asynchronous device-to-device copy (a mapped peer buffer included).
  * 0 on success, -1 otherwise. */
 int lz4mtHipIpcAlloc(uint64_t bytes, void** d_ptr, void* handle64);
+/* The same, choosing the memory kind (*kind receives it): 2 uncached device
+ * memory (hipDeviceMallocUncached: no L2 line of it is ever held, so a peer
+ * copy engine's writes are what every later read sees), 1 fine-grained,
+ * 0 plain hipMalloc -- the best kind <= want that allocates and exports an
+ * IPC handle.  lz4mtHipShardUnpack starts with a system-scope acquire in
+ * every case. */
+int lz4mtHipIpcAllocKind(uint64_t bytes, void** d_ptr, void* handle64, int want, int* kind);
+/* PCI bus id ("dddd:bb:dd.f", len >= 13) of device `dev`; the ordinal of the
+ * visible device with that bus id (-1: not visible); hipDeviceCanAccessPeer
+ * (1 yes, 0 no, -1 error).  The IPC setup identifies the root's GPU by bus id
+ * so that processes that number devices differently agree. */
+int lz4mtHipDevicePciBusId(int dev, char* buf, int len);
+int lz4mtHipDeviceByPciBusId(const char* busId);
+int lz4mtHipCanAccessPeer(int dev, int peer);
 int lz4mtHipIpcOpen(const void* handle64, void** d_ptr);
 int lz4mtHipIpcClose(void* d_ptr);
 int lz4mtHipFree(void* d_ptr);
@@ -213,10 +227,17 @@ int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, 
  * 64 bytes, d_csize: nb int32.  Asynchronous; 0, or -1 on bad arguments. */
 int lz4mtHipDebugEncode(const void* d_src, uint64_t n, uint32_t blockSize, void* d_slots, void* d_csize, void* stream);
 /* 1 when the current device applies one wave's same-address LDS exchanges
- * in ascending lane order (what the block encoder's table probe relies on;
- * checked once per device before the first encode, which fails with an
- * error when it does not hold), 0 when it does not, -1 without a device. */
+ * in ascending lane order (what the block encoders' exchange probe relies
+ * on; checked once per device before the first encode), 0 when it does not
+ * (the encoders then run their read-back probe: same bytes, no ordering
+ * assumed), -1 without a device or when the check could not run. */
 int lz4mtHipCheckEncoderOrder(void);
+/* The table probe the block encoders use on the current device: 1 the LDS
+ * exchange, 0 the read-back probe (the order check failed, or
+ * LZ4MT_AMD_ENC_PROBE=readback), -1 without a device / on a HIP error.  A
+ * call whose stream is being captured into a graph before this device was
+ * checked also takes the read-back probe (the check synchronises). */
+int lz4mtHipEncoderProbe(void);
 /* The parse work of a split parse: n bytes in streams of S bytes, stream b
  * parsed from ov bytes before its start (the overlap a join needs), S + ov
  * <= 4 MiB, into d_slots (nb x (S + ov) + 64 bytes), sizes into d_csize;

@@ -124,6 +124,10 @@ PROTOTYPES = {
     "lz4mtHipShardUnpack": (c_int, [c_void_p, c_uint64, SD_P, c_void_p, c_uint64, c_void_p]),
     "lz4mtHipShardAssemble": (c_int, [c_void_p, c_uint64, SD_P, c_void_p, c_uint64, c_void_p, c_uint64, c_void_p]),
     "lz4mtHipIpcAlloc": (c_int, [c_uint64, ctypes.POINTER(c_void_p), c_void_p]),
+    "lz4mtHipIpcAllocKind": (c_int, [c_uint64, ctypes.POINTER(c_void_p), c_void_p, c_int, ctypes.POINTER(c_int)]),
+    "lz4mtHipDevicePciBusId": (c_int, [c_int, c_char_p, c_int]),
+    "lz4mtHipDeviceByPciBusId": (c_int, [c_char_p]),
+    "lz4mtHipCanAccessPeer": (c_int, [c_int, c_int]),
     "lz4mtHipIpcOpen": (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
     "lz4mtHipIpcClose": (c_int, [c_void_p]),
     "lz4mtHipFree": (c_int, [c_void_p]),
@@ -132,6 +136,7 @@ PROTOTYPES = {
     "lz4mtHipDebugEncodeStats": (c_int, [c_void_p, c_uint64, c_uint32, ctypes.POINTER(c_uint64), c_void_p]),
     "lz4mtHipDebugEncode": (c_int, [c_void_p, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p]),
     "lz4mtHipCheckEncoderOrder": (c_int, []),
+    "lz4mtHipEncoderProbe": (c_int, []),
     "lz4mtHipDebugEncodeOverlap": (c_int, [c_void_p, c_uint64, c_uint32, c_uint32, c_int, c_void_p, c_void_p, c_void_p]),
     "lz4mtDebugBdPlan": (c_int, [c_int, c_int, c_void_p, c_uint64, c_void_p]),
     "lz4mtHipDebugFetchCal": (c_int, [c_void_p, c_uint64, c_int, c_void_p, c_void_p]),

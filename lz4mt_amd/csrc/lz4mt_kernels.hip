@@ -633,74 +633,6 @@ static_assert(kCatchLanes >= 1 && kCatchLanes <= 64, "catch-up lanes");
 constexpr uint64_t kCatchMask = kCatchLanes >= 64 ? ~0ull : (1ull << kCatchLanes) - 1ull;
 static_assert(kCountLanes >= 1 && kCountLanes <= 63, "count lanes");
 constexpr uint32_t kSRMirror = 64;    // ring[kSR .. kSR+64) mirrors ring[0 .. 64)
-// near candidates: when every byte of a stop's round trip (verify and count
-// words, catch-up bytes) lies in the source ring, read them from LDS
-#ifndef LZ4MT_RING_RT
-#define LZ4MT_RING_RT 0
-#endif
-constexpr bool kRingRT = LZ4MT_RING_RT != 0;
-// LZ4MT_CAND_PF (A/B): right after the table probe, every lane whose
-// candidate passed the tag test loads its candidate's word, so the stop's
-// round trip finds the candidate's line on chip (1: the candidate words; 2:
-// the other lanes also touch the first such candidate's line before it and
-// the line its forward count ends in)
-#ifndef LZ4MT_CAND_PF
-#define LZ4MT_CAND_PF 0
-#endif
-// LZ4MT_IP_RING (A/B): the round trip's ip-side words and catch-up bytes from
-// the LDS source ring whenever they lie in it (only the candidate side goes
-// to global memory)
-#ifndef LZ4MT_IP_RING
-#define LZ4MT_IP_RING 0
-#endif
-// LZ4MT_ENC_XCHG: the u32 table probe as ONE LDS exchange per lane
-// (ds_wrxchg_rtn_b32).  A wave's same-address exchanges take effect in
-// ascending lane order (tools/probe/lds_xchg_order.hip: 6.4 M lanes, every
-// one), lanes are in position order, so each lane gets exactly the entry
-// LZ4's sequential inserts leave for it -- its in-window predecessor's mark,
-// or the table's entry -- with no readback and no predecessor resolution.
-#ifndef LZ4MT_ENC_XCHG
-#define LZ4MT_ENC_XCHG 1
-#endif
-// LZ4MT_ENC_LATE (A/B): a sequence's layout (extension lengths, the output
-// offset, limitedOutput's margin checks) is worked out in the NEXT window's
-// round-trip shadow, just before its bytes are stored, instead of between
-// the forward count and the next window's probe
-#ifndef LZ4MT_ENC_LATE
-#define LZ4MT_ENC_LATE 0
-#endif
-// LZ4MT_ENC_XCHG_SP (A/B): the same exchange probe on the split u16 + u8
-// tables (k_encode16, k_encode_p17): a masked OR with return
-// (ds_mskor_rtn_b32) replaces just the lane's 16-bit position and its tag
-// byte, and is lane-ordered the same way (tools/probe/lds_mskor_order.hip)
-#ifndef LZ4MT_ENC_XCHG_SP
-#define LZ4MT_ENC_XCHG_SP 1
-#endif
-// LZ4MT_ENC_TIDY (A/B): the window's last-probe offset carried as loop state
-// (61 after every match) instead of recomputed with a saturating VALU
-// subtract + readfirstlane each window; catch-up byte indices materialised
-// as 32-bit offsets (SGPR-base loads, no 64-bit address adds)
-#ifndef LZ4MT_ENC_TIDY
-#define LZ4MT_ENC_TIDY 1
-#endif
-// LZ4MT_ENC_PFR (A/B): the first window after a match gets its hash inputs
-// from a ring read issued at the end of the previous sequence (its positions
-// are known once the match end is), so the LDS latency overlaps the layout
-#ifndef LZ4MT_ENC_PFR
-#define LZ4MT_ENC_PFR 0
-#endif
-// LZ4MT_ENC_HTAG (A/B): the u32 table's tag taken from the hash product's
-// bits 42..51 (bits 52..63 are the hash) instead of a second multiply.  Those
-// bits depend on the first 28 bits of the 4 bytes only, so equal words still
-// have equal tags; and within one bucket, equal low 28 bits force equal
-// words (the remaining bits would move the hash), so the filter is as sharp
-#ifndef LZ4MT_ENC_HTAG
-#define LZ4MT_ENC_HTAG 1
-#endif
-#ifndef LZ4MT_ENC_HTAG_SP
-#define LZ4MT_ENC_HTAG_SP 1
-#endif
-
 // ds_mskor_rtn_b32 on two LDS dwords (one position half, one tag byte): each
 // word becomes (word & ~mask) | data; returns the old words
 __device__ __forceinline__ void mskor2_rtn(l_u32* w16, uint32_t m16, uint32_t d16, l_u32* w8, uint32_t m8,
@@ -712,17 +644,6 @@ __device__ __forceinline__ void mskor2_rtn(l_u32* w16, uint32_t m16, uint32_t d1
                  : "v"((uint32_t)(uintptr_t)w16), "v"(m16), "v"(d16), "v"((uint32_t)(uintptr_t)w8), "v"(m8), "v"(d8)
                  : "memory");
 }
-#ifndef LZ4MT_NOSTORE_TEST
-#define LZ4MT_NOSTORE_TEST 0
-#endif
-// LZ4MT_ENC_NT: the encoder's byte stores non-temporal, so output lines do not
-// displace the source lines the round trips read back from L2.  Off: it
-// saves 0.3 % of k_encode but the byte stores then reach HBM uncombined --
-// WRITE_SIZE 24.2 GB per 8 GiB launch instead of 4.24 GB
-// (profiles/r03s_enc_nt_ab.txt, r03t_pmc.json)
-#ifndef LZ4MT_ENC_NT
-#define LZ4MT_ENC_NT 0
-#endif
 
 __device__ __forceinline__ uint32_t gld4u(g_cu8* p) { return *(g_cu32u*)p; }
 __device__ __forceinline__ uint64_t gld8u(g_cu8* p) { return *(g_cu64u*)p; }
@@ -805,11 +726,15 @@ template <bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false> str
     static constexpr uint32_t PM = (1u << PB) - 1u;
     static constexpr bool SP = SPLIT || P17;                  // u16 + u8 storage
     static constexpr uint32_t TB = P17 ? 7u : SPLIT ? 8u : 32u - PB;   // tag bits
-    // tag from the hash product: u32 tables, and with LZ4MT_ENC_HTAG_SP the
-    // byU16 split table (its hash4 product's bits 19 - TB .. 18; B4 218.0 ->
-    // 216.3 ms) -- not P17, whose 7 bits from the hash5 product filter a
-    // little worse (132.0 -> 132.3 ms at B5; profiles/r04htsp_encoder_ab.txt)
-    static constexpr bool HT = LZ4MT_ENC_HTAG != 0 && (!SP || (U16 && LZ4MT_ENC_HTAG_SP != 0));
+    // tag from the hash product (one multiply for hash and tag): the u32
+    // table takes bits 42..51 of the hash5 product (bits 52..63 are the
+    // hash); those bits depend on the word's first 28 bits only, so equal
+    // words keep equal tags, and within one bucket equal low 28 bits force
+    // equal words, so the filter is as sharp (profiles/r04htag_encoder_ab.txt).
+    // The byU16 split table takes its hash4 product's bits 19 - TB .. 18 (B4
+    // 218.0 -> 216.3 ms); not P17, whose 7 bits from the hash5 product filter
+    // a little worse (132.0 -> 132.3 ms at B5; profiles/r04htsp_encoder_ab.txt)
+    static constexpr bool HT = !SP || U16;
     static __device__ __forceinline__ uint32_t tag(uint32_t w0) {
         if constexpr (HT && U16) return ((w0 * 2654435761u) >> (19 - TB)) & ((1u << TB) - 1u);
         else if constexpr (HT) return (uint32_t)(((uint64_t)w0 << 24) * 889523592379ull >> (52 - TB)) & ((1u << TB) - 1u);
@@ -869,7 +794,6 @@ template <bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false> str
 // (few loop-carried fields; the layout is derived at store time)
 struct PendSeq {
     uint32_t op, lit, mcf, off, anchor;
-    bool test;   // (LZ4MT_ENC_LATE) the match was found by the TEST lane: no literal margin check
 };
 struct SeqLayout {
     uint32_t total, a1, a2, token, litRem, mlRem, off;
@@ -908,14 +832,10 @@ __device__ __forceinline__ void store_pend(const PendSeq& p, const SrcRing& V, g
             const uint32_t x = min(base + L, e.total - 1);   // lanes past the end repeat the last byte
             uint32_t lv = V.r[(p.anchor + x - e.a1) & (kSR - 1)];
             asm volatile("" : "+v"(lv));
-#if LZ4MT_NOSTORE_TEST   // timing experiment only: the bytes are computed, never stored
-            const uint32_t pb = pend_byte(e, x, lv);
-            asm volatile("" ::"v"(pb));
-#elif LZ4MT_ENC_NT
-            __builtin_nontemporal_store((uint8_t)pend_byte(e, x, lv), (g_u8*)&d[p.op + x]);
-#else
+            // (plain stores: non-temporal ones saved 0.3 % of k_encode but
+            // reach HBM uncombined, profiles/r03s_enc_nt_ab.txt; with no
+            // stores at all the encoder is only 1.4 % faster)
             d[p.op + x] = (uint8_t)pend_byte(e, x, lv);
-#endif
         }
     } else {   // literals no longer (or not yet) in the ring: global bytes
         for (uint32_t base = 0; base < e.total; base += 64) {
@@ -954,14 +874,25 @@ __device__ __forceinline__ void publish_progress(uint32_t* pub, uint32_t v) {
 // LZ4MT_AMD_BD_REFERENCE): every candidate-side load goes through xld4 /
 // xld1, and the carried entries' tags are recomputed from the bytes those
 // positions now hold (lz4 compares the memory as it is, not as it was).
+// XCHG (the product path): the table probe is ONE LDS exchange per lane
+// (ds_wrxchg_rtn_b32; on the split u16 + u8 tables a masked OR with return,
+// ds_mskor_rtn_b32, on the dword of the lane's position half and on the one of
+// its tag byte).  A wave's same-address exchanges take effect in ascending
+// lane order on gfx950 (tools/probe/lds_xchg_order.hip, lds_mskor_order.hip:
+// 6.4 M lanes, every one), lanes are in position order, so each lane gets
+// exactly the entry LZ4's sequential inserts leave for it -- its in-window
+// predecessor's mark, or the table's -- with no readback and no predecessor
+// resolution.  That order is not architected: encoder_path() checks it once
+// per device (k_xchg_order) and runs the !XCHG instantiation -- read, write
+// the marker, read back, resolve same-bucket predecessors exactly -- when the
+// check fails (or LZ4MT_AMD_ENC_PROBE=readback forces it).
 template <bool ST, bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false, bool PUB = false,
-          bool XH = false>
+          bool XH = false, bool XCHG = true>
 __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
                                    l_u32* __restrict__ T, l_u8* __restrict__ R, uint64_t* acc,
                                    LinkArgs lk = LinkArgs{0, 0, 0, true}, uint32_t* pub = nullptr) {
     using G = V5Geo<U16, SPLIT, LINK, P17>;
     const G tab{T};
-    constexpr bool XCHG = LZ4MT_ENC_XCHG != 0 && (!G::SP || LZ4MT_ENC_XCHG_SP != 0);
     const uint32_t L = laneid();
     uint64_t ts = STAMP_T();
     const uint32_t o0 = LINK ? kLinkO0 : 0u;   // position of the block's first byte
@@ -1017,25 +948,10 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     PendSeq pe{};
     bool havePe = false;
     bool done = false, fail = false;
-    // LZ4MT_ENC_LATE: the pending sequence's layout, right before its store;
-    // false when limitedOutput's margins fail (the block is then stored raw)
-    auto settle = [&]() -> bool {
-        const uint32_t litExt = ext_len(pe.lit), mlExt = ext_len(pe.mcf);
-        if (op + 2 * (pe.lit + pe.mcf) + 16 > capL) {
-            if ((!pe.test && op + 1 + pe.lit + 8 + pe.lit / 255 > cap) ||
-                (op + 1 + litExt + pe.lit + 2 + 6 + (pe.mcf + 240) / 255 > cap))
-                return false;
-        }
-        pe.op = op;
-        if constexpr (PUB) {   // every sequence before this one has been stored: [0, op) is final
-            if ((op ^ (op + 1 + litExt + pe.lit + 2 + mlExt)) >> kPubShift) publish_progress(pub, op);
-        }
-        op += 1 + litExt + pe.lit + 2 + mlExt;
-        return true;
-    };
+    // (the layout is settled right after the count: deferring it into the
+    // next round trip's shadow cost 3.2 ms, profiles/r04late_encoder_layout_ab.txt)
     auto store_pending = [&]() {
-        if (!LZ4MT_ENC_LATE || settle()) store_pend(pe, V, s, d);
-        else fail = true;
+        store_pend(pe, V, s, d);
         havePe = false;
     };
     // window: lane 0 INSERT insPos, lane 1 TEST testPos, lane L >= 2 SEARCH
@@ -1044,9 +960,9 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     // (0 continuation: search only; 1 after a match ending at sBase - 1:
     // INSERT sBase - 3, TEST sBase - 1; 2 first window: INSERT 0)
     uint32_t sBase = o0 + 1, k0 = 0, s0 = 1, j1 = 65, mode = 2;
-    uint32_t spanHi = 61;   // (TIDY) 61 * s0 + max(0, 61 - j1): the last SEARCH probe's offset from sBase
-    uint64_t v8pf = 0;      // (PFR) the next window's hash inputs, read ahead
-    bool pfOk = false;
+    // 61 * s0 + max(0, 61 - j1): the last SEARCH probe's offset from sBase,
+    // carried as loop state (61 after every match) rather than recomputed
+    uint32_t spanHi = 61;
     uint32_t nextSweep = 32768;   // P17
     // ONE exit and no continue: the structurizer then needs no flow
     // variables and the loop-carried state stays in place across windows
@@ -1072,16 +988,15 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         // and 1 wrap j, but take the INSERT / TEST position below)
         uint32_t p = sBase + __umul24(j, s0) + (uint32_t)max(jx, 0);
         const uint32_t step = s0 + (jx >= 0 ? 1u : 0u);
-        const uint32_t sHi = LZ4MT_ENC_TIDY ? sBase + spanHi : sBase + 61 * s0 + (61 > j1 ? 61 - j1 : 0u);
-        const bool insOn = mode != 0, testOn = mode == 1;
+        const uint32_t sHi = sBase + spanHi;
+        const bool insOn = mode != 0;
         const uint32_t insPos = mode == 2 ? o0 : sBase - 3, testPos = sBase - 1;
         p = L == 0 ? insPos : (L == 1 ? testPos : p);
         // lane predicates as wave masks (SALU), turned back into per-lane
         // conditions with inverse_ballot (the mask is the select's condition):
-        // no 0/1 materialisation chains
-        // (TIDY: lane 0 / 1's bits straight from the mode -- 2: INSERT only, 1: both)
-        const uint64_t roleM = LZ4MT_ENC_TIDY ? (uint64_t)((0x130u >> (4 * mode)) & 3u)
-                                              : (insOn ? 1ull : 0ull) | (testOn ? 2ull : 0ull);
+        // no 0/1 materialisation chains.  Lane 0 / 1's bits come straight
+        // from the mode (2: INSERT only, 1: both, 0: neither)
+        const uint64_t roleM = (uint64_t)((0x130u >> (4 * mode)) & 3u);
         const uint64_t liveM = (bal(p <= mflimitP1) & ~3ull) | roleM;
         const uint64_t tmk = bal(p + step > mflimitP1) & liveM & ~3ull;
         const bool live = __builtin_amdgcn_inverse_ballot_w64(liveM);
@@ -1089,10 +1004,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         const uint32_t lo = insOn ? insPos : sBase;
         const uint32_t hi = (sHi < mflimitP1 ? sHi : mflimitP1) + 8;
         uint64_t v8;
-        if (LZ4MT_ENC_PFR && pfOk) {   // read at the end of the previous sequence, the ring unchanged since
-            v8 = v8pf;
-            pfOk = false;
-        } else if (hi - lo <= 1024) {
+        if (hi - lo <= 1024) {
             V.cover(hi);
             v8 = V.rd8(p);
         } else {   // wide window (long searches): hash inputs straight from global
@@ -1137,16 +1049,6 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         uint64_t mm = cokM & bal((told >> G::PB) == (mark >> G::PB));
         bool maybe = __builtin_amdgcn_inverse_ballot_w64(mm);
         uint64_t sm = mm | tmk;
-#if LZ4MT_CAND_PF
-        uint32_t pfw = 0;
-        if (!LINK && mm) {
-            const uint32_t c0 = rdlane(cand, (int)sff1(mm));
-            uint32_t a = c0;
-            if (LZ4MT_CAND_PF >= 2) a = (L & 1) ? c0 + 4 * kCountLanes + 4 : (c0 > 64 ? c0 - 64 : 0u);
-            a = maybe ? cand : a;
-            pfw = gld4u(s + (a < last4 ? a : last4));
-        }
-#endif
         STAMP_ADD(0, ts);
         // ---- resolve the first stop.  Exact in-window predecessors are
         // resolved (once) whenever a collision reaches the current stop
@@ -1231,26 +1133,15 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                     const bool cOn = L <= kCountLanes;
                     const uint32_t ci = cOn ? cd + 4 * L : cd, ii = cOn ? ip + 4 * L : ip;
                     const bool bOn = L < maxb && L < kCatchLanes;
-                    if (kRingRT && cd >= V.B + kCatchLanes && ip + 4 * kCountLanes + 4 <= V.B + kSR) {
-                        // every byte the round trip would load lies in the source
-                        // ring (a near candidate): read them from LDS instead
-                        cw = *(const l_u32u*)(V.r + ((ci < last4 ? ci : last4) & (kSR - 1)));
-                        iw = *(const l_u32u*)(V.r + ((ii < last4 ? ii : last4) & (kSR - 1)));
-                        bi = V.r[(bOn ? ip - L - 1 : ip - 1) & (kSR - 1)];
-                        bc = V.r[(bOn ? cd - L - 1 : cd - 1) & (kSR - 1)];
-                    } else if (LZ4MT_IP_RING && ip >= V.B + kCatchLanes && ip + 4 * kCountLanes + 4 <= V.B + kSR) {
-                        cw = xld4(ci < last4 ? ci : last4);
-                        bc = xld1(bOn ? cd - L - 1 : o0);
-                        iw = *(const l_u32u*)(V.r + ((ii < last4 ? ii : last4) & (kSR - 1)));
-                        bi = V.r[(bOn ? ip - L - 1 : ip - 1) & (kSR - 1)];
-                    } else {
-                        cw = xld4(ci < last4 ? ci : last4);
-                        iw = gld4u(s + (ii < last4 ? ii : last4));
-                        uint32_t bix = bOn ? ip - L - 1 : o0, bcx = bOn ? cd - L - 1 : o0;   // (o0: a byte of the block itself)
-                        if (LZ4MT_ENC_TIDY) asm volatile("" : "+v"(bix), "+v"(bcx));
-                        bi = s[bix];
-                        bc = xld1(bcx);
-                    }
+                    // every side from global memory: reading the near side(s)
+                    // from the LDS ring when they lie in it was slower
+                    // (profiles/r03j_encoder_ring_rt_ab.txt, r04s_encoder_ip_ring_ab.txt)
+                    cw = xld4(ci < last4 ? ci : last4);
+                    iw = gld4u(s + (ii < last4 ? ii : last4));
+                    uint32_t bix = bOn ? ip - L - 1 : o0, bcx = bOn ? cd - L - 1 : o0;   // (o0: a byte of the block itself)
+                    asm volatile("" : "+v"(bix), "+v"(bcx));   // 32-bit offsets, SGPR-base loads
+                    bi = s[bix];
+                    bc = xld1(bcx);
                     if (havePe) store_pending();
                     table_writes(w, false);   // in the round trip's shadow; redone if w moves
                     twDone = true;
@@ -1270,9 +1161,6 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         }
         if (havePe) store_pending();
         if (!twDone) table_writes(w, wTerm);
-#if LZ4MT_CAND_PF
-        asm volatile("" ::"v"(pfw));   // (the early loads retire before the window ends)
-#endif
         STAMP_ADD(1, ts);
         STAMP_ADD(2, ts);
         if (w == 64) {   // no stop: the search goes on
@@ -1281,10 +1169,10 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             s0 = (63 + k0) >> 6;   // k0 >= 62: no max(1, .) needed
             j1 = (k0 < 65 ? 65u : ((k0 - 1) & ~63u) + 65) - k0;
             mode = 0;
-            if (LZ4MT_ENC_TIDY) spanHi = 61 * s0 + (61 > j1 ? 61 - j1 : 0u);
+            spanHi = 61 * s0 + (61 > j1 ? 61 - j1 : 0u);
         }
-      } while (w == 64 && !(LZ4MT_ENC_LATE && fail));
-        if (wTerm || (LZ4MT_ENC_LATE && fail)) {
+      } while (w == 64);
+        if (wTerm) {
             done = true;
         } else {
             // ---- catch-up (backwards) and LZ4_count (forwards from ip + 4).
@@ -1339,10 +1227,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             pe.mcf = mcf;
             pe.off = ip - cd;
             pe.anchor = anchor;
-            pe.test = w == 1;
-            if (LZ4MT_ENC_LATE) {
-                havePe = true;
-            } else {
+            {
                 const uint32_t litExt = ext_len(lit), mlExt = ext_len(mcf);
                 // 1.9.3's limitedOutput margins; both hold whenever
                 // op + 2 (lit + mcf) + 16 <= cap, so the exact test runs rarely
@@ -1366,21 +1251,11 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             s0 = 1;
             j1 = 65;
             spanHi = 61;
-            if (LZ4MT_ENC_PFR && !done) {   // the next window (mode 1): INSERT, TEST, then sBase + j
-                const uint32_t hiN = (sBase + 61 < mflimitP1 ? sBase + 61 : mflimitP1) + 8;
-                if (hiN <= V.B + kSR) {
-                    v8pf = V.rd8(L == 0 ? sBase - 3 : (L == 1 ? sBase - 1 : sBase + (L - 2)));
-                    pfOk = true;
-                }
-            }
             STAMP_ADD(4, ts);
         }
     }
     if (fail) return 0;
-    if (havePe) {
-        store_pending();
-        if (fail) return 0;
-    }
+    if (havePe) store_pending();
     // ---- last literals
     {
         const uint32_t run = n - anchor;
@@ -1410,6 +1285,9 @@ static_assert(kSR + kSRMirror <= 3072, "ring exceeds the shared scratch");
 static_assert(kDedup == 1024, "scratch layout");
 
 #if LZ4MT_PART != 2
+// XC: the exchange probe (true, the product) or the read-back probe (false,
+// the fallback when k_xchg_order fails); see encode_block_v5
+template <bool XC>
 __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, uint64_t srcSize, uint32_t blockSize,
                                                uint8_t* __restrict__ slots, uint64_t slotStride,
                                                uint32_t capOverride, int32_t* __restrict__ csize) {
@@ -1427,7 +1305,8 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
     if (n < (uint32_t)kLimit64K)
         r = encode_block<true, false, false>(s, n, d, cap, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
     else if (n <= (1u << kPosBits))
-        [[clang::always_inline]] r = encode_block_v5<false, false>(s, n, d, cap, Tl, Xl, nullptr);
+        [[clang::always_inline]] r =
+            encode_block_v5<false, false, false, false, false, false, false, XC>(s, n, d, cap, Tl, Xl, nullptr);
     else
         r = encode_block<false, false, false>(s, n, d, cap, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
     if (laneid() == 0) csize[b] = r;
@@ -1437,6 +1316,7 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
 // block-sharded streamed gather): the same parse and bytes; pub[b] = bytes
 // of slot b already final, while the block encodes (the v5 path, 65 547 B ..
 // 4 MiB blocks, every 64 KiB of output), then kPubDone | size (or kPubRaw).
+template <bool XC>
 __global__ void __launch_bounds__(64) k_encode_pub(const uint8_t* __restrict__ src, uint64_t srcSize,
                                                    uint32_t blockSize, uint8_t* __restrict__ slots,
                                                    uint64_t slotStride, int32_t* __restrict__ csize,
@@ -1454,8 +1334,8 @@ __global__ void __launch_bounds__(64) k_encode_pub(const uint8_t* __restrict__ s
     if (n < (uint32_t)kLimit64K)
         r = encode_block<true, false, false>(s, n, d, n, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
     else if (n <= (1u << kPosBits))
-        r = encode_block_v5<false, false, false, false, false, true>(s, n, d, n, Tl, Xl, nullptr,
-                                                                     LinkArgs{0, 0, 0, true}, pub + b);
+        r = encode_block_v5<false, false, false, false, false, true, false, XC>(s, n, d, n, Tl, Xl, nullptr,
+                                                                                LinkArgs{0, 0, 0, true}, pub + b);
     else
         r = encode_block<false, false, false>(s, n, d, n, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
     if (laneid() == 0) csize[b] = r;
@@ -1509,22 +1389,23 @@ __global__ void __launch_bounds__(64) k_xchg_order(uint32_t* ok) {
     if (L == 0) *ok = all ? 1u : 0u;
 }
 
-// once per device: hipSuccess when the check passed (or the encoder does not
-// use exchanges), hipErrorNotSupported (and one stderr line) when it failed.
-// A call whose stream is being captured into a graph skips the check until
-// an uncaptured call runs it.
-hipError_t encoder_ready(hipStream_t st) {
-    if (!LZ4MT_ENC_XCHG && !LZ4MT_ENC_XCHG_SP) return hipSuccess;
-    static std::atomic<int> state[64];   // 0 unchecked, 1 passed, -1 failed
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    const int v = state[dev].load(std::memory_order_acquire);
-    if (v) return v > 0 ? hipSuccess : hipErrorNotSupported;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (st && hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return hipSuccess;
+// Which table probe the frame encoders run on the current device (*xc):
+//   true   the exchange probe: k_xchg_order passed on this device (run once);
+//   false  the read-back probe (no ordering assumed): the check failed (one
+//          stderr line), LZ4MT_AMD_ENC_PROBE=readback forces it, or `st` is
+//          being captured into a graph before any uncaptured call checked
+//          this device (the check synchronises; the read-back probe is exact
+//          on any device, so the captured graph is right either way).
+// Returns a HIP error only when the check itself could not run.
+static std::atomic<int> g_xchg_state[64];   // per device: 0 unchecked, 1 passed, -1 failed
+static bool probe_forced_readback() {
+    const char* e = getenv("LZ4MT_AMD_ENC_PROBE");
+    return e && !strcmp(e, "readback");
+}
+static hipError_t xchg_check(int dev) {   // runs k_xchg_order once on `dev` (the current device)
     static std::mutex mu;
     std::lock_guard<std::mutex> g(mu);
-    if (state[dev].load()) return state[dev].load() > 0 ? hipSuccess : hipErrorNotSupported;
+    if (g_xchg_state[dev].load()) return hipSuccess;
     hipStream_t ps = nullptr;
     uint32_t* d = nullptr;
     uint32_t h = 0;
@@ -1536,34 +1417,67 @@ hipError_t encoder_ready(hipStream_t st) {
     }
     if (e == hipSuccess) e = hipMemcpyAsync(&h, d, 4, hipMemcpyDeviceToHost, ps);
     if (e == hipSuccess) e = hipStreamSynchronize(ps);
-    if (d) hipFree(d);
-    if (ps) hipStreamDestroy(ps);
+    if (d) (void)hipFree(d);
+    if (ps) (void)hipStreamDestroy(ps);
     if (e != hipSuccess) return e;
-    state[dev].store(h == 1 ? 1 : -1, std::memory_order_release);
+    g_xchg_state[dev].store(h == 1 ? 1 : -1, std::memory_order_release);
     if (h != 1)
         fprintf(stderr, "lz4mt_amd: device %d does not apply a wave's same-address LDS exchanges in lane order; "
-                        "the block encoder (LZ4MT_ENC_XCHG) cannot run here\n", dev);
-    return h == 1 ? hipSuccess : hipErrorNotSupported;
+                        "the block encoders use the read-back table probe there\n", dev);
+    return hipSuccess;
+}
+hipError_t encoder_path(hipStream_t st, bool* xc) {
+    *xc = false;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (probe_forced_readback()) return hipSuccess;
+    int v = g_xchg_state[dev].load(std::memory_order_acquire);
+    if (v == 0) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (st && hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return hipSuccess;
+        if (const hipError_t e = xchg_check(dev); e != hipSuccess) return e;
+        v = g_xchg_state[dev].load(std::memory_order_acquire);
+    }
+    *xc = v > 0;
+    return hipSuccess;
+}
+// the diagnostic kernels exist only with the exchange probe
+hipError_t encoder_ready(hipStream_t st) {
+    bool xc = false;
+    if (const hipError_t e = encoder_path(st, &xc); e != hipSuccess) return e;
+    return xc ? hipSuccess : hipErrorNotSupported;
 }
 
 extern "C" int lz4mtHipCheckEncoderOrder(void) {
+    int n = 0, dev = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+        return -1;
+    if (g_xchg_state[dev].load() == 0 && xchg_check(dev) != hipSuccess) return -1;
+    return g_xchg_state[dev].load() > 0 ? 1 : 0;
+}
+
+extern "C" int lz4mtHipEncoderProbe(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -1;
-    return encoder_ready(nullptr) == hipSuccess ? 1 : 0;
+    bool xc = false;
+    if (encoder_path(nullptr, &xc) != hipSuccess) return -1;
+    return xc ? 1 : 0;
 }
 
 hipError_t launch_encode_pub(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                              uint8_t* slots, int32_t* csize, uint32_t* pub, hipStream_t st) {
-    if (const hipError_t r = encoder_ready(st); r != hipSuccess) return r;
+    bool xc = true;
+    if (const hipError_t r = encoder_path(st, &xc); r != hipSuccess) return r;
     if (nBlocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_encode_pub, dim3(nBlocks), dim3(64), 0, st, src, srcSize, blockSize, slots,
-                       (uint64_t)blockSize, csize, pub);
+    hipLaunchKernelGGL(xc ? k_encode_pub<true> : k_encode_pub<false>, dim3(nBlocks), dim3(64), 0, st, src, srcSize,
+                       blockSize, slots, (uint64_t)blockSize, csize, pub);
     return hipGetLastError();
 }
 
 // The v5 encoder with the 3-byte table (V5Geo P17): 14.25 KiB of LDS, 11
 // waves per CU instead of 8.  Blocks of 65 547 B .. 4 MiB; others are left
 // to k_encode (csize untouched here).
+template <bool XC>
 __global__ void __launch_bounds__(64) k_encode_p17(const uint8_t* __restrict__ src, uint64_t srcSize,
                                                    uint32_t blockSize, uint8_t* __restrict__ slots,
                                                    uint64_t slotStride, uint32_t capOverride,
@@ -1576,7 +1490,7 @@ __global__ void __launch_bounds__(64) k_encode_p17(const uint8_t* __restrict__ s
     const uint32_t cap = (capOverride == 0xFFFFFFFFu) ? n : capOverride;   // lz4mt: cap = n
     l_u8* Xl = (l_u8*)PLDS + 3 * (4096 + 64);
     int32_t r;
-    [[clang::always_inline]] r = encode_block_v5<false, false, false, false, true>(
+    [[clang::always_inline]] r = encode_block_v5<false, false, false, false, true, false, false, XC>(
         gptr(src) + off, n, gptr(slots) + (uint64_t)b * slotStride, cap, (l_u32*)PLDS, Xl, nullptr);
     if (laneid() == 0) csize[b] = r;
 }
@@ -1610,12 +1524,10 @@ __global__ void __launch_bounds__(64) k_encode_stats(const uint8_t* __restrict__
 // Frames of blocks below 65 547 bytes (-B4: 64 KiB): every block uses the
 // byU16 table, so the kernel carries the 8192-entry table (34.3 KiB of LDS,
 // 4 waves per CU) instead of k_encode's 20 KiB.
-#ifndef LZ4MT_E16_SPLIT
-#define LZ4MT_E16_SPLIT 1
-#endif
-constexpr bool kE16Split = LZ4MT_E16_SPLIT;
-constexpr uint32_t kE16TabWords = kE16Split ? (8192 + 64) * 3 / 4 : 8192 + 64;
+// The table is split (u16 positions + u8 tags, 26.3 KiB, 6 waves per CU).
+constexpr uint32_t kE16TabWords = (8192 + 64) * 3 / 4;
 constexpr uint32_t kE16Words = kE16TabWords + (kSR + kSRMirror) / 4;
+template <bool XC>
 __global__ void __launch_bounds__(64) k_encode16(const uint8_t* __restrict__ src, uint64_t srcSize,
                                                  uint32_t blockSize, uint8_t* __restrict__ slots,
                                                  uint64_t slotStride, uint32_t capOverride,
@@ -1625,8 +1537,9 @@ __global__ void __launch_bounds__(64) k_encode16(const uint8_t* __restrict__ src
     const uint64_t off = (uint64_t)b * blockSize;
     const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
     const uint32_t cap = (capOverride == 0xFFFFFFFFu) ? n : capOverride;   // lz4mt: cap = n
-    const int32_t r = encode_block_v5<false, true, kE16Split>(gptr(src) + off, n, gptr(slots) + (uint64_t)b * slotStride,
-                                                              cap, (l_u32*)E16, (l_u8*)(E16 + kE16TabWords), nullptr);
+    const int32_t r = encode_block_v5<false, true, true, false, false, false, false, XC>(
+        gptr(src) + off, n, gptr(slots) + (uint64_t)b * slotStride, cap, (l_u32*)E16, (l_u8*)(E16 + kE16TabWords),
+        nullptr);
     if (laneid() == 0) csize[b] = r;
 }
 
@@ -1650,7 +1563,7 @@ __device__ __forceinline__ uint32_t link_rebase(uint32_t e, uint32_t n) {
 // the table between calls: read unless `fresh`, written at the end.  The
 // per-block lz4 mode (prefix / external dictionary, dictionary size) comes
 // from the host's replay of the reference's buffer handling (LinkPlan).
-template <bool XH>
+template <bool XH, bool XC>
 __global__ void __launch_bounds__(64) k_encode_linked(const uint8_t* __restrict__ src, uint64_t srcSize,
                                                       uint32_t blockSize, uint32_t nBlocks,
                                                       uint8_t* __restrict__ slots, const LinkPlan* __restrict__ plan,
@@ -1678,7 +1591,7 @@ __global__ void __launch_bounds__(64) k_encode_linked(const uint8_t* __restrict_
         const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
         const LinkPlan pl = plan[b];
         const LinkArgs lk{pl.lowIn, pl.lowDict, pl.candLow, fresh && b == 0, pl.shift};
-        const int32_t r = encode_block_v5<false, false, false, true, false, false, XH>(
+        const int32_t r = encode_block_v5<false, false, false, true, false, false, XH, XC>(
             gptr(src) + off - kLinkO0, kLinkO0 + n, gptr(slots) + off, n - 1, Tl, Xl, nullptr, lk);
         if (L == 0) csize[b] = r;
         WAVE_SYNC();
@@ -1695,9 +1608,12 @@ __global__ void __launch_bounds__(64) k_encode_linked(const uint8_t* __restrict_
 hipError_t launch_encode_linked(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                                 uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh, bool xh,
                                 int32_t* csize, hipStream_t st) {
-    if (const hipError_t r = encoder_ready(st); r != hipSuccess) return r;
+    bool xc = true;
+    if (const hipError_t r = encoder_path(st, &xc); r != hipSuccess) return r;
     if (nBlocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(xh ? k_encode_linked<true> : k_encode_linked<false>, dim3(1), dim3(64), 0, st, src, srcSize,
+    hipLaunchKernelGGL(xh ? (xc ? k_encode_linked<true, true> : k_encode_linked<true, false>)
+                          : (xc ? k_encode_linked<false, true> : k_encode_linked<false, false>),
+                       dim3(1), dim3(64), 0, st, src, srcSize,
                        blockSize, nBlocks, slots, plan, table, fresh ? 1 : 0, csize, (const uint32_t*)nullptr,
                        (const uint32_t*)nullptr, (const uint32_t*)nullptr);
     return hipGetLastError();
@@ -1720,7 +1636,7 @@ hipError_t launch_encode_linked(const uint8_t* src, uint64_t srcSize, uint32_t b
 // finishes from the first unsettled block (its entry is exact).
 //   ctl words: changed[kLinkRounds + 1] | first[kLinkRounds + 1] |
 //              flag[nBlocks] | enc[nBlocks]
-template <bool XH>
+template <bool XH, bool XC>
 __global__ void __launch_bounds__(64) k_encode_linked_round(const uint8_t* __restrict__ src, uint64_t srcSize,
                                                             uint32_t blockSize, uint8_t* __restrict__ slots,
                                                             const LinkPlan* __restrict__ plan,
@@ -1746,7 +1662,7 @@ __global__ void __launch_bounds__(64) k_encode_linked_round(const uint8_t* __res
     const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
     const LinkPlan pl = plan[b];
     const LinkArgs lk{pl.lowIn, pl.lowDict, pl.candLow, fr, pl.shift};
-    const int32_t r = encode_block_v5<false, false, false, true, false, false, XH>(
+    const int32_t r = encode_block_v5<false, false, false, true, false, false, XH, XC>(
         gptr(src) + off - kLinkO0, kLinkO0 + n, gptr(slots) + off, n - 1, Tl, (l_u8*)X, nullptr, lk);
     if (L == 0) {
         csize[b] = r;
@@ -1796,6 +1712,7 @@ __global__ void __launch_bounds__(256) k_link_settle(const uint32_t* __restrict_
 // whose head entry changed.  Blocks inside a chain are exact given the head,
 // so only chain heads are compared (k_link_settle_chain) and can be the
 // serial kernel's first unsettled block.
+template <bool XC>
 __global__ void __launch_bounds__(64) k_encode_linked_chain(const uint8_t* __restrict__ src, uint64_t srcSize,
                                                             uint32_t blockSize, uint32_t nBlocks, uint32_t G,
                                                             uint8_t* __restrict__ slots,
@@ -1824,8 +1741,8 @@ __global__ void __launch_bounds__(64) k_encode_linked_chain(const uint8_t* __res
         const uint32_t n = (uint32_t)((srcSize - off) < blockSize ? (srcSize - off) : blockSize);
         const LinkPlan pl = plan[b];
         const LinkArgs lk{pl.lowIn, pl.lowDict, pl.candLow, fr && b == 0};
-        const int32_t r = encode_block_v5<false, false, false, true>(gptr(src) + off - kLinkO0, kLinkO0 + n,
-                                                                     gptr(slots) + off, n - 1, Tl, (l_u8*)X, nullptr, lk);
+        const int32_t r = encode_block_v5<false, false, false, true, false, false, false, XC>(
+            gptr(src) + off - kLinkO0, kLinkO0 + n, gptr(slots) + off, n - 1, Tl, (l_u8*)X, nullptr, lk);
         if (L == 0) csize[b] = r;
         WAVE_SYNC();
         for (uint32_t i = L; i < 4096; i += 64) Tl[i] = link_rebase(Tl[i], n);
@@ -1888,6 +1805,7 @@ __global__ void k_link_init(uint32_t* __restrict__ ctl, uint32_t nBlocks) {
 // the table the stream has, and round 0 then rarely needs a second round.
 // The warm parse writes its (discarded) output into block b's own slot,
 // which round 0 overwrites.  A wrong guess costs a round, never a byte.
+template <bool XC>
 __global__ void __launch_bounds__(64) k_link_warm(const uint8_t* __restrict__ src, uint32_t blockSize, uint32_t W,
                                                   uint8_t* __restrict__ slots, uint32_t* __restrict__ entry) {
     ENCODE_LDS
@@ -1897,8 +1815,8 @@ __global__ void __launch_bounds__(64) k_link_warm(const uint8_t* __restrict__ sr
     const uint32_t b = blockIdx.x + 1;
     const uint64_t off = (uint64_t)b * blockSize;   // block b's start; the warm bytes end there
     const LinkArgs lk{kLinkO0, kLinkO0, kLinkO0, true};   // no history: a fresh stream over the W bytes
-    (void)encode_block_v5<false, false, false, true>(gptr(src) + off - W - kLinkO0, kLinkO0 + W, gptr(slots) + off,
-                                                     W + W / 255 + 16, Tl, (l_u8*)X, nullptr, lk);
+    (void)encode_block_v5<false, false, false, true, false, false, false, XC>(
+        gptr(src) + off - W - kLinkO0, kLinkO0 + W, gptr(slots) + off, W + W / 255 + 16, Tl, (l_u8*)X, nullptr, lk);
     WAVE_SYNC();
     uint32_t* o = entry + (uint64_t)b * 4096;
     for (uint32_t i = L; i < 4096; i += 64) {
@@ -1942,7 +1860,8 @@ uint64_t link_round_bytes(uint64_t nBlocks) {
 hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks,
                                     uint8_t* slots, const LinkPlan* plan, uint32_t* table, bool fresh, bool xh,
                                     uint32_t* scratch, int32_t* csize, int rounds, hipStream_t st) {
-    if (const hipError_t r = encoder_ready(st); r != hipSuccess) return r;
+    bool xc = true;
+    if (const hipError_t r = encoder_path(st, &xc); r != hipSuccess) return r;
     if (nBlocks == 0) return hipSuccess;
     if (rounds < 1 || rounds > kLinkRounds) rounds = kLinkRounds;
     uint32_t* entry = scratch;
@@ -1957,14 +1876,14 @@ hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32
     if (hipMemsetAsync(entry, 0, (uint64_t)nBlocks * 4096 * 4, st) != hipSuccess) return hipErrorUnknown;
     const uint32_t warm = link_cold() ? 0u : link_warm_bytes(blockSize);
     if (nBlocks > 1 && warm)
-        hipLaunchKernelGGL(k_link_warm, dim3(nBlocks - 1), dim3(64), 0, st, src, blockSize, warm, slots, entry);
+        hipLaunchKernelGGL(xc ? k_link_warm<true> : k_link_warm<false>, dim3(nBlocks - 1), dim3(64), 0, st, src, blockSize, warm, slots, entry);
     const uint32_t nInit = 2 * (kLinkRounds + 1) + nBlocks;
     hipLaunchKernelGGL(k_link_init, dim3((nInit + 255) / 256), dim3(256), 0, st, ctl, nBlocks);
     // chains only below 1 MiB; the reference's own-history blocks (xh) are 1 / 4 MiB
     const uint32_t G = xh ? 0u : link_chain(blockSize);
     for (int r = 0; r < rounds && G > 1; ++r) {   // chained rounds
         const uint32_t nc = (nBlocks + G - 1) / G;
-        hipLaunchKernelGGL(k_encode_linked_chain, dim3(nc), dim3(64), 0, st, src, srcSize, blockSize, nBlocks, G, slots,
+        hipLaunchKernelGGL(xc ? k_encode_linked_chain<true> : k_encode_linked_chain<false>, dim3(nc), dim3(64), 0, st, src, srcSize, blockSize, nBlocks, G, slots,
                            plan, (const uint32_t*)table, fresh ? 1 : 0, (const uint32_t*)entry, exitT, csize,
                            (const uint32_t*)(changed + r), (const uint32_t*)flag, enc, (uint32_t)r);
         if (nc > 1)
@@ -1973,7 +1892,9 @@ hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32
                                firstU + r + 1, (uint32_t)r);
     }
     for (int r = 0; r < rounds && G <= 1; ++r) {
-        hipLaunchKernelGGL(xh ? k_encode_linked_round<true> : k_encode_linked_round<false>, dim3(nBlocks), dim3(64), 0,
+        hipLaunchKernelGGL(xh ? (xc ? k_encode_linked_round<true, true> : k_encode_linked_round<true, false>)
+                              : (xc ? k_encode_linked_round<false, true> : k_encode_linked_round<false, false>),
+                           dim3(nBlocks), dim3(64), 0,
                            st, src, srcSize, blockSize, slots, plan, (const uint32_t*)table, fresh ? 1 : 0,
                            (const uint32_t*)entry, exitT, csize, (const uint32_t*)(changed + r), (const uint32_t*)flag,
                            enc, (uint32_t)r);
@@ -1983,8 +1904,9 @@ hipError_t launch_encode_linked_par(const uint8_t* src, uint64_t srcSize, uint32
                                firstU + r + 1, (uint32_t)r);
     }
     // a single block settles in round 0 (changed[1] stays 0)
-    hipLaunchKernelGGL(xh ? k_encode_linked<true> : k_encode_linked<false>, dim3(1), dim3(64), 0, st, src, srcSize,
-                       blockSize, nBlocks, slots, plan, table, fresh ? 1 : 0, csize,
+    hipLaunchKernelGGL(xh ? (xc ? k_encode_linked<true, true> : k_encode_linked<true, false>)
+                          : (xc ? k_encode_linked<false, true> : k_encode_linked<false, false>),
+                       dim3(1), dim3(64), 0, st, src, srcSize, blockSize, nBlocks, slots, plan, table, fresh ? 1 : 0, csize,
                        (const uint32_t*)(changed + rounds), (const uint32_t*)(firstU + rounds),
                        (const uint32_t*)entry);
     hipLaunchKernelGGL(k_link_final, dim3(1), dim3(256), 0, st, (const uint32_t*)exitT, nBlocks,
@@ -2021,7 +1943,10 @@ __global__ void __launch_bounds__(64) k_encode_overlap(const uint8_t* __restrict
     const uint64_t lo = (uint64_t)b * S > ov ? (uint64_t)b * S - ov : 0u;
     const uint64_t hi = min<uint64_t>((uint64_t)(b + 1) * S, srcSize);
     const uint32_t n = (uint32_t)(hi - lo);
-    if (n < (uint32_t)kLimit64K || n > (1u << kPosBits)) return;
+    if (n < (uint32_t)kLimit64K || n > (1u << kPosBits)) {   // not a v5 block: no size
+        if (laneid() == 0) csize[b] = -1;
+        return;
+    }
     l_u8* ring = P17 ? (l_u8*)OLDS + 3 * (4096 + 64) : (l_u8*)(OLDS + 4352);
     // inlined here, so k_encode / k_encode_p17 stay the only call sites of
     // their instantiations (a second call site outlines the encoder into a
@@ -2053,21 +1978,23 @@ static uint32_t enc_lds_pad() {
 
 hipError_t launch_encode(const uint8_t* src, uint64_t srcSize, uint32_t blockSize, uint32_t nBlocks, uint8_t* slots,
                          uint64_t slotStride, uint32_t capOverride, int32_t* csize, hipStream_t st) {
-    if (const hipError_t r = encoder_ready(st); r != hipSuccess) return r;
+    bool xc = true;
+    if (const hipError_t r = encoder_path(st, &xc); r != hipSuccess) return r;
     if (nBlocks == 0) return hipSuccess;
     const uint32_t pad = enc_lds_pad();
+    const auto kEnc = xc ? k_encode<true> : k_encode<false>;
     if (blockSize < (uint32_t)kLimit64K)
-        hipLaunchKernelGGL(k_encode16, dim3(nBlocks), dim3(64), pad, st, src, srcSize, blockSize, slots, slotStride,
+        hipLaunchKernelGGL(xc ? k_encode16<true> : k_encode16<false>, dim3(nBlocks), dim3(64), pad, st, src, srcSize, blockSize, slots, slotStride,
                            capOverride, csize);
     else if (enc_p17(blockSize) && blockSize <= (1u << kPosBits)) {   // 3-byte table; a short last block on k_encode
-        hipLaunchKernelGGL(k_encode_p17, dim3(nBlocks), dim3(64), pad, st, src, srcSize, blockSize, slots, slotStride,
+        hipLaunchKernelGGL(xc ? k_encode_p17<true> : k_encode_p17<false>, dim3(nBlocks), dim3(64), pad, st, src, srcSize, blockSize, slots, slotStride,
                            capOverride, csize);
         const uint64_t lastOff = (uint64_t)(nBlocks - 1) * blockSize;
         if (srcSize - lastOff < (uint64_t)kLimit64K)
-            hipLaunchKernelGGL(k_encode, dim3(1), dim3(64), 0, st, src + lastOff, srcSize - lastOff, blockSize,
+            hipLaunchKernelGGL(kEnc, dim3(1), dim3(64), 0, st, src + lastOff, srcSize - lastOff, blockSize,
                                slots + (nBlocks - 1) * slotStride, slotStride, capOverride, csize + (nBlocks - 1));
     } else
-        hipLaunchKernelGGL(k_encode, dim3(nBlocks), dim3(64), pad, st, src, srcSize, blockSize, slots, slotStride,
+        hipLaunchKernelGGL(kEnc, dim3(nBlocks), dim3(64), pad, st, src, srcSize, blockSize, slots, slotStride,
                            capOverride, csize);
     return hipGetLastError();
 }
@@ -2116,48 +2043,20 @@ constexpr uint32_t kNxPast = 1024, kNxDead = 1026;
 #define LZ4MT_FAR_TAB 8
 #endif
 constexpr int kFarTab = LZ4MT_FAR_TAB;
-// LZ4MT_FAR_LANES=1: a batch's far-match parameters are read straight from
-// their lanes (s_ff1 over the far mask + v_readlane) instead of a rank-
-// ordered LDS table read back by broadcast, so no far load waits on an LDS
-// round trip (k_decode 31.36 -> 31.03 ms at 8 GiB B7, two passes each,
-// profiles/r04c_decoder_ab.txt; A/B: -DLZ4MT_FAR_LANES=0)
-#ifndef LZ4MT_FAR_LANES
-#define LZ4MT_FAR_LANES 1
-#endif
-// LZ4MT_ORD_LANES=1: the same for the ordered matches (5d): each one's
-// parameters by v_readlane from its lane, no rank table in LDS (k_decode
-// 31.03 -> 30.90 ms, profiles/r04f_decoder_ordlanes_ab.txt)
-#ifndef LZ4MT_ORD_LANES
-#define LZ4MT_ORD_LANES 1
-#endif
-// LZ4MT_FAR_DEFER=1: a batch's far bytes (up to kFarTab matches) are written
-// into the ring at the NEXT batch's first use of the ring (after its token
-// parse), so the far loads' latency overlaps the end of this batch and the
-// next batch's parse instead of stalling 5c; written at once when one of the
-// batch's ordered matches reads a far output, and before any serial
-// sequence (requires LZ4MT_FAR_LANES).  Off: k_decode 30.9 -> 34.1 ms.
-// vmcnt retires in issue order, so the next batch's first waited load (its
-// input refill) waits for the deferred far loads anyway, and the loop-
-// carried far registers double the kernel's VGPRs (87 -> 175) and add SGPR
-// spills (profiles/r04g_decoder_far_defer_ab.txt)
-#ifndef LZ4MT_FAR_DEFER
-#define LZ4MT_FAR_DEFER 0
-#endif
-static_assert(!LZ4MT_FAR_DEFER || LZ4MT_FAR_LANES, "deferred far writes read the far lanes' parameters");
+// A batch's far-match parameters are read straight from their lanes (s_ff1
+// over the far mask + v_readlane) instead of a rank-ordered LDS table read
+// back by broadcast, so no far load waits on an LDS round trip (k_decode
+// 31.36 -> 31.03 ms at 8 GiB B7, profiles/r04c_decoder_ab.txt); the ordered
+// matches (5d) likewise (31.03 -> 30.90 ms, r04f_decoder_ordlanes_ab.txt).
+// Rejected (records kept): deferring a batch's far-byte writes to the next
+// batch (34.1 ms: vmcnt retires in issue order and the loop-carried far
+// registers double the VGPRs, r04g_decoder_far_defer_ab.txt); a two-hop
+// table beside the next table (33.9 ms, r04c_decoder_ab.txt).
 static_assert(kFarTab >= 1 && kFarTab <= 24, "far table");
-constexpr int32_t kFpOff = kInWin + 128 + 1040;   // far-match table of a batch (kFarTab x 16 B)
-// LZ4MT_HOP2=1: the batch's hop takes two sequences per dependent LDS read:
-// D2[p] = next(next(p)) - p as a byte (0 = past the candidates, a complex
-// token or 256+ bytes on: one more single hop), beside the next table; the
-// single hop to the odd sequence is read in the same round.  Off: building
-// D2 (8 conflicting LDS gathers per lane) and the per-pair scalar branch cost
-// more than the halved chain saves (k_decode 31.0 -> 33.9 ms at 8 GiB B7,
-// profiles/r04c_decoder_ab.txt)
-#ifndef LZ4MT_HOP2
-#define LZ4MT_HOP2 0
-#endif
-constexpr int32_t kD2Off = kFpOff + 16 * kFarTab;   // 512 two-hop deltas + 2 sentinels (PAST, DEAD) = 0
-[[maybe_unused]] constexpr int32_t kWinAlloc = kD2Off + (LZ4MT_HOP2 ? 520 : 0);
+// (the window allocation keeps the 16 B x kFarTab the far table had: the
+// decoder's LDS layout, and so its timing, is unchanged by its removal)
+constexpr int32_t kFpOff = kInWin + 128 + 1040;
+[[maybe_unused]] constexpr int32_t kWinAlloc = kFpOff + 16 * kFarTab;
 static_assert(kRing + kWinAlloc <= 20480 || kRing != 16384, "decoder LDS: 8 waves per CU need <= 20 KiB each");
 
 template <bool ST>
@@ -2176,27 +2075,6 @@ struct Dec {
     int64_t flushed;      // [0, flushed) stored to dst
     int64_t completed;    // [0, completed) known complete in memory
     int32_t lowP;         // lowest position a match may read: 0, or -65536 with a 64 KiB prefix before dst
-    // far bytes of the last batch not yet in the ring (LZ4MT_FAR_DEFER):
-    // pfN matches, ring target / length per match (uniform), their bytes per lane
-    uint32_t pfN;
-    uint32_t pfOm[kFarTab], pfLen[kFarTab], pfv[kFarTab], pfv2[kFarTab];
-
-    __device__ __forceinline__ void flush_far() {
-        if (!LZ4MT_FAR_DEFER || pfN == 0) return;
-        const uint32_t L = laneid();
-        l_u8* const dummy = win + kInWin;
-#pragma unroll
-        for (int g = 0; g < kFarTab; ++g) {
-            if ((uint32_t)g < pfN) {
-                const uint32_t qy = pfOm[g], qz = pfLen[g];
-                *(L < qz ? ring + ((qy + L) & (kRing - 1)) : dummy + L) = (uint8_t)pfv[g];
-                if (qz > 64) *(L + 64 < qz ? ring + ((qy + 64 + L) & (kRing - 1)) : dummy + 64 + L) = (uint8_t)pfv2[g];
-            }
-        }
-        pfN = 0;
-        WAVE_SYNC();
-    }
-
     __device__ __forceinline__ void refill(int64_t i) {
         const uintptr_t base = (reinterpret_cast<uintptr_t>(src) + (uintptr_t)i) & ~uintptr_t(15);
         wlo = (int64_t)(base - reinterpret_cast<uintptr_t>(src));
@@ -2343,7 +2221,6 @@ struct Dec {
         // every sequence is validated against 1.9.3's fast-loop conditions
         // below; this guard only keeps the batch machinery inside the block
         if (ip64 + 17 > iend64 || op64 + 64 > oend64) {
-            flush_far();   // the serial path reads the ring
             return 0;
         }
         STAMP_ADD(0, ts);
@@ -2396,40 +2273,6 @@ struct Dec {
             *(l_u4*)(nxb + 16 * L) = (v4u){nv[0], nv[1], nv[2], nv[3]};
             WAVE_SYNC();
             uint32_t x = 0, startA = 0, nextA = kNxDead;
-#if LZ4MT_HOP2
-            l_u8* const d2b = win + kD2Off;
-            {   // D2 for positions 8L .. 8L+7: next(next(p)) from the table just written
-                uint32_t q0 = 0, q1 = 0;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const uint32_t n1 = (nv[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;   // next(p), a byte offset
-                    const uint32_t nn = *(l_u16*)(nxb + n1);   // next(n1); PAST / DEAD map to DEAD
-                    const uint32_t t = nn < 1024 ? (nn >> 1) - (8 * L + (uint32_t)e) : 0u;
-                    const uint32_t v = t < 256 ? t : 0u;
-                    if (e < 4) q0 |= v << (8 * e);
-                    else q1 |= v << (8 * (e - 4));
-                }
-                *(l_u64*)(d2b + 8 * L) = ((uint64_t)q1 << 32) | q0;
-                WAVE_SYNC();
-            }
-            for (uint32_t m0 = 0; m0 < 64; m0 += 8) {
-#pragma unroll
-                for (uint32_t e = 0; e < 8; e += 2) {
-                    // sequence m0+e starts at x; x1 = its successor, x2 = the one after
-                    const uint32_t x1 = *(l_u16*)(nxb + x);
-                    const uint32_t dd = (uint32_t)__builtin_amdgcn_readfirstlane((int)d2b[x >> 1]);
-                    uint32_t x2;
-                    if (dd) x2 = x + 2 * dd;
-                    else x2 = *(l_u16*)(nxb + x1);
-                    nextA = L == m0 + e ? x1 : nextA;
-                    startA = L == m0 + e + 1 ? x1 : startA;
-                    nextA = L == m0 + e + 1 ? x2 : nextA;
-                    startA = L == m0 + e + 2 ? x2 : startA;
-                    x = x2;
-                }
-                if ((uint32_t)__builtin_amdgcn_readfirstlane((int)x) == kNxDead) break;
-            }
-#else
             for (uint32_t m0 = 0; m0 < 64; m0 += 8) {
 #pragma unroll
                 for (uint32_t e = 0; e < 8; ++e) {
@@ -2439,15 +2282,11 @@ struct Dec {
                 }
                 if ((uint32_t)__builtin_amdgcn_readfirstlane((int)x) == kNxDead) break;
             }
-#endif
             cnt = (uint32_t)__popcll(bal(nextA != kNxDead));
             startRel = startA >> 1;
         }
         STAMP_ADD(12, ts);
-        if (cnt == 0) {
-            flush_far();
-            return 0;
-        }
+        if (cnt == 0) return 0;
         if (ST) acc[4] += 1;
         // 3. fields (lane j = sequence j), branch-free
         const bool act = L < cnt;
@@ -2486,7 +2325,6 @@ struct Dec {
         const uint64_t bad = ballot(act && !ok);
         const uint32_t nb = bad ? (uint32_t)(__ffsll((long long)bad) - 1) : cnt;
         STAMP_ADD(13, ts);
-        flush_far();   // the last batch's far bytes: before this batch's copies and flushes read the ring
         if (nb == 0) return 0;
         const bool in = L < nb;
         if (ST) { acc[6] += nb; acc[8] += nb; }
@@ -2500,19 +2338,10 @@ struct Dec {
         const bool ord = in && !far && (longLit || src + (int32_t)mlen > op || lit + mlen > 128);
         const uint64_t farM = ballot(far), ordM = ballot(ord);
         // 5a. far loads (up to 8 sequences, lane per byte), in flight during 5b.
-        // The far lanes publish (source, ring target, length) in rank order to
-        // a small LDS table that the wave reads back by broadcast.
-#if LZ4MT_FAR_DEFER
-        // the far loads land straight in the pending registers (flush_far ran
-        // above): no register move that would wait for them
-        uint32_t (&fv)[kFarTab] = pfv;
-        uint32_t (&fv2)[kFarTab] = pfv2;
-#else
+        // Each far sequence's parameters come from its lane (v_readlane).
         uint32_t fv[kFarTab], fv2[kFarTab];
-#endif
         const uint32_t fr = __builtin_amdgcn_mbcnt_hi((uint32_t)(farM >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)farM, 0u));
         const uint32_t nf8 = min((uint32_t)__popcll(farM), (uint32_t)kFarTab);
-#if LZ4MT_FAR_LANES
         uint32_t flane[kFarTab];   // lane of the g-th far sequence (uniform)
         if (farM) {
             if (completed < (int64_t)ringLo) {   // their bytes were stored to dst: make sure the stores landed
@@ -2535,28 +2364,6 @@ struct Dec {
                 }
             }
         }
-#else
-        l_u4* const fprm = (l_u4*)(win + kFpOff);
-        if (farM) {
-            if (completed < (int64_t)ringLo) {   // their bytes were stored to dst: make sure the stores landed
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                completed = flushed;
-            }
-            if (ST) acc[7] += __popcll(farM);
-            if (far && fr < (uint32_t)kFarTab) fprm[fr] = (v4u){(uint32_t)src, (uint32_t)om & (kRing - 1), mlen, 0u};
-            WAVE_SYNC();
-#pragma unroll
-            for (int g = 0; g < kFarTab; ++g) {
-                fv[g] = 0; fv2[g] = 0;
-                if ((uint32_t)g < nf8) {
-                    const v4u q = fprm[g];   // bytes past the match repeat its last one (never written)
-                    const int64_t fs = (int32_t)q.x;   // a prefix source is negative
-                    fv[g] = dst[fs + min(L, q.z - 1)];
-                    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)q.z) > 64) fv2[g] = dst[fs + min(L + 64, q.z - 1)];
-                }
-            }
-        }
-#endif
         STAMP_ADD(15, ts);
         // 5b. literal runs of every sequence + grouped matches, 8 per group
         const uint32_t tot = longLit ? 0u : lit + ((in && !far && !ord) ? mlen : 0u);
@@ -2655,44 +2462,14 @@ struct Dec {
         }
         // 5c. far bytes into the ring at the match outputs
         if (farM) {
-#if LZ4MT_FAR_DEFER
-            // deferred to the next batch unless an ordered match of this one
-            // reads a far output (its source range meets [farLo, farHi))
-            int32_t farLo = INT32_MAX, farHi = INT32_MIN;
 #pragma unroll
             for (int g = 0; g < kFarTab; ++g) {
                 if ((uint32_t)g < nf8) {
-                    const int32_t o = (int32_t)rdlane((uint32_t)om, (int)flane[g]);
-                    farLo = min(farLo, o);
-                    farHi = max(farHi, o + (int32_t)rdlane(mlen, (int)flane[g]));
-                }
-            }
-            const bool deferFar = !ballot(ord && src < farHi && src + (int32_t)mlen > farLo);
-#else
-            const bool deferFar = false;
-#endif
-#pragma unroll
-            for (int g = 0; g < kFarTab; ++g) {
-                if ((uint32_t)g < nf8) {
-#if LZ4MT_FAR_DEFER
-                    if (deferFar) {   // fv / fv2 are pfv / pfv2
-                        pfOm[g] = rdlane((uint32_t)om, (int)flane[g]) & (kRing - 1);
-                        pfLen[g] = rdlane(mlen, (int)flane[g]);
-                        continue;
-                    }
-#endif
-#if LZ4MT_FAR_LANES
                     const uint32_t qy = rdlane((uint32_t)om, (int)flane[g]) & (kRing - 1);
                     const uint32_t qz = rdlane(mlen, (int)flane[g]);
                     *(L < qz ? ringp + ((qy + L) & (kRing - 1)) : dummy + L) = (uint8_t)fv[g];
                     if (qz > 64)
                         *(L + 64 < qz ? ringp + ((qy + 64 + L) & (kRing - 1)) : dummy + 64 + L) = (uint8_t)fv2[g];
-#else
-                    const v4u q = fprm[g];
-                    *(L < q.z ? ringp + ((q.y + L) & (kRing - 1)) : dummy + L) = (uint8_t)fv[g];
-                    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)q.z) > 64)
-                        *(L + 64 < q.z ? ringp + ((q.y + 64 + L) & (kRing - 1)) : dummy + 64 + L) = (uint8_t)fv2[g];
-#endif
                 }
             }
             uint64_t farLeft = ballot(far && fr >= (uint32_t)kFarTab);
@@ -2707,12 +2484,8 @@ struct Dec {
                 if (L + 64 < jm) ring[(jo + 64 + L) & (kRing - 1)] = (uint8_t)a1;
                 farLeft &= farLeft - 1;
             }
-            if (deferFar) {
-                pfN = nf8;   // written by flush_far; their loads stay in flight until then
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                completed = flushed;
-            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            completed = flushed;
         }
         WAVE_SYNC();
         STAMP_ADD(3, ts);
@@ -2722,7 +2495,6 @@ struct Dec {
         const uint32_t nOrd = (uint32_t)__popcll(ordM);
         if (nOrd) {
             const uint32_t magicL = (off > 0 && off < 64) ? (65536u + off - 1) / off : 0u;
-#if LZ4MT_ORD_LANES
             uint64_t oLeft = ordM;
             for (uint32_t g = 0; g < nOrd; ++g) {
                 const int lg = (int)__builtin_ctzll(oLeft);
@@ -2730,16 +2502,6 @@ struct Dec {
                 const uint32_t jom = rdlane((uint32_t)om, lg) & (kRing - 1), joff = rdlane(off, lg);
                 const uint32_t jm = rdlane(mlen, lg), magic = rdlane(magicL, lg);
                 const uint32_t jmS = jm;
-#else
-            l_u4* const oprm = (l_u4*)(win + kNxOff);
-            const uint32_t orank = __builtin_amdgcn_mbcnt_hi((uint32_t)(ordM >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ordM, 0u));
-            if (ord) oprm[orank] = (v4u){(uint32_t)om & (kRing - 1), off, mlen, magicL};
-            WAVE_SYNC();
-            for (uint32_t g = 0; g < nOrd; ++g) {
-                const v4u q = oprm[g];
-                const uint32_t jom = q.x, joff = q.y, jm = q.z, magic = q.w;
-                const uint32_t jmS = (uint32_t)__builtin_amdgcn_readfirstlane((int)jm);
-#endif
                 for (uint32_t base = 0; base < jmS; base += 64) {
                     const uint32_t k = base + L;
                     const uint32_t kk = (joff >= 64 || k < joff) ? k : k - ((k * magic) >> 16) * joff;
@@ -2786,8 +2548,6 @@ __device__ int32_t decode_block(Dec<ST>& D, int64_t cap) {
     if (cap == 0) return (D.len == 1 && D.in8(0) == 0) ? 0 : -1;
     if (D.len == 0) return -1;
     *(l_u32*)(D.win + kNxOff + kNxPast) = kNxDead | (kNxDead << 16);   // next(PAST) = next(DEAD) = DEAD
-    D.pfN = 0;
-    if (LZ4MT_HOP2) *(l_u32*)(D.win + kD2Off + 512) = 0u;                  // D2(PAST) = D2(DEAD) = 0
 
 #define PHYS_CHECK(end_) \
     if ((end_) > D.physcap) return kDecodeOutputTooSmall;
@@ -2900,7 +2660,6 @@ safe_decode:
         op = cpy;
     }
 #undef PHYS_CHECK
-    D.flush_far();
     D.flush_tail(op);
     return (int32_t)op;
 
@@ -3458,19 +3217,9 @@ hipError_t launch_decode(const uint8_t* frame, const BlockRec* recs, uint32_t nB
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t xround(uint32_t acc, uint32_t w) { return rotl32(acc + w * kP2, 13) * kP1; }
 // a round on a word premultiplied by P2 (LLVM fuses the multiply with the
-// next round's add into one v_mad_u64_u32: the chain is alignbit + mad)
-// LZ4MT_XXH_NOFUSE (A/B): keep the multiply a v_mul_lo_u32 and the next add
-// a v_add_u32 instead of the fused 64-bit v_mad_u64_u32
-#ifndef LZ4MT_XXH_NOFUSE
-#define LZ4MT_XXH_NOFUSE 0
-#endif
-__device__ __forceinline__ uint32_t xround_pm(uint32_t acc, uint32_t wp) {
-    uint32_t m = rotl32(acc + wp, 13) * kP1;
-#if LZ4MT_XXH_NOFUSE
-    asm volatile("" : "+v"(m));
-#endif
-    return m;
-}
+// next round's add into one v_mad_u64_u32: the chain is alignbit + mad;
+// an unfused v_mul_lo_u32 + v_add_u32 was slower, profiles/r03n_xxh32_ab.txt)
+__device__ __forceinline__ uint32_t xround_pm(uint32_t acc, uint32_t wp) { return rotl32(acc + wp, 13) * kP1; }
 // LZ4MT_XXH_FULL: a whole 1 KiB chunk's LDS reads in flight before its 64
 // rounds (k_xxh32_stored 4.05 -> 3.78 ms at 8 GiB; profiles/r03n_xxh32_ab.txt)
 #ifndef LZ4MT_XXH_FULL
@@ -3584,18 +3333,10 @@ __device__ __forceinline__ uint32_t xq_rounds(uint32_t v, const uint32_t (&w)[kX
 
 // XXH32 (seed 0) of [p, p+len) for the quad's block; every lane of the quad
 // returns the digest.  All 64 lanes must call it (DPP reads neighbours).
-// LZ4MT_XQ_INLINE=1: xxh32_quad inlined into its three kernels (LLVM outlines
-// it: three call sites).  Off: the decode it runs beside is 0.3 ms slower with
-// it inlined (30.9 -> 31.2 ms at 8 GiB; profiles/r04m_xxh32_quad_inline_ab.txt)
-#ifndef LZ4MT_XQ_INLINE
-#define LZ4MT_XQ_INLINE 0
-#endif
-#if LZ4MT_XQ_INLINE
-#define XQ_INLINE __forceinline__
-#else
-#define XQ_INLINE __noinline__
-#endif
-__device__ XQ_INLINE uint32_t xxh32_quad(g_cu8* p, uint32_t len, g_cu8* safe /* any readable byte */) {
+// Kept a called function (three call sites): inlined, the decode it runs
+// beside is 0.3 ms slower (30.9 -> 31.2 ms at 8 GiB;
+// profiles/r04m_xxh32_quad_inline_ab.txt)
+__device__ __noinline__ uint32_t xxh32_quad(g_cu8* p, uint32_t len, g_cu8* safe /* any readable byte */) {
     const uint32_t c = laneid() & 3u;
     const uint32_t ns = len >> 4;
     const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
@@ -3851,10 +3592,6 @@ __global__ void __launch_bounds__(1024) k_frame_scan(const int32_t* __restrict__
     if (t == 1023) recOff[nBlocks] = part[1023];
 }
 
-// LZ4MT_ASM_NT=1: non-temporal stores for the frame bytes (A/B)
-#ifndef LZ4MT_ASM_NT
-#define LZ4MT_ASM_NT 0
-#endif
 // chunks per thread in flight in the assembly's middle loop (A/B)
 #ifndef LZ4MT_ASM_UNROLL
 #define LZ4MT_ASM_UNROLL 1
@@ -3902,11 +3639,7 @@ __global__ void __launch_bounds__(256) k_frame_assemble(const uint8_t* __restric
         v.y = __builtin_amdgcn_alignbyte(a2, a1, s3);
         v.z = __builtin_amdgcn_alignbyte(a3, a2, s3);
         v.w = __builtin_amdgcn_alignbyte(a4, a3, s3);
-#if LZ4MT_ASM_NT
-        __builtin_nontemporal_store(v, (g_u4*)(D + (A0 - Da) + 16 * j));
-#else
         *(g_u4*)(D + (A0 - Da) + 16 * j) = v;
-#endif
     }
 }
 

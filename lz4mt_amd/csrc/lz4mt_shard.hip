@@ -31,6 +31,8 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 
 #include "../../include/lz4mt_hip.h"
 #include "lz4mt_device.h"
@@ -188,7 +190,12 @@ __global__ void __launch_bounds__(64) k_shard_plan(uint32_t* pub, uint32_t* __re
             const uint32_t pv = __hip_atomic_load(pub + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             hi = (pv & 0x40000000u) ? 0u : (pv & 0x3FFFFFFFu);
         }
-        lo = s & ~kRawBit;
+        // never past the block's slot (its stored bytes are at most n), never
+        // from past what is available: a workspace whose round state was not
+        // reset then packs nothing wrong-sized instead of
+        // reading outside the slots
+        hi = min(hi, n);
+        lo = min(s & ~kRawBit, hi);
         const uint32_t avail = hi > lo ? hi - lo : 0u;
         const uint32_t len = min(avail, cap);
         desc[b] = Desc{lo | (raw ? kRawBit : 0u), len, 0};
@@ -233,9 +240,17 @@ __global__ void __launch_bounds__(256) k_shard_pack(const uint8_t* __restrict__ 
 // Root: a received pack into the mirror of that shard's slots (source bytes
 // of an incompressible block land in its slot too: the assembly reads raw
 // blocks from the mirror).
+// The pack may have been written into this device's memory by ANOTHER
+// device's copy engine (IpcPushTransport): no XCD L2 here saw those writes,
+// and this workgroup's L2 may still hold lines of the same buffer from the
+// round that used it two rounds ago.  The receive buffers are allocated
+// uncached where the runtime allows (lz4mtHipIpcAllocKind), and every
+// workgroup starts with a system-scope acquire (buffer_inv sc0 sc1: L1 and
+// the non-coherent L2 lines invalidated) before its first read of the pack.
 __global__ void __launch_bounds__(256) k_shard_unpack(const uint8_t* __restrict__ pack, uint32_t bm, uint32_t nb,
                                                       uint8_t* __restrict__ mirror, int32_t* __restrict__ csize,
                                                       uint32_t* __restrict__ bsum) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     const uint32_t b = blockIdx.x;
     const PackHdr* h = reinterpret_cast<const PackHdr*>(pack);
     if ((h->flags & kFlagFinal) && threadIdx.x == 0) {
@@ -281,6 +296,27 @@ bool use_pub(uint32_t bm) {   // k_encode_pub's v5 path: 1 and 4 MiB blocks (64 
     return bm >= (1u << 20) && bm <= (4u << 20);
 }
 
+// The call order a shard workspace must follow: Reset, then
+// Encode, then Packs -- kept per workspace address on the host, so that an
+// Encode into a workspace whose round state was not reset since its last
+// encode, or a Pack from one never encoded since its reset, returns BAD_ARG
+// instead of packing from stale (or, on a fresh buffer, arbitrary) counts.
+enum class WsState { kReset, kEncoded };
+std::mutex g_ws_mu;
+std::unordered_map<const void*, WsState> g_ws_state;
+bool ws_advance(const void* ws, WsState need, WsState next) {
+    std::lock_guard<std::mutex> g(g_ws_mu);
+    auto it = g_ws_state.find(ws);
+    if (it == g_ws_state.end() || it->second != need) return false;
+    it->second = next;
+    return true;
+}
+bool ws_is(const void* ws, WsState st) {
+    std::lock_guard<std::mutex> g(g_ws_mu);
+    auto it = g_ws_state.find(ws);
+    return it != g_ws_state.end() && it->second == st;
+}
+
 }  // namespace
 
 extern "C" uint64_t lz4mtHipShardWorkspaceSize(uint64_t n, const Lz4MtStreamDescriptor* sd) {
@@ -320,6 +356,8 @@ extern "C" Lz4MtResult lz4mtHipShardReset(uint64_t n, const Lz4MtStreamDescripto
     SHCHK(hipMemsetAsync(w.pub, 0, nb * 4 + 4, st));
     SHCHK(hipMemsetAsync(w.sent, 0, nb * 4 + 4, st));
     SHCHK(hipMemsetAsync(w.xdone, 0, nb * 4 + 4, st));
+    std::lock_guard<std::mutex> g(g_ws_mu);
+    g_ws_state[d_ws] = WsState::kReset;
     return LZ4MT_RESULT_OK;
 }
 
@@ -336,6 +374,7 @@ extern "C" Lz4MtResult lz4mtHipShardEncode(const void* d_src, uint64_t n, const 
     const hipStream_t st = static_cast<hipStream_t>(stream);
     const ShardWs w = carve(static_cast<uint8_t*>(d_ws), nb, bm);
     const uint8_t* src = static_cast<const uint8_t*>(d_src);
+    if (!ws_advance(d_ws, WsState::kReset, WsState::kEncoded)) return LZ4MT_RESULT_BAD_ARG;   // not reset
     if (nb == 0) return LZ4MT_RESULT_OK;
     // block checksums hashed beside the encode (k_xxh32_follow on a side
     // stream; `stream` waits for it, so the shard is complete on `stream`)
@@ -368,6 +407,7 @@ extern "C" Lz4MtResult lz4mtHipShardPack(const void* d_src, uint64_t n, const Lz
     if ((!d_src && n) || !d_ws || !d_pack || wsSize < carve(nullptr, nb, bm).bytes || perBlockCap == 0 ||
         packCap < lz4mtHipShardPackBound(n, sd, perBlockCap))
         return LZ4MT_RESULT_BAD_ARG;
+    if (!ws_is(d_ws, WsState::kEncoded)) return LZ4MT_RESULT_BAD_ARG;   // no encode since the last reset
     const hipStream_t st = static_cast<hipStream_t>(stream);
     const ShardWs w = carve(static_cast<uint8_t*>(d_ws), nb, bm);
     uint8_t* pack = static_cast<uint8_t*>(d_pack);
@@ -442,15 +482,56 @@ extern "C" uint64_t lz4mtHipShardBodyBytes(uint64_t n, const Lz4MtStreamDescript
 }
 
 // ---- the root's receive buffers, shared with the senders (copy-engine push)
-extern "C" int lz4mtHipIpcAlloc(uint64_t bytes, void** d_ptr, void* handle64) {
+// Kinds, best first: 2 uncached device memory (hipDeviceMallocUncached: no
+// XCD L2 ever holds a line of it, so a peer's copy-engine writes are what
+// every later read sees), 1 fine-grained (its L2 lines are invalidated by
+// the unpack's system-scope acquire), 0 plain hipMalloc (coarse-grained: the
+// acquire still invalidates the reading CU's L1; the setup's pattern check
+// is then the proof).  The first kind that allocates AND exports an IPC
+// handle is taken; `want` caps the kind (2 = best available).
+extern "C" int lz4mtHipIpcAllocKind(uint64_t bytes, void** d_ptr, void* handle64, int want, int* kind) {
     if (!d_ptr || !handle64) return -1;
-    if (hipMalloc(d_ptr, bytes ? bytes : 1) != hipSuccess) { *d_ptr = nullptr; return -1; }
-    hipIpcMemHandle_t h;
-    if (hipIpcGetMemHandle(&h, *d_ptr) != hipSuccess) { hipFree(*d_ptr); *d_ptr = nullptr; return -1; }
-    static_assert(sizeof(h) <= 64, "ipc handle");
-    memset(handle64, 0, 64);
-    memcpy(handle64, &h, sizeof(h));
-    return 0;
+    static_assert(sizeof(hipIpcMemHandle_t) <= 64, "ipc handle");
+    const unsigned flags[3] = {0u, hipDeviceMallocFinegrained, hipDeviceMallocUncached};
+    for (int k = std::min(want, 2); k >= 0; --k) {
+        void* p = nullptr;
+        const hipError_t e = k == 0 ? hipMalloc(&p, bytes ? bytes : 1)
+                                    : hipExtMallocWithFlags(&p, bytes ? bytes : 1, flags[k]);
+        if (e != hipSuccess || !p) { (void)hipGetLastError(); continue; }
+        hipIpcMemHandle_t h;
+        if (hipIpcGetMemHandle(&h, p) != hipSuccess) { (void)hipGetLastError(); (void)hipFree(p); continue; }
+        memset(handle64, 0, 64);
+        memcpy(handle64, &h, sizeof(h));
+        *d_ptr = p;
+        if (kind) *kind = k;
+        return 0;
+    }
+    *d_ptr = nullptr;
+    return -1;
+}
+
+extern "C" int lz4mtHipIpcAlloc(uint64_t bytes, void** d_ptr, void* handle64) {
+    return lz4mtHipIpcAllocKind(bytes, d_ptr, handle64, 2, nullptr);
+}
+
+// PCI bus id ("dddd:bb:dd.f") of device `dev`, and the ordinal of the visible
+// device with a given bus id (-1: not visible here): the IPC setup names the
+// root's GPU by bus id, which every process resolves to its own ordinal.
+extern "C" int lz4mtHipDevicePciBusId(int dev, char* buf, int len) {
+    if (!buf || len < 13) return -1;
+    return hipDeviceGetPCIBusId(buf, len, dev) == hipSuccess ? 0 : -1;
+}
+
+extern "C" int lz4mtHipDeviceByPciBusId(const char* busId) {
+    int dev = -1;
+    if (!busId || hipDeviceGetByPCIBusId(&dev, busId) != hipSuccess) { (void)hipGetLastError(); return -1; }
+    return dev;
+}
+
+extern "C" int lz4mtHipCanAccessPeer(int dev, int peer) {
+    int ok = 0;
+    if (dev == peer) return 1;
+    return hipDeviceCanAccessPeer(&ok, dev, peer) == hipSuccess ? (ok ? 1 : 0) : -1;
 }
 
 extern "C" int lz4mtHipIpcOpen(const void* handle64, void** d_ptr) {

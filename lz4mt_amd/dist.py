@@ -547,9 +547,24 @@ def peer_access_matrix():
     return [[i == j or bool(torch.cuda.can_device_access_peer(i, j)) for j in range(n)] for i in range(n)]
 
 
+def dist_timeout():
+    """Timeout of every process group this path makes (init_process_group in
+    bench.py, the gloo control group): a rank that stops answering ends the
+    run with an error instead of stalling it for torch's default 30 min.
+    LZ4MT_DIST_TIMEOUT_S overrides the 300 s default."""
+    import datetime
+    import os
+    return datetime.timedelta(seconds=float(os.environ.get("LZ4MT_DIST_TIMEOUT_S", "300")))
+
+
+def _bus_id(L, dev_index):
+    buf = ctypes.create_string_buffer(64)
+    return buf.value.decode() if L.lib.lz4mtHipDevicePciBusId(int(dev_index), buf, 64) == 0 else None
+
+
 class IpcPushTransport:
     """Each sender's pack goes straight into a receive buffer in the root's
-    HBM, exported once by IPC handle (lz4mtHipIpcAlloc / lz4mtHipIpcOpen),
+    HBM, exported once by IPC handle (lz4mtHipIpcAllocKind / lz4mtHipIpcOpen),
     with an asynchronous device-to-device copy (lz4mtHipCopyAsync: a copy
     engine over xGMI, no kernel and no LDS) before the round's exchange; two
     buffers per sender alternate, and the root finishes unpacking round k
@@ -557,23 +572,38 @@ class IpcPushTransport:
     pack the root still reads.  Only the round's sizes go over the (gloo)
     control group.
 
+    Visibility on the root: a peer's copy-engine writes land in the root's
+    HBM behind the back of its XCD L2s.  The receive buffers are uncached
+    device memory where the runtime exports such memory by IPC (no L2 line
+    of them is ever held; ``kind`` says which memory was taken), and the
+    root's k_shard_unpack starts every workgroup with a system-scope acquire
+    (buffer_inv sc0 sc1).  The setup then PROVES the path end to end: every
+    sender pushes a seeded pattern into both of its buffers and the root
+    compares the XXH32 of every 1 MiB piece with the sender's; any mismatch
+    (or a failed map / peer-access check) raises IpcSetupError on every rank
+    together, and the caller falls back to RcclTransport.  The root's GPU is
+    named by PCI bus id, which each sender resolves to its own ordinal, so
+    ranks that number devices differently still agree.
+
     The buffers are kept for the next call with the same layout (shard
     sizes, descriptor, per-block cap, root); a call with another layout
     tears them down and sets up again, on every rank alike (every rank sees
-    the same all-gathered layout).  A sender whose device cannot reach the
-    root's (hipDeviceCanAccessPeer) fails the setup on every rank."""
+    the same all-gathered layout)."""
+
+    CHUNK = 1 << 20   # pattern check granule
 
     def __init__(self, device):
         self.device = device
         self.bufs, self.remote, self.copy_stream = {}, [], None
-        self.key, self.cap_bytes = None, 0
+        self.key, self.cap_bytes, self.kind = None, 0, None
 
     @staticmethod
     def _layout_key(sizes, sd, cap, dst):
         return (tuple(sizes), bytes(sd), int(cap), int(dst))
 
     def setup(self, E, sizes, sd, cap, rank, dst, ctrl):
-        """Collective over ``ctrl``: every rank either sets up or raises IpcSetupError."""
+        """Collective over ``ctrl``: every rank either sets up (and passes the
+        pattern check) or raises IpcSetupError."""
         import lz4mt_amd as L
         key = self._layout_key(sizes, sd, cap, dst)
         if (self.bufs or self.remote) and key == self.key:   # an earlier call with this same layout
@@ -581,9 +611,8 @@ class IpcPushTransport:
         if self.bufs or self.remote:   # another layout: every rank sees the same sizes, so all re-set up
             self.close()
         self.L, self.rank, self.dst = L, rank, dst
-        handles, err = {}, None
-        # the root's device index, for the senders' peer-access check
-        root_dev = [self.device.index if rank == dst else -1]
+        me = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        handles, kinds, err = {}, [], None
         if rank == dst:
             try:
                 for r in range(len(sizes)):
@@ -592,23 +621,29 @@ class IpcPushTransport:
                     nbytes = L.shard_pack_bound(sizes[r], sd, cap)
                     pair = []
                     for _ in range(2):
-                        ptr, h = ctypes.c_void_p(), (ctypes.c_uint8 * 64)()
-                        if L.lib.lz4mtHipIpcAlloc(nbytes, ctypes.byref(ptr), h) != 0:
-                            raise IpcSetupError("lz4mtHipIpcAlloc failed")
+                        ptr, h, k = ctypes.c_void_p(), (ctypes.c_uint8 * 64)(), ctypes.c_int(-1)
+                        if L.lib.lz4mtHipIpcAllocKind(nbytes, ctypes.byref(ptr), h, 2, ctypes.byref(k)) != 0:
+                            raise IpcSetupError("lz4mtHipIpcAllocKind failed")
                         pair.append(ptr.value)
+                        kinds.append(k.value)
                         handles.setdefault(r, []).append(bytes(h))
                     self.bufs[r] = pair
             except IpcSetupError as e:
                 err, handles = e, None
-        obj = [handles, root_dev[0]]
+        obj = [handles, _bus_id(L, me) if rank == dst else None, min(kinds) if kinds else None]
         dist.broadcast_object_list(obj, src=dst if ctrl is None else dist.get_global_rank(ctrl, dst), group=ctrl)
         ok = obj[0] is not None
+        names = {2: "uncached", 1: "fine-grained", 0: "coarse-grained"}
+        self.kind = names.get(obj[2], "none")
         if ok and rank != dst:
             try:
-                rd = int(obj[1])
-                me = self.device.index if self.device.index is not None else torch.cuda.current_device()
-                if rd != me and not torch.cuda.can_device_access_peer(me, rd):
-                    raise IpcSetupError(f"device {me} cannot access the root's device {rd} (hipDeviceCanAccessPeer)")
+                rd = L.lib.lz4mtHipDeviceByPciBusId(obj[1].encode()) if obj[1] else -1
+                # rd < 0: the root's GPU is not visible to this process (its
+                # own device list is restricted); the map and the pattern
+                # check below still decide
+                if rd >= 0 and rd != me and L.lib.lz4mtHipCanAccessPeer(me, rd) != 1:
+                    raise IpcSetupError(f"device {me} cannot access the root's device {rd} = {obj[1]} "
+                                        "(hipDeviceCanAccessPeer)")
                 self.cap_bytes = L.shard_pack_bound(sizes[rank], sd, cap)
                 for h in obj[0][rank]:
                     ptr = ctypes.c_void_p()
@@ -619,12 +654,69 @@ class IpcPushTransport:
                 self.copy_stream = torch.cuda.Stream(self.device)
             except IpcSetupError as e:
                 err, ok = e, False
+        if self._all_ok(ok, ctrl):
+            ok, err = self._pattern_check(sizes, sd, cap, ctrl)
+            if self._all_ok(ok, ctrl):
+                self.key = key
+                return
+        self.close()
+        raise err or IpcSetupError("IpcPushTransport: another rank failed the setup or the pattern check")
+
+    @staticmethod
+    def _all_ok(ok, ctrl):
         flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=ctrl)
-        if int(flag.item()) == 0:
-            self.close()
-            raise err or IpcSetupError("IpcPushTransport: another rank could not set up its buffers")
-        self.key = key
+        return int(flag.item()) == 1
+
+    def _pattern_check(self, sizes, sd, cap, ctrl):
+        """Every sender fills both of its root buffers with a seeded pattern
+        (through the same copies the rounds use); the root hashes what
+        arrived, 1 MiB at a time, and compares.  Returns (ok, error) on every
+        rank.  LZ4MT_AMD_IPC_CORRUPT=1 (tests) flips one pattern byte after
+        the sender's digests are taken, so the check must fail."""
+        import os
+        L = self.L
+        digs = None
+        if self.rank != self.dst:
+            n = self.cap_bytes
+            g = torch.Generator(device=self.device)
+            g.manual_seed(0x5EED + 7919 * self.rank)
+            digs = []
+            st = self.copy_stream
+            for k in range(2):
+                pat = torch.randint(0, 256, (n,), dtype=torch.uint8, device=self.device, generator=g)
+                digs.append(L.xxh32_chunks(pat, self.CHUNK).cpu().tolist())
+                if os.environ.get("LZ4MT_AMD_IPC_CORRUPT") == "1":
+                    pat[n // 2] ^= 0x5A
+                st.wait_stream(torch.cuda.current_stream(self.device))
+                if L.lib.lz4mtHipCopyAsync(ctypes.c_void_p(self.remote[k]), ctypes.c_void_p(pat.data_ptr()), n,
+                                           ctypes.c_void_p(st.cuda_stream)) != 0:
+                    return False, IpcSetupError("lz4mtHipCopyAsync failed during the pattern check")
+                st.synchronize()
+                del pat
+        world = dist.get_world_size(ctrl)
+        alld = [None] * world
+        dist.all_gather_object(alld, digs, group=ctrl)
+        if self.rank != self.dst:
+            return True, None
+        bad = []
+        cur = torch.cuda.current_stream(self.device)
+        for r, pair in self.bufs.items():
+            n = L.shard_pack_bound(sizes[r], sd, cap)
+            nc = (n + self.CHUNK - 1) // self.CHUNK
+            for k, ptr in enumerate(pair):
+                out = torch.empty(nc, dtype=torch.int32, device=self.device)
+                if L.lib.lz4mtHipXxh32Chunks(ctypes.c_void_p(ptr), n, self.CHUNK, ctypes.c_void_p(out.data_ptr()),
+                                             ctypes.c_void_p(cur.cuda_stream)) != 0:
+                    return False, IpcSetupError("lz4mtHipXxh32Chunks failed during the pattern check")
+                got = [v & 0xFFFFFFFF for v in out.cpu().tolist()]
+                want = [v & 0xFFFFFFFF for v in (alld[r][k] if alld[r] else [])]
+                if got != want:
+                    bad.append((r, k))
+        if bad:
+            return False, IpcSetupError(f"IPC pattern check failed: (sender, buffer) {bad} did not arrive intact "
+                                        f"in the root's {self.kind} receive buffers")
+        return True, None
 
     def push(self, k, buf, nbytes):
         if self.rank == self.dst or not nbytes:
@@ -663,13 +755,34 @@ def control_group(group=None):
     is gloo.  Made once per group (collective on first use)."""
     if dist.get_backend(group) == "gloo":
         return group
-    # keyed by the group AND the default group, so a new process group in
-    # the same process (after destroy_process_group) gets a new control group
-    key = (id(group) if group is not None else None, id(dist.group.WORLD))
-    if key not in _CTRL_GROUPS:
+    # keyed by the group AND the default group, compared by identity (an id()
+    # of a destroyed group can be reused by a new one, ADVICE r04), so a new
+    # process group in the same process gets a new control group
+    world = dist.group.WORLD
+    key = id(group) if group is not None else None
+    hit = _CTRL_GROUPS.get(key)
+    if hit is None or hit[0] is not group or hit[1] is not world:
         ranks = dist.get_process_group_ranks(group) if group is not None else None
-        _CTRL_GROUPS[key] = dist.new_group(ranks=ranks, backend="gloo")
-    return _CTRL_GROUPS[key]
+        _CTRL_GROUPS[key] = (group, world, dist.new_group(ranks=ranks, backend="gloo", timeout=dist_timeout()))
+    return _CTRL_GROUPS[key][2]
+
+
+def _shard_sizes(n, world, ctrl):
+    alln = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(alln, torch.tensor([n], dtype=torch.int64), group=ctrl)
+    return [int(x.item()) for x in alln]
+
+
+def prepare_transport(transport, engine, n, sd, dst=0, group=None, ctrl=None, per_block_cap=128 << 10):
+    """Sets ``transport`` up for compress_gather_streamed calls over shards of
+    this layout (this rank's shard: n bytes), collectively, ahead of any
+    timed call: the IPC buffers, their export, the senders' maps and the
+    pattern check happen here instead of inside the first call.  Raises
+    IpcSetupError on every rank together when the IPC path is not usable."""
+    ctrl = ctrl if ctrl is not None else control_group(group)
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    transport.setup(engine, _shard_sizes(n, world, ctrl), sd, per_block_cap, rank, dst, ctrl)
 
 
 def compress_gather_streamed(src, sd, dst=0, group=None, engine=None, per_block_cap=128 << 10, ws=None, stats=None,
@@ -704,9 +817,7 @@ def compress_gather_streamed(src, sd, dst=0, group=None, engine=None, per_block_
     T = transport or RcclTransport(group)
     dev = src.device
     n = src.numel()
-    alln = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(alln, torch.tensor([n], dtype=torch.int64), group=ctrl)
-    sizes = [int(x.item()) for x in alln]
+    sizes = _shard_sizes(n, world, ctrl)
     # the stitched frame is the whole stream's only if every shard but the
     # last non-empty one is a whole number of blocks (every rank sees the
     # same sizes, so every rank raises here together)

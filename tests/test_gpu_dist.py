@@ -242,3 +242,129 @@ def test_bench_nccl_world1_distributed_path():
     assert line["gather"].startswith("streamed")
     assert line["root_memory"]["max_allocated_GiB"] > 0.25 and line["peer_access"][0][0] is True
     assert line["scatter_split_ms"]["host_staged"] is False
+
+
+def _ipc_setup_rank(rank, world, port, corrupt, q):
+    """One rank of an IpcPushTransport set-up on the shared test GPU (gloo):
+    the root exports its receive buffers, the sender maps them (the root's GPU
+    named by PCI bus id) and pushes the seeded pattern; the root checks it."""
+    import torch.distributed as dist
+
+    from lz4mt_amd import dist as D
+    import lz4mt_amd as L
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if corrupt:
+        os.environ["LZ4MT_AMD_IPC_CORRUPT"] = "1"
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=D.dist_timeout())
+    try:
+        sd = L.make_sd(7, stream_checksum=False, block_checksum=True)
+        n = 96 << 20
+        tr = D.IpcPushTransport(torch.device("cuda", 0))
+        eng = D.HipShardEngine(torch.device("cuda", 0))
+        try:
+            D.prepare_transport(tr, eng, n, sd)
+            res = ("ok", tr.kind)
+            # the set-up is kept for the same layout: a streamed gather over it
+            src = L.gen_synthetic(n, seed=77 + rank)
+            full = D.compress_gather_streamed(src, sd, transport=tr, engine=eng)
+            if rank == 0:   # whole 4 MiB blocks per shard: the frame of the concatenated shards
+                want = L.compress_frame(torch.cat([L.gen_synthetic(n, seed=77), L.gen_synthetic(n, seed=78)]), sd)
+                res = res + (full.numel() == want.numel() and bool(torch.equal(full, want)),)
+            tr.close()
+        except D.IpcSetupError as e:
+            res = ("setup_error", str(e))
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_two(target, *args, timeout=240):
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(r, 2, port, *args, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=timeout) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return got
+
+
+@pytest.mark.gpu
+def test_ipc_setup_pattern_check_passes():
+    """the IPC set-up proves the push end to end (seeded
+    pattern, XXH32 per 1 MiB compared on the root) and reports the receive
+    buffers' memory kind; a streamed gather then runs over it."""
+    got = _run_two(_ipc_setup_rank, False)
+    assert got[0][0] == "ok" and got[1][0] == "ok", got
+    assert got[0][1] in ("uncached", "fine-grained", "coarse-grained")
+    assert got[0][2] is True
+
+
+@pytest.mark.gpu
+def test_ipc_setup_corrupt_pattern_fails_on_every_rank():
+    """A pattern that does not arrive intact (LZ4MT_AMD_IPC_CORRUPT=1 flips a
+    byte after the sender's digests) raises IpcSetupError on BOTH ranks."""
+    got = _run_two(_ipc_setup_rank, True)
+    assert got[0][0] == "setup_error" and got[1][0] == "setup_error", got
+    assert "pattern check failed" in got[0][1]
+
+
+@pytest.mark.gpu
+def test_bench_corrupt_ipc_falls_back_to_rccl():
+    """bench.py at N = 2 with a forced-corrupt pattern: every rank takes the
+    RCCL (here: gloo point-to-point) transport together, the line says so,
+    and the stitched frame is still right."""
+    env_extra = {"LZ4MT_AMD_IPC_CORRUPT": "1"}
+    old = {k: os.environ.get(k) for k in env_extra}
+    os.environ.update(env_extra)
+    try:
+        line = _bench("--gpus", "2", "--gib", "0.25", "--steps", "1", "--warmup", "0", "--no-cpu-baseline")
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert line["transport"].startswith("rccl (IPC setup failed") and "pattern check failed" in line["transport"]
+    assert line["stitched_frame_ok"] is True and line["roundtrip_ok"] is True
+
+
+@pytest.mark.gpu
+def test_shard_call_order_is_enforced():
+    """an encode into a workspace not reset since its last encode,
+    or a pack from a workspace never encoded since its reset, is BAD_ARG."""
+    import ctypes
+
+    import lz4mt_amd as L
+    n = 8 << 20
+    sd = L.make_sd(7, stream_checksum=False, block_checksum=True)
+    src = L.gen_synthetic(n, seed=5)
+    ws = torch.zeros(L.lib.lz4mtHipShardWorkspaceSize(n, ctypes.byref(sd)), dtype=torch.uint8, device="cuda")
+    pk = torch.empty(L.shard_pack_bound(n, sd, 64 << 10), dtype=torch.uint8, device="cuda")
+
+    def enc():
+        return L.lib.lz4mtHipShardEncode(ctypes.c_void_p(src.data_ptr()), n, ctypes.byref(sd),
+                                         ctypes.c_void_p(ws.data_ptr()), ws.numel(), None)
+
+    def pack():
+        return L.lib.lz4mtHipShardPack(ctypes.c_void_p(src.data_ptr()), n, ctypes.byref(sd),
+                                       ctypes.c_void_p(ws.data_ptr()), ws.numel(), ctypes.c_void_p(pk.data_ptr()),
+                                       pk.numel(), 64 << 10, 0, None)
+    BAD = int(L.Result.BAD_ARG)
+    assert enc() == BAD                      # fresh workspace, never reset
+    assert pack() == BAD
+    assert L.lib.lz4mtHipShardReset(n, ctypes.byref(sd), ctypes.c_void_p(ws.data_ptr()), ws.numel(), None) == 0
+    assert pack() == BAD                     # reset but not encoded
+    assert enc() == 0
+    assert pack() == 0
+    assert enc() == BAD                      # a second encode without a reset
+    torch.cuda.synchronize()

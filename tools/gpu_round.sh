@@ -11,6 +11,7 @@
 #   pmcbid  the same on App. F at block ids 4, 5, 6 (the configs[4] sweep: profiles/pmc_b<id>.json)
 #   dist2   bench.py --gpus 2 over gloo on this one GPU (rehearsal of the N > 1 path)
 #   fcal    FETCH_SIZE calibration on a known byte count (tools/fetch_cal.py + fetchcal_sum.py)
+#   unpack  the root's unpack from each IPC receive-buffer memory kind (tools/unpack_ab.py)
 #   tail    the streamed gather's exposed tail on one GPU (tools/tail_model.py)
 #   ab      kernel times of every exp_libs/*.so (tools/mkvariants.sh), two passes
 #   abtrace kernel-trace stats of every exp_libs/*.so;  abbid  ab at every block size
@@ -96,6 +97,10 @@ for step in "$@"; do
       timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -T -f csv -d "$out/fcal" -o fcal -- \
           python3 tools/fetch_cal.py 8 > "$out/fcal.log" 2>&1
       python3 tools/fetchcal_sum.py "$out/fcal" 8 | tee "$out/fcal_summary.json" ;;
+    unpack)   # the root's unpack cost per receive-buffer memory kind (tools/unpack_ab.py)
+      timeout -k 10 200 python3 tools/unpack_ab.py 8 > "$out/unpack_ab.json" 2> "$out/unpack_ab.err" \
+          || { tail -20 "$out/unpack_ab.err"; exit 1; }
+      cat "$out/unpack_ab.json" ;;
     tail)
       timeout -k 10 300 python3 tools/tail_model.py 8 8 > "$out/tail_model.txt" 2>&1
       cat "$out/tail_model.txt" ;;
