@@ -121,6 +121,12 @@ for step in "$@"; do
         done
       done
       cat "$out/follow.txt" ;;
+    abpar)   # quick parity screen (tools/abparity.py) of every exp_libs/*.so; mismatches are reported, not fatal
+      for f in exp_libs/*.so; do
+        LZ4MT_AMD_LIB_OLDER=1 LZ4MT_AMD_LIB=$f timeout -k 10 200 python3 -u tools/abparity.py 2>&1 | grep -v amdgpu \
+            >> "$out/abpar.txt" || true
+      done
+      cat "$out/abpar.txt" ;;
     abtest)   # parity tests against exp_libs/$ABLIB.so (the candidate of an A/B)
       LZ4MT_AMD_LIB=exp_libs/$ABLIB.so timeout -k 10 900 python3 -u -m pytest -m gpu -x -q --timeout 300 \
           --timeout-method thread tests/test_gpu.py tests/test_gpu_configs.py tests/test_gpu_bd.py \
