@@ -26,7 +26,6 @@
 #include <algorithm>
 #include <atomic>
 #include <mutex>
-#include <type_traits>
 
 // LZ4MT_PART splits this file into two objects so each half gets its own
 // scheduler flags (Makefile): 1 = everything but the decoder kernels,
@@ -618,18 +617,6 @@ typedef __attribute__((address_space(3))) uint16_t __attribute__((aligned(1))) l
 typedef __attribute__((address_space(3))) uint64_t l_u64;
 
 constexpr uint32_t kSR = 2048;        // source ring bytes
-#ifndef LZ4MT_EXP_TW
-#define LZ4MT_EXP_TW 0
-#endif
-#ifndef LZ4MT_EXP_PEEL
-#define LZ4MT_EXP_PEEL 0
-#endif
-#ifndef LZ4MT_EXP_VLAY
-#define LZ4MT_EXP_VLAY 0
-#endif
-#ifndef LZ4MT_EXP_HASH24
-#define LZ4MT_EXP_HASH24 0
-#endif
 // forward-count words the v5 round trip loads per side (the first 4 * this
 // many bytes after the minimum match; longer matches take 256-byte rounds)
 #ifndef LZ4MT_COUNT_LANES
@@ -839,17 +826,12 @@ __device__ __forceinline__ uint32_t pend_byte(const SeqLayout& e, uint32_t x, ui
 __device__ __forceinline__ void store_pend(const PendSeq& p, const SrcRing& V, g_cu8* __restrict__ s,
                                            g_u8* __restrict__ d) {
     const uint32_t L = laneid();
-#if LZ4MT_EXP_VLAY
     // the layout in VALU (uniform values in VGPRs): the scalar unit is the
     // CU's busiest port in the encoder window, the vector ALU is not
     PendSeq q = p;
     asm volatile("" : "+v"(q.lit), "+v"(q.mcf), "+v"(q.off));
     const SeqLayout e(q);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane((int)e.total);
-#else
-    const SeqLayout e(p);
-    const uint32_t total = e.total;
-#endif
     if (p.anchor >= V.B && p.anchor + p.lit <= V.B + kSR) {
         for (uint32_t base = 0; base < total; base += 64) {
             const uint32_t x = min(base + L, e.total - 1);   // lanes past the end repeat the last byte
@@ -987,7 +969,6 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     // carried as loop state (61 after every match) rather than recomputed
     uint32_t spanHi = 61;
     uint32_t nextSweep = 32768;   // P17
-    [[maybe_unused]] bool firstW = false;   // (LZ4MT_EXP_PEEL) the next window is the first after a match
     // ONE exit and no continue: the structurizer then needs no flow
     // variables and the loop-carried state stays in place across windows
     while (!done) {
@@ -995,13 +976,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
       // match-path state (anchor, op, pe) is not touched by them
       uint32_t w, ip, cd, maxb, cw, iw, bi, bc;
       bool wTerm;
-      // One window.  FIRST: the first window after a match (mode 1, k0 = 0,
-      // s0 = 1, j1 = 65, spanHi = 61 as constants: LZ4MT_EXP_PEEL), so the
-      // match path resets none of that state and this window's head folds it.
-      auto window = [&](auto firstT) __attribute__((always_inline)) {
-        constexpr bool FIRST = decltype(firstT)::value;
-        const uint32_t wk0 = FIRST ? 0u : k0, ws0 = FIRST ? 1u : s0, wj1 = FIRST ? 65u : j1;
-        const uint32_t wmode = FIRST ? 1u : mode, wspan = FIRST ? 61u : spanHi;
+      do {
         if (ST) acc[10] += 1;
         if (P17) {
             while (sBase >= nextSweep) {   // (long matches cross several)
@@ -1009,24 +984,24 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                 nextSweep += 32768;
             }
         }
-        // ---- probe positions.  SEARCH lane L probes k = wk0 + j (j = L - 2) at
-        // sBase + j*ws0 + max(0, j - wj1): the step ws0 = step(wk0) rises by one at
-        // most once inside a window (at j = wj1; never in the wk0 = 0 window)
+        // ---- probe positions.  SEARCH lane L probes k = k0 + j (j = L - 2) at
+        // sBase + j*s0 + max(0, j - j1): the step s0 = step(k0) rises by one at
+        // most once inside a window (at j = j1; never in the k0 = 0 window)
         const uint32_t j = L - 2;
-        const int32_t jx = (int32_t)j - (int32_t)wj1;
-        // j < 62 and the step ws0 < 2^24: a full-rate 24-bit multiply (lanes 0
+        const int32_t jx = (int32_t)j - (int32_t)j1;
+        // j < 62 and the step s0 < 2^24: a full-rate 24-bit multiply (lanes 0
         // and 1 wrap j, but take the INSERT / TEST position below)
-        uint32_t p = sBase + __umul24(j, ws0) + (uint32_t)max(jx, 0);
-        const uint32_t step = ws0 + (jx >= 0 ? 1u : 0u);
-        const uint32_t sHi = sBase + wspan;
-        const bool insOn = wmode != 0;
-        const uint32_t insPos = wmode == 2 ? o0 : sBase - 3, testPos = sBase - 1;
+        uint32_t p = sBase + __umul24(j, s0) + (uint32_t)max(jx, 0);
+        const uint32_t step = s0 + (jx >= 0 ? 1u : 0u);
+        const uint32_t sHi = sBase + spanHi;
+        const bool insOn = mode != 0;
+        const uint32_t insPos = mode == 2 ? o0 : sBase - 3, testPos = sBase - 1;
         p = L == 0 ? insPos : (L == 1 ? testPos : p);
         // lane predicates as wave masks (SALU), turned back into per-lane
         // conditions with inverse_ballot (the mask is the select's condition):
         // no 0/1 materialisation chains.  Lane 0 / 1's bits come straight
-        // from the wmode (2: INSERT only, 1: both, 0: neither)
-        const uint64_t roleM = (uint64_t)((0x130u >> (4 * wmode)) & 3u);
+        // from the mode (2: INSERT only, 1: both, 0: neither)
+        const uint64_t roleM = (uint64_t)((0x130u >> (4 * mode)) & 3u);
         const uint64_t liveM = (bal(p <= mflimitP1) & ~3ull) | roleM;
         const uint64_t tmk = bal(p + step > mflimitP1) & liveM & ~3ull;
         const bool live = __builtin_amdgcn_inverse_ballot_w64(liveM);
@@ -1051,21 +1026,9 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             h = P >> 19;
             tg = (P >> (19 - G::TB)) & ((1u << G::TB) - 1u);
         } else if constexpr (G::HT) {   // one product: hash5 = bits 52..63, tag = the TB bits below
-#if LZ4MT_EXP_HASH24
-            // P = (x K mod 2^40) << 24 for the 5 bytes x: with K = Kl + 0xCF 2^32,
-            // x K mod 2^40 = xl Kl + ((xl 0xCF + x4 0xBB) mod 2^8) 2^32 -- one
-            // 32x32 -> 64 multiply and two full-rate 24-bit ones instead of
-            // a 64x64 product's three quarter-rate multiplies
-            const uint32_t xl = (uint32_t)v8, xh = (uint32_t)(v8 >> 32);
-            const uint64_t M = (uint64_t)xl * 0x1BBCDCBBu;
-            const uint32_t hi = (uint32_t)(M >> 32) + __umul24(xl, 0xCFu) + __umul24(xh, 0xBBu);
-            h = __builtin_amdgcn_alignbit(hi, (uint32_t)M, 28) & 0xFFFu;
-            tg = ((uint32_t)M >> (28 - G::TB)) & ((1u << G::TB) - 1u);
-#else
             const uint64_t P = (v8 << 24) * 889523592379ull;
             h = (uint32_t)(P >> 52);
             tg = (uint32_t)(P >> (52 - G::TB)) & ((1u << G::TB) - 1u);
-#endif
         } else {
             h = lz4_hash<U16>(w0, (uint32_t)(v8 >> 32));
             tg = G::tag(w0);
@@ -1117,19 +1080,12 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
                 // lanes past the stop: the first of each bucket puts back the
                 // entry it displaced (the last mark up to the stop, or the
                 // table's entry); a later one displaced a lane past the stop.
-#if LZ4MT_EXP_TW
                 // Lanes are in position order and every entry a lane can
                 // displace is an older table entry or an earlier lane's
                 // mark, so "displaced by no lane past the stop" is "its
                 // position is at most lane wlim's" (P17 keeps positions
                 // mod 2^17: compare distances from p)
                 const bool first = P17 ? dq >= p - pB : (told & G::PM) <= pB;
-#else
-                (void)pB;
-                const uint64_t past = liveM & ~(wlim < 0 ? 0ull : mask_le((uint32_t)wlim));
-                const uint32_t pfl = rdlane(p, (int)sff1(past | (1ull << 63)));
-                const bool first = P17 ? dq > p - pfl : (told & G::PM) < pfl;
-#endif
                 tab.st((live && !le && first) ? h : dumIdx, told);
             } else {
                 tab.st((live && !le) ? h : dumIdx, told);
@@ -1212,33 +1168,20 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             }
         }
         if (havePe) store_pending();
-#if LZ4MT_EXP_TW
         // no stop in the window (w == 64): every insert stays, nothing to put
         // back -- unless an alias moved the stop here after the lanes past the
         // old one were put back (twRedo: they insert again)
         if (!twDone && (!XCHG || w < 64 || twRedo)) table_writes(w, wTerm, rdlane(p, (int)(w < 64 ? w - 1 : 63)));
-#else
-        if (!twDone) table_writes(w, wTerm, 0u);
-#endif
         STAMP_ADD(1, ts);
         STAMP_ADD(2, ts);
         if (w == 64) {   // no stop: the search goes on
-            sBase += 62 * ws0 + (62 > wj1 ? 62 - wj1 : 0u);
-            k0 = wk0 + 62;
+            sBase += 62 * s0 + (62 > j1 ? 62 - j1 : 0u);
+            k0 += 62;
             s0 = (63 + k0) >> 6;   // k0 >= 62: no max(1, .) needed
             j1 = (k0 < 65 ? 65u : ((k0 - 1) & ~63u) + 65) - k0;
             mode = 0;
             spanHi = 61 * s0 + (61 > j1 ? 61 - j1 : 0u);
         }
-      };
-      do {
-#if LZ4MT_EXP_PEEL
-        if (firstW) window(std::integral_constant<bool, true>{});
-        else window(std::integral_constant<bool, false>{});
-        firstW = false;
-#else
-        window(std::integral_constant<bool, false>{});
-#endif
       } while (w == 64);
         if (wTerm) {
             done = true;
@@ -1313,16 +1256,12 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             const uint32_t ipe = ip + kMinMatch + mc;
             anchor = ipe;
             done = fail || ipe >= mflimitP1;
-            sBase = ipe + 1;
-#if LZ4MT_EXP_PEEL
-            firstW = true;
-#else
             mode = 1;
+            sBase = ipe + 1;
             k0 = 0;
             s0 = 1;
             j1 = 65;
             spanHi = 61;
-#endif
             STAMP_ADD(4, ts);
         }
     }

@@ -227,9 +227,13 @@ def encode_xchg(s, cap):
                     if live[L] and L <= wlim:
                         T[h[L]] = mark[L]
             past = [L for L in range(64) if live[L] and L > wlim]
-            pfl = p[past[0]] if past else p[63]
-            for L in past:   # the first lane of each bucket past the stop restores
-                if (told[L] & MASK) < pfl:
+            # the first lane of each bucket past the stop restores: lanes are in
+            # position order, so "displaced by no lane past the stop" is "the
+            # displaced entry's position is at most lane wlim's" (the kernel's
+            # table_writes; no mask scan for the first lane past the stop)
+            pB = p[wlim] if wlim >= 0 else -1
+            for L in past:
+                if (told[L] & MASK) <= pB:
                     T[h[L]] = told[L]
 
         while True:
