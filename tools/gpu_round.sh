@@ -8,6 +8,7 @@
 #   trace   rocprofv3 kernel-trace stats of a 5-step bench run
 #   sq      SQ counters of the encoder / decoder (tools/kprof.py 2) + the window count (tools/kstats.py 2)
 #   pmc     FETCH_SIZE / WRITE_SIZE passes (tools/prof.sh without its trace)
+#   pmc32   the same at 32 GiB (configs[2]'s decompress traffic, tools/pmcsum.py --gib=32)
 #   pmcbid  the same on App. F at block ids 4, 5, 6 (the configs[4] sweep: profiles/pmc_b<id>.json)
 #   dist2   bench.py --gpus 2 over gloo on this one GPU (rehearsal of the N > 1 path)
 #   fcal    FETCH_SIZE calibration on a known byte count (tools/fetch_cal.py + fetchcal_sum.py)
@@ -67,6 +68,13 @@ for step in "$@"; do
         timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -T -f csv -d "$out/bid$bid/write_appf" -o write -- \
             python3 tools/kprof.py 8 --bid=$bid > "$out/bid$bid/write.log" 2>&1
       done ;;
+    pmc32)   # FETCH_SIZE / WRITE_SIZE of a 32 GiB App. F compress + decompress (configs[2]'s decode traffic)
+      mkdir -p "$out/p32"
+      timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -T -f csv -d "$out/p32/fetch_appf" -o fetch -- \
+          python3 tools/kprof.py 32 > "$out/fetch_32.log" 2>&1
+      timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -T -f csv -d "$out/p32/write_appf" -o write -- \
+          python3 tools/kprof.py 32 > "$out/write_32.log" 2>&1
+      tail -1 "$out/fetch_32.log" ;;
     e2e)
       timeout -k 10 300 python3 tools/e2e.py 8 7 > "$out/e2e_mem.txt" 2>&1 || { tail -20 "$out/e2e_mem.txt"; exit 1; }
       cat "$out/e2e_mem.txt"

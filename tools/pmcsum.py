@@ -12,14 +12,18 @@ argument); bench.py divides each kernel's FETCH_SIZE by that factor.
 With --bid=K (K != 7) the profile is the configs[4] sweep point of block id
 K (appf runs only): profiles/pmc_b<K>.json, its encoder kernel
 (k_encode16 at 64 KiB, k_encode_p17 at 256 KiB) calibrated like k_encode.
-usage: python tools/pmcsum.py <gpu_round dir> <tag> [fcal_summary.json] [--current] [--bid=K]"""
+With --gib=G (G != 8) the input is G GiB (tools/kprof.py G): --gib=32 is
+configs[2]'s 32 GiB stream, written to profiles/pmc_dec32.json (bench.py's
+--decompress-only line reads its k_decode traffic there).
+usage: python tools/pmcsum.py <gpu_round dir> <tag> [fcal_summary.json] [--current] [--bid=K] [--gib=G]"""
 import csv
 import glob
 import json
 import sys
 
 src, tag = sys.argv[1], sys.argv[2]
-N = 8 << 30
+GIB = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--gib=")), 8))
+N = GIB << 30
 
 
 def counters(run):
@@ -39,7 +43,7 @@ def counters(run):
 
 bid = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--bid=")), 7))
 appf = counters("appf")
-rnd = counters("random") if bid == 7 else {}
+rnd = counters("random") if bid == 7 and GIB == 8 else {}
 for k in appf.values():
     k["traffic_raw"] = k["fetch_bytes"] + k["write_bytes"]
 stats = glob.glob(f"{src}/trace/*kernel_stats.csv")
@@ -76,10 +80,12 @@ if "k_encode" in rnd:
                 "the counter factor -- not a calibration"}
 bm = 1 << (8 + 2 * bid)
 res = {"tag": tag, "config": {"bytes": N, "block_bytes": bm, "flg": 0x70,
-                              "workload": f"tools/kprof.py 8 --bid={bid}: 8 GiB App. F synthetic, {bm >> 10} KiB "
+                              "workload": f"tools/kprof.py {GIB} --bid={bid}: {GIB} GiB App. F synthetic, {bm >> 10} KiB "
                                           "blocks, -Sx -BX"},
        "kernels": appf, "calibration": cal, "random_input": rnd}
-json.dump(res, open(f"profiles/{tag}_pmc.json" if bid == 7 else f"profiles/pmc_b{bid}.json", "w"), indent=1)
+out = (f"profiles/pmc_dec{GIB}.json" if GIB != 8 else
+       f"profiles/{tag}_pmc.json" if bid == 7 else f"profiles/pmc_b{bid}.json")
+json.dump(res, open(out, "w"), indent=1)
 if "--current" in sys.argv:
     json.dump(res, open("profiles/pmc_current.json", "w"), indent=1)
 print(json.dumps({"kernels": {k: appf[k] for k in enc_kernels if k in appf}, "calibration": cal},
