@@ -534,8 +534,160 @@ struct CallBuf {
     bool alloc(size_t n) { return hipMalloc(&p, n) == hipSuccess; }
 };
 
+// ---------------------------------------------------------------------------
+// Streamed DEVICE compress (independent 1 / 4 MiB blocks, levels 0..2):
+// k_encode_stream (lz4mt_kernels.hip) is launched once, before the first
+// read(); the calling thread reads block after block into a ring of
+// coherent pinned staging slots and publishes each one; the persistent grid
+// encodes each block as soon as it is published and pushes its record's
+// payload into a ring of coherent pinned output slots; a writer thread
+// writes the records in block order as they appear.  So encoding overlaps
+// the reads (no batch waits for its last block, no batch-sized copy after
+// the last read) and the writes overlap the encodes.
+// LZ4MT_AMD_STREAM=0 keeps the batch pipeline below.
+// ---------------------------------------------------------------------------
+bool stream_enabled() {
+    const char* e = getenv("LZ4MT_AMD_STREAM");
+    return !e || atoi(e) != 0;
+}
+
+struct StreamBufs {
+    uint8_t *hIn = nullptr, *hOut = nullptr, *dIn = nullptr, *dSlot = nullptr;
+    uint32_t* hCtl = nullptr;       // g[8] | in[4 Rin] | out[4 Rout]  (coherent pinned)
+    uint32_t* dNext = nullptr;      // the grid's block counter
+    uint32_t bm = 0, waves = 0, Rin = 0, Rout = 0;
+    hipStream_t st = nullptr;
+    int dev = -1;
+    void release() {
+        if (st) hipStreamSynchronize(st);
+        hipHostFree(hIn); hipHostFree(hOut); hipHostFree(hCtl);
+        hipFree(dIn); hipFree(dSlot); hipFree(dNext);
+        if (st) hipStreamDestroy(st);
+        *this = StreamBufs();
+    }
+    bool ensure(uint32_t bm_, uint32_t waves_, uint32_t rin, uint32_t rout) {
+        int d = -1;
+        if (hipGetDevice(&d) != hipSuccess) return false;
+        if (hIn && bm == bm_ && waves == waves_ && Rin == rin && Rout == rout && dev == d) return true;
+        release();
+        bm = bm_; waves = waves_; Rin = rin; Rout = rout; dev = d;
+        const unsigned hf = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&hIn), (uint64_t)Rin * bm + 64, hf) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&hOut), (uint64_t)Rout * bm + 64, hf) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&hCtl), 4ull * (8 + 4ull * Rin + 4ull * Rout), hf) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&dIn), (uint64_t)waves * (bm + 64)) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&dSlot), (uint64_t)waves * (bm + 64)) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&dNext), 64) != hipSuccess) {
+            (void)hipGetLastError();
+            release();
+            return false;
+        }
+        return true;
+    }
+};
+thread_local StreamBufs g_stream;
+
+inline uint32_t ld_acq(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+inline void st_rel(uint32_t* p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+
+// spins briefly, then sleeps in 20 us steps, until pred() or stop()
+template <class P, class Q>
+bool host_wait(P pred, Q stop) {
+    for (int i = 0;; ++i) {
+        if (pred()) return true;
+        if (stop()) return false;
+        if (i < 64) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
+bool stream_eligible(const Session& s, const Lz4MtStreamDescriptor* sd) {
+    const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
+    return stream_enabled() && sd->flg.blockIndependence && s.level() < 3 && bm >= (1u << 20) && bm <= (4u << 20);
+}
+
+void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
+    const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
+    const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
+    int cus = 0, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+        hipSuccess || cus <= 0) {
+        s.quit(LZ4MT_RESULT_ERROR);
+        return;
+    }
+    // a wave per 20 KiB of LDS: 8 per CU; the staging ring only has to stay
+    // ahead of the pulls (~1 ms per block), the output ring behind the writer
+    const uint32_t waves = (uint32_t)cus * 8;
+    const uint32_t Rin = (uint32_t)env_int("LZ4MT_AMD_STREAM_IN", 256, 8, 65536);
+    const uint32_t Rout = (uint32_t)env_int("LZ4MT_AMD_STREAM_OUT", 512, 8, 65536);
+    StreamBufs& B = g_stream;
+    if (!B.ensure(bm, waves, Rin, Rout)) { s.quit(LZ4MT_RESULT_ERROR); return; }
+    uint32_t* g = B.hCtl;
+    uint32_t* inC = g + 8;
+    uint32_t* outC = inC + 4ull * Rin;
+    memset(g, 0, 4ull * (8 + 4ull * Rin + 4ull * Rout));
+    g[0] = 0xFFFFFFFFu;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    if (hipMemsetAsync(B.dNext, 0, 4, B.st) != hipSuccess ||
+        launch_encode_stream(B.hIn, B.hOut, inC, outC, g, B.dNext, B.dIn, B.dSlot, bm, Rin, Rout, waves, bck ? 1 : 0,
+                             B.st) != hipSuccess) {
+        (void)hipGetLastError();
+        s.quit(LZ4MT_RESULT_ERROR);
+        return;
+    }
+    std::atomic<uint32_t> total{0xFFFFFFFFu};   // blocks in the stream, once known
+    std::atomic<bool> wfail{false};
+    auto gpuFailed = [&] { return ld_acq(g + 4) != 0; };
+    std::thread writer([&] {
+        for (uint32_t b = 0;; ++b) {
+            uint32_t* o = outC + 4ull * (b % Rout);
+            const bool ok = host_wait([&] { return ld_acq(o) == b + 1 || b >= total.load(); },
+                                      [&] { return gpuFailed() || ld_acq(g + 1) != 0; });
+            if (!ok || (b >= total.load() && ld_acq(o) != b + 1)) {
+                if (!ok) wfail = true;
+                return;
+            }
+            const uint32_t word = ld_acq(o + 1), len = word & ~kRawBit, sum = ld_acq(o + 2);
+            const uint8_t* payload = B.hOut + (uint64_t)(b % Rout) * bm;
+            if (!s.writeU32(word) || !s.write(payload, (int)len) || (bck && !s.writeU32(sum))) {
+                wfail = true;
+                st_rel(g + 1, 1u);   // abort: the grid and the reader stop
+                return;
+            }
+            st_rel(o + 3, b + 1);   // the slot may take block b + Rout
+            st_rel(g + 3, b + 1);   // heartbeat
+        }
+    });
+    // the reader: every read() on this thread, one block per read (a short
+    // read is a short block; 0 ends the stream: src/lz4mt.cpp:434-447)
+    uint32_t b = 0;
+    for (;; ++b) {
+        uint32_t* ic = inC + 4ull * (b % Rin);
+        if (b >= Rin && !host_wait([&] { return ld_acq(ic + 2) == b - Rin + 1; },
+                                   [&] { return gpuFailed() || ld_acq(g + 1) != 0; }))
+            break;
+        if (ld_acq(g + 1) != 0 || gpuFailed()) break;   // the writer or the grid stopped
+        uint8_t* dst = B.hIn + (uint64_t)(b % Rin) * bm;
+        const int n = s.read(dst, (int)bm);
+        if (n <= 0) break;
+        if (sck) xs.update(dst, (size_t)n);
+        st_rel(ic + 1, (uint32_t)n);
+        st_rel(ic, b + 1);
+        st_rel(g + 2, b + 1);   // heartbeat
+    }
+    total = b;
+    st_rel(g, b);   // waves waiting for a block >= b leave
+    writer.join();
+    if (wfail || gpuFailed()) st_rel(g + 1, 1u);
+    const hipError_t e = hipStreamSynchronize(B.st);
+    if (e != hipSuccess || gpuFailed() || (wfail && !s.error())) s.quit(LZ4MT_RESULT_ERROR);
+    if (!(s.mode() & LZ4MT_MODE_DEVICE)) B.release();
+}
+
 void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
     if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return; }
+    if (stream_eligible(s, sd)) { compress_streamed(s, sd, xs); return; }
     // LZ4-HC on independent blocks: levels 3..9 the hashChain parser, 10..12
     // (and above, clamped) the optimal parser.  Block-dependent frames at any
     // level >= 3 are the reference's HC stream, at level 9 (HcBdSim).
@@ -854,7 +1006,7 @@ bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
 // Frees this thread's cached DEVICE-engine slots (pinned staging, device
 // buffers, streams); called by lz4mtHipReleaseCaches.
 namespace lz4mt {
-void release_slot_cache() { g_slots.release(); }
+void release_slot_cache() { g_slots.release(); g_stream.release(); }
 }  // namespace lz4mt
 
 // ===========================================================================

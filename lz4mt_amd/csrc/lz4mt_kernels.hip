@@ -891,8 +891,10 @@ __device__ __forceinline__ void publish_progress(uint32_t* pub, uint32_t v) {
 // per device (k_xchg_order) and runs the !XCHG instantiation -- read, write
 // the marker, read back, resolve same-bucket predecessors exactly -- when the
 // check fails (or LZ4MT_AMD_ENC_PROBE=readback forces it).
+// DUP: no effect on the code; a separate instantiation for a kernel that
+// must not share (and so outline) another kernel's one (k_encode_stream).
 template <bool ST, bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false, bool PUB = false,
-          bool XH = false, bool XCHG = true>
+          bool XH = false, bool XCHG = true, bool DUP = false>
 __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
                                    l_u32* __restrict__ T, l_u8* __restrict__ R, uint64_t* acc,
                                    LinkArgs lk = LinkArgs{0, 0, 0, true}, uint32_t* pub = nullptr) {
@@ -3395,6 +3397,142 @@ __global__ void __launch_bounds__(64) k_xxh32_stored(const uint8_t* __restrict__
     const int32_t cs = csize[b];
     const uint32_t h = xxh32_wave(cs > 0 ? gptr(slots) + off : gptr(src) + off, cs > 0 ? (uint64_t)cs : n, (l_u32*)buf);
     if (laneid() == 0) digest[b] = h;
+}
+
+// ---------------------------------------------------------------------------
+// Streamed compress: lz4mtCompress over the callbacks (MODE_DEVICE, or a
+// relinked PARALLEL caller), independent 1 / 4 MiB blocks, levels 0..2
+// (reference compress(), src/lz4mt.cpp:372-457, and the
+// FILE* reads of src/lz4mt_io_cstdio.cpp:112-118).  Batches of blocks staged
+// to HBM and encoded by one launch each leave a whole block latency plus the
+// last batch's copy after the final read(); here ONE persistent grid encodes
+// every block as soon as the host has read it:
+//   * the host reads block b into in[b % Rin] (coherent pinned memory: GPU
+//     reads of it are never served from a GPU cache), then publishes its
+//     length and b + 1 in that slot's control words;
+//   * a wave takes the next block number (a device counter), waits for it
+//     (system-scope polls with s_sleep), copies it into its own HBM buffer,
+//     marks the staging slot free, encodes it (the frame encoder's code, its
+//     own instantiation), hashes the stored bytes (block XXH32), waits until
+//     out[b % Rout] is free, pushes the stored bytes there (coherent pinned)
+//     and publishes size word, checksum and b + 1;
+//   * a host writer thread calls write() record by record in block order as
+//     they appear.
+// Every wait gives up after kStreamWaitTicks without progress of the other
+// side (a heartbeat word), so the grid always drains; the host sets the
+// block count once read() returns 0 and every wave still waiting leaves.
+// Control words (u32, coherent pinned host memory):
+//   g[0] blocks in the stream (0xFFFFFFFF until known)  g[1] abort (host)
+//   g[2] blocks read (heartbeat)  g[3] records written (heartbeat)
+//   g[4] error (GPU: a wait timed out)
+//   in[r]  {seq = b + 1, length, pulled = b + 1}   (4 words per slot)
+//   out[r] {seq = b + 1, size word, XXH32, written = b + 1}
+// A waiting wave sleeps in proportion to how far the awaited heartbeat is
+// from its target (~35 us per block still to come, at most ~1.8 ms), so 2048
+// waves waiting for blocks far ahead of the reader cost the PCIe link only a
+// few hundred thousand small reads per second.
+// ---------------------------------------------------------------------------
+constexpr uint64_t kStreamWaitTicks = 60ull * 100000000ull;   // s_memrealtime: 100 MHz -> 60 s
+__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// n bytes, both sides 16-byte aligned: dwordx4 per lane, 8 in flight
+__device__ __forceinline__ void wave_copy16(g_u8* d, g_cu8* s, uint32_t n) {
+    const uint32_t L = laneid(), n16 = n >> 4;
+    for (uint32_t i = L; i < n16; i += 64 * 8) {
+        v4u v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (i + 64 * k < n16) v[k] = ((g_cu4*)s)[i + 64 * k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (i + 64 * k < n16) ((g_u4*)d)[i + 64 * k] = v[k];
+    }
+    for (uint32_t i = (n16 << 4) + L; i < n; i += 64) d[i] = s[i];
+}
+// Waits until *w == want.  hb: the heartbeat (2 = blocks read, 3 = records
+// written) that reaches `target` when *w is about to change.  false on
+// abort, on a timeout (g[4] set), or -- endAt >= 0 -- once the stream is
+// known to hold no block endAt (*ended).
+__device__ __forceinline__ bool stream_wait(const uint32_t* w, uint32_t want, uint32_t* g, uint32_t hb,
+                                            uint32_t target, int64_t endAt, bool* ended) {
+    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t beat = ld_sys(g + hb);
+    for (;;) {
+        if (ld_sys(w) == want) return true;
+        const uint32_t total = ld_sys(g), abort = ld_sys(g + 1), now = ld_sys(g + hb);
+        if (endAt >= 0 && (uint64_t)endAt >= total) { *ended = true; return false; }
+        if (abort) return false;
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        if (now != beat) { beat = now; t0 = t; }
+        else if (t - t0 > kStreamWaitTicks) {
+            if (laneid() == 0) st_sys(g + 4, 1u);
+            return false;
+        }
+        const uint32_t dist = target > now ? min(target - now, 64u) : 0u;
+        for (uint32_t k = 0; k < 8 * dist + 2; ++k) __builtin_amdgcn_s_sleep(127);
+    }
+}
+
+template <bool XC>
+__global__ void __launch_bounds__(64) k_encode_stream(const uint8_t* __restrict__ hin, uint8_t* __restrict__ hout,
+                                                      uint32_t* inCtl, uint32_t* outCtl, uint32_t* g,
+                                                      uint32_t* __restrict__ next, uint8_t* __restrict__ dIn,
+                                                      uint8_t* __restrict__ dSlot, uint32_t bm, uint32_t Rin,
+                                                      uint32_t Rout, int bck) {
+    ENCODE_LDS
+    const uint32_t L = laneid();
+    g_u8* din = gptr(dIn) + (uint64_t)blockIdx.x * (bm + 64);
+    g_u8* dsl = gptr(dSlot) + (uint64_t)blockIdx.x * (bm + 64);
+    for (;;) {
+        uint32_t b = 0;
+        if (L == 0) b = atomicAdd(next, 1u);
+        b = rdlane(b, 0);
+        const uint32_t ri = b % Rin, ro = b % Rout;
+        bool ended = false;
+        if (!stream_wait(inCtl + 4 * ri, b + 1, g, 2, b + 1, (int64_t)b, &ended)) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        const uint32_t n = ld_sys(inCtl + 4 * ri + 1);
+        wave_copy16(din, gptr(hin) + (uint64_t)ri * bm, n);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (L == 0) st_sys(inCtl + 4 * ri + 2, b + 1);   // the staging slot may be refilled
+        int32_t r;
+        if (n < (uint32_t)kLimit64K)
+            r = encode_block<true, false, false>(din, n, dsl, n, (l_u32*)T, (l_u8*)S, (l_u32*)X, (l_u8*)X + kRingE,
+                                                 nullptr);
+        else
+            [[clang::always_inline]] r = encode_block_v5<false, false, false, false, false, false, false, XC, true>(
+                din, n, dsl, n, (l_u32*)T, (l_u8*)X, nullptr);
+        WAVE_SYNC();
+        g_cu8* stored = r > 0 ? dsl : din;
+        const uint32_t sl = r > 0 ? (uint32_t)r : n;
+        const uint32_t sum = bck ? xxh32_wave(stored, sl, (l_u32*)T) : 0u;
+        // the record's slot in host memory: free once the writer wrote block b - Rout
+        if (b >= Rout && !stream_wait(outCtl + 4 * ro + 3, b - Rout + 1, g, 3, b - Rout + 1, -1, &ended)) return;
+        wave_copy16(gptr(hout) + (uint64_t)ro * bm, stored, sl);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (L == 0) {
+            st_sys(outCtl + 4 * ro + 1, r > 0 ? (uint32_t)r : (n | 0x80000000u));
+            st_sys(outCtl + 4 * ro + 2, sum);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (L == 0) st_sys(outCtl + 4 * ro, b + 1);
+    }
+}
+
+hipError_t launch_encode_stream(const uint8_t* hin, uint8_t* hout, uint32_t* inCtl, uint32_t* outCtl, uint32_t* g,
+                                uint32_t* next, uint8_t* dIn, uint8_t* dSlot, uint32_t bm, uint32_t Rin,
+                                uint32_t Rout, uint32_t waves, int bck, hipStream_t st) {
+    bool xc = true;
+    if (const hipError_t r = encoder_path(st, &xc); r != hipSuccess) return r;
+    if (bm < (uint32_t)kLimit64K || bm > (1u << kPosBits) || !waves || !Rin || !Rout) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(xc ? k_encode_stream<true> : k_encode_stream<false>, dim3(waves), dim3(64), 0, st, hin, hout,
+                       inCtl, outCtl, g, next, dIn, dSlot, bm, Rin, Rout, bck);
+    return hipGetLastError();
 }
 
 __global__ void __launch_bounds__(64) k_xxh32_frame_blocks(const uint8_t* __restrict__ frame,

@@ -1,0 +1,172 @@
+"""The streamed callback compress.
+
+lz4mtCompress in MODE_DEVICE (and a relinked PARALLEL caller with null codec
+callbacks) over independent 1 / 4 MiB blocks runs ONE persistent encoder grid
+(k_encode_stream) that encodes each block as soon as read() has returned
+it, while a writer thread writes the records in block order as they appear
+(reference compress(), src/lz4mt.cpp:372-457: one read() per block, a read
+of 0 ends the stream, write() per record piece).  Frames must be byte for
+byte the batch engine's (LZ4MT_AMD_STREAM=0) and the App. F known answers;
+the staging / output rings are forced tiny so they wrap thousands of times;
+short reads are short blocks; a failing write() ends the call with an error
+and the grid drains (the next call works)."""
+import ctypes
+import random
+import struct
+
+import pytest
+import torch
+import xxhash
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+L = None
+
+APP_F = {  # SURVEY.md App. F, 256 MiB seed 42: (sck, bck, bid) -> (frame bytes, XXH32(frame))
+    (1, 0, 7): (133159140, 0x157099A8), (0, 0, 7): (133159136, 0x8AC5DBC8), (1, 1, 7): (133159396, 0xC532D9D2),
+    (0, 1, 7): (133159392, 0x1686045A), (1, 0, 6): (133770948, 0x7D1BC1BA), (0, 1, 6): (133771968, 0x535404A3),
+}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def lib():
+    global L
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    import lz4mt_amd
+    L = lz4mt_amd
+    return L
+
+
+@pytest.fixture(scope="module")
+def data256():
+    d = oracle.gen_synthetic(256 << 20, 42)
+    assert xxhash.xxh32(d).intdigest() == 0xE6F24EBA
+    return d
+
+
+@pytest.mark.parametrize("row", sorted(APP_F))
+def test_streamed_known_answers(data256, row):
+    sck, bck, bid = row
+    r, frame = L.compress(data256, L.make_sd(bid, bool(sck), bool(bck)), mode=L.MODE_DEVICE)
+    assert r == 0, L.result_to_string(r)
+    assert (len(frame), xxhash.xxh32(frame).intdigest()) == APP_F[row], row
+    r, out, _ = L.decompress(frame, len(data256) + 64, mode=L.MODE_DEVICE)
+    assert r == 0 and xxhash.xxh32(out).intdigest() == 0xE6F24EBA
+
+
+@pytest.mark.parametrize("rin,rout", [(8, 8), (9, 64), (256, 11)])
+def test_streamed_tight_rings(data256, monkeypatch, rin, rout):
+    """Staging and output rings of a few slots: the reader waits for pulls,
+    the waves wait for the writer -- same bytes; the PARALLEL mode with null
+    codecs takes the same engine."""
+    monkeypatch.setenv("LZ4MT_AMD_STREAM_IN", str(rin))
+    monkeypatch.setenv("LZ4MT_AMD_STREAM_OUT", str(rout))
+    for row, m in (((0, 1, 6), L.MODE_DEVICE), ((1, 0, 7), L.MODE_PARALLEL)):
+        sck, bck, bid = row
+        r, frame = L.compress(data256, L.make_sd(bid, bool(sck), bool(bck)), mode=m)
+        assert r == 0 and (len(frame), xxhash.xxh32(frame).intdigest()) == APP_F[row], (rin, rout, row)
+
+
+def test_streamed_equals_batched(monkeypatch):
+    """Mixed input (App. F text, incompressible stretches, zero runs; raw and
+    compressed blocks) at 1 and 4 MiB blocks: the streamed frame is the batch
+    engine's, byte for byte, and the oracle's."""
+    rnd = random.Random(3)
+    syn = oracle.gen_synthetic(40 << 20, 7)
+    data = bytearray(syn)
+    for s in range(0, len(data), 5 << 20):
+        data[s:s + 1_500_000] = oracle.gen_random(1_500_000, s)
+        z, k = s + 3_000_000, rnd.randrange(1, 900_000)
+        data[z:z + k] = bytes(k)
+    data = bytes(data[:(40 << 20) - 12345])
+    for bid, sck, bck in ((6, True, True), (7, False, True), (6, False, False)):
+        sd = L.make_sd(bid, sck, bck)
+        r1, f1 = L.compress(data, sd, mode=L.MODE_DEVICE)
+        monkeypatch.setenv("LZ4MT_AMD_STREAM", "0")
+        r2, f2 = L.compress(data, sd, mode=L.MODE_DEVICE)
+        monkeypatch.delenv("LZ4MT_AMD_STREAM")
+        assert r1 == r2 == 0 and f1 == f2, (bid, sck, bck)
+        assert f1 == oracle.compress_frame(data, oracle.params(bid, sck, bck)), (bid, sck, bck)
+
+
+def _callbacks(data, sd, chunk_seed=None, fail_after=None):
+    """lz4mtCompress in MODE_DEVICE with Python callbacks: random short reads
+    (chunk_seed), or a write() that fails from its fail_after-th call on."""
+    from lz4mt_amd import _abi
+    rnd = random.Random(chunk_seed)
+    src = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+    st = {"pos": 0, "w": 0}
+    reads, out = [], []
+
+    def rd(ctx, dst, n):
+        k = min(n, len(data) - st["pos"])
+        if chunk_seed is not None and k > 1:
+            k = rnd.choice([k, k, max(1, k // 3), rnd.randrange(1, k + 1)])
+        ctypes.memmove(dst, ctypes.addressof(src) + st["pos"], k)
+        st["pos"] += k
+        reads.append(k)
+        return k
+
+    def wr(ctx, p, n):
+        st["w"] += 1
+        if fail_after is not None and st["w"] > fail_after:
+            return -1
+        out.append(ctypes.string_at(p, n))
+        return n
+
+    keep = [_abi.READ_FN(rd), _abi.WRITE_FN(wr)]
+    ctx = L.init_context()
+    ctx.mode = L.MODE_DEVICE
+    ctx.read = ctypes.cast(keep[0], ctypes.c_void_p)
+    ctx.write = ctypes.cast(keep[1], ctypes.c_void_p)
+    r = L.lib.lz4mtCompress(ctypes.byref(ctx), ctypes.byref(sd))
+    return r, b"".join(out), reads
+
+
+def test_streamed_short_reads_are_short_blocks():
+    data = oracle.gen_synthetic(30 << 20, 5)
+    for bid, sck, bck, seed in ((6, True, True, 1), (7, False, True, 2)):
+        r, frame, reads = _callbacks(data, L.make_sd(bid, sck, bck), chunk_seed=seed)
+        assert r == 0, L.result_to_string(r)
+        pieces, pos = [], 0
+        for k in reads:
+            if k:
+                pieces.append(data[pos:pos + k])
+                pos += k
+        bm = 1 << (8 + 2 * bid)
+        assert pos == len(data) and any(len(p) < bm for p in pieces[:-1])
+        head = oracle.compress_frame(b"", oracle.params(bid, sck, bck))[:7]
+        want = bytearray(head)
+        for p in pieces:
+            c = oracle.compress_block(p, len(p))
+            stored = c if c else p
+            want += struct.pack("<I", len(c) if c else len(p) | 0x80000000) + stored
+            if bck:
+                want += struct.pack("<I", xxhash.xxh32(stored).intdigest())
+        want += b"\0\0\0\0"
+        if sck:
+            want += struct.pack("<I", xxhash.xxh32(data).intdigest())
+        assert frame == bytes(want), (bid, sck, bck)
+
+
+def test_streamed_empty_and_tiny_inputs():
+    for data in (b"", b"x", oracle.gen_synthetic(1 << 20, 3), oracle.gen_synthetic((1 << 20) + 5, 3)):
+        sd = L.make_sd(6, True, True)
+        r, frame, _ = _callbacks(data, sd)
+        assert r == 0 and frame == oracle.compress_frame(data, oracle.params(6, True, True)), len(data)
+
+
+def test_streamed_write_failure_drains():
+    """write() fails part-way: the call returns an error (no hang, the grid
+    drains), the records before it were written, and the next call is fine."""
+    data = oracle.gen_synthetic(64 << 20, 9)
+    sd = L.make_sd(6, False, True)
+    r, frame, _ = _callbacks(data, sd, fail_after=40)
+    assert r != 0
+    want = oracle.compress_frame(data, oracle.params(6, False, True))
+    assert want.startswith(frame) and len(frame) > 7
+    r, frame, _ = _callbacks(data, sd)
+    assert r == 0 and frame == want

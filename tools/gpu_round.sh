@@ -17,10 +17,12 @@
 #   ab      kernel times of every exp_libs/*.so (tools/mkvariants.sh), two passes
 #   abtrace kernel-trace stats of every exp_libs/*.so;  abbid  ab at every block size
 #   fuzz    random differential campaign (300 s);  sweep  the secondary bench configs
+#   e2ems   end-to-end memory path: streamed compress vs the batch engine
 #   e2e     end-to-end rates (tools/e2e.py 8 7: host memory, then file -> file in /dev/shm)
 #   occ     encoder time against resident waves per CU (tools/occ_sweep.py)
 #   ovl     the split parse's parse work with real overlap (occ_sweep.py --overlap)
 #   bdref   the -BD reference-bytes tests (tests/test_gpu_bd.py -k reference)
+#   tstream the streamed callback compress tests + the callback-engine config tests
 #   nccl1   the world-size-1 nccl tests (tests/test_gpu_dist.py -k nccl)
 set -euo pipefail
 tag=$1; shift
@@ -68,6 +70,11 @@ for step in "$@"; do
         timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -T -f csv -d "$out/bid$bid/write_appf" -o write -- \
             python3 tools/kprof.py 8 --bid=$bid > "$out/bid$bid/write.log" 2>&1
       done ;;
+    e2ems)   # end-to-end memory path, streamed compress (default) and the batch engine (LZ4MT_AMD_STREAM=0)
+      timeout -k 10 300 python3 tools/e2e.py 8 7 > "$out/e2e_mem_stream.txt" 2>&1 || { tail -20 "$out/e2e_mem_stream.txt"; exit 1; }
+      LZ4MT_AMD_STREAM=0 timeout -k 10 300 python3 tools/e2e.py 8 7 > "$out/e2e_mem_batch.txt" 2>&1 \
+          || { tail -20 "$out/e2e_mem_batch.txt"; exit 1; }
+      grep e2e "$out/e2e_mem_stream.txt" | sed 's/^/streamed: /'; grep e2e "$out/e2e_mem_batch.txt" | sed 's/^/batch: /' ;;
     pmc32)   # FETCH_SIZE / WRITE_SIZE of a 32 GiB App. F compress + decompress (configs[2]'s decode traffic)
       mkdir -p "$out/p32"
       timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -T -f csv -d "$out/p32/fetch_appf" -o fetch -- \
@@ -93,6 +100,10 @@ for step in "$@"; do
       timeout -k 10 600 python3 -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread tests/test_gpu_bd.py \
           -k reference > "$out/pytest_bdref.log" 2>&1 || { tail -40 "$out/pytest_bdref.log"; exit 1; }
       tail -3 "$out/pytest_bdref.log" ;;
+    tstream)   # the streamed callback compress (tests/test_gpu_stream.py) and the callback-engine tests
+      timeout -k 10 900 python3 -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread tests/test_gpu_stream.py \
+          tests/test_gpu_configs.py > "$out/pytest_stream.log" 2>&1 || { tail -40 "$out/pytest_stream.log"; exit 1; }
+      tail -3 "$out/pytest_stream.log" ;;
     nccl1)
       timeout -k 10 600 python3 -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread tests/test_gpu_dist.py \
           -k nccl > "$out/pytest_nccl1.log" 2>&1 || { tail -40 "$out/pytest_nccl1.log"; exit 1; }
