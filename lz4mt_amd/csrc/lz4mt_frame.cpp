@@ -659,25 +659,44 @@ void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
             st_rel(g + 3, b + 1);   // heartbeat
         }
     });
+    // the content checksum (FLG.2) is one serial XXH32 chain: a hasher
+    // thread runs it over the staged blocks in order, beside the reads (a
+    // staging slot is refilled only once it is both pulled and hashed)
+    std::atomic<uint32_t> hashed{0};
+    std::thread hasher;
+    if (sck) {
+        hasher = std::thread([&] {
+            for (uint32_t h = 0;; ++h) {
+                const uint32_t* ic = inC + 4ull * (h % Rin);
+                if (!host_wait([&] { return ld_acq(ic) == h + 1 || h >= total.load(); },
+                               [&] { return gpuFailed() || ld_acq(g + 1) != 0; }) ||
+                    ld_acq(ic) != h + 1)
+                    return;
+                xs.update(B.hIn + (uint64_t)(h % Rin) * bm, ld_acq(ic + 1));
+                hashed.store(h + 1, std::memory_order_release);
+            }
+        });
+    }
     // the reader: every read() on this thread, one block per read (a short
     // read is a short block; 0 ends the stream: src/lz4mt.cpp:434-447)
     uint32_t b = 0;
     for (;; ++b) {
         uint32_t* ic = inC + 4ull * (b % Rin);
-        if (b >= Rin && !host_wait([&] { return ld_acq(ic + 2) == b - Rin + 1; },
+        if (b >= Rin && !host_wait([&] { return ld_acq(ic + 2) == b - Rin + 1 &&
+                                                (!sck || hashed.load(std::memory_order_acquire) > b - Rin); },
                                    [&] { return gpuFailed() || ld_acq(g + 1) != 0; }))
             break;
         if (ld_acq(g + 1) != 0 || gpuFailed()) break;   // the writer or the grid stopped
         uint8_t* dst = B.hIn + (uint64_t)(b % Rin) * bm;
         const int n = s.read(dst, (int)bm);
         if (n <= 0) break;
-        if (sck) xs.update(dst, (size_t)n);
         st_rel(ic + 1, (uint32_t)n);
         st_rel(ic, b + 1);
         st_rel(g + 2, b + 1);   // heartbeat
     }
     total = b;
     st_rel(g, b);   // waves waiting for a block >= b leave
+    if (hasher.joinable()) hasher.join();
     writer.join();
     if (wfail || gpuFailed()) st_rel(g + 1, 1u);
     const hipError_t e = hipStreamSynchronize(B.st);

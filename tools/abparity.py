@@ -27,13 +27,20 @@ def main():
         src = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
         for bid in (4, 5, 6, 7):
             for sck, bck in ((False, True), (True, False)):
-                got = bytes(L.compress_frame(src, L.make_sd(bid, sck, bck)).cpu().numpy().tobytes())
+                fr = L.compress_frame(src, L.make_sd(bid, sck, bck))
+                got = bytes(fr.cpu().numpy().tobytes())
                 if got != oracle.compress_frame(data, oracle.params(bid, sck, bck)):
                     bad.append((label, bid, sck, bck))
+                out, r = L.decompress_frame(fr)
+                if r != 0 or not torch.equal(out, src):
+                    bad.append(("decode", label, bid, sck, bck))
     t = L.gen_synthetic(256 << 20)
     fr = L.compress_frame(t, L.make_sd(7, False, True))
     if (fr.numel(), L.xxh32(fr)) != (133159392, 0x1686045A):
         bad.append("known answer 256 MiB B7 -Sx -BX")
+    out, r = L.decompress_frame(fr)
+    if r != 0 or L.xxh32(out) != 0xE6F24EBA:
+        bad.append("decode of the 256 MiB known answer")
     print(f"{name}: parity {'OK' if not bad else 'MISMATCH ' + str(bad)}")
     sys.exit(1 if bad else 0)
 
