@@ -30,9 +30,10 @@ for _ in range(3):
     wc, wd = min(wc, t1 - t0), min(wd, t2 - t1)
     L.lib.lz4mtHipGetTimings(ms)
     dec, xd = min(dec, ms[1]), min(xd, ms[2])
-    assert r == 0
+    assert r == 0 or os.environ.get("KTIME_NOCHECK") == "1"
     del fr, out
-assert torch.equal(L.decompress_frame(L.compress_frame(src, sd))[0], src)
+if os.environ.get("KTIME_NOCHECK") != "1":
+    assert torch.equal(L.decompress_frame(L.compress_frame(src, sd))[0], src)
 xcs = f"{xc:.2f}" if xc > 0.05 else "side stream"   # frame compress runs it beside the assembly
 print(f"{os.path.basename(os.environ.get('LZ4MT_AMD_LIB', 'product'))}: encode {enc:.2f} ms  decode {dec:.2f} ms  "
       f"| block xxh32 {xcs} / {xd:.2f} ms (+verify) | compress call {wc * 1e3:.2f} ms  decompress call {wd * 1e3:.2f} ms")
