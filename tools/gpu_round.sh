@@ -17,6 +17,7 @@
 #   ab      kernel times of every exp_libs/*.so (tools/mkvariants.sh), two passes
 #   abtrace kernel-trace stats of every exp_libs/*.so;  abbid  ab at every block size
 #   fuzz    random differential campaign (300 s);  sweep  the secondary bench configs
+#   probe   k_encode with the exchange probe vs the read-back fallback
 #   e2ems   end-to-end memory path: streamed compress vs the batch engine
 #   e2e     end-to-end rates (tools/e2e.py 8 7: host memory, then file -> file in /dev/shm)
 #   occ     encoder time against resident waves per CU (tools/occ_sweep.py)
@@ -167,6 +168,12 @@ for step in "$@"; do
         BID=$b bash tools/ab.sh >> "$out/ab_bid.txt" 2>&1
       done
       cat "$out/ab_bid.txt" ;;
+    probe)   # kernel times with the exchange probe (default) and the read-back fallback (LZ4MT_AMD_ENC_PROBE=readback)
+      for i in 1 2; do
+        timeout -k 10 200 python3 tools/ktime.py 2>&1 | tail -1 | sed 's/^/exchange  /' | tee -a "$out/probe.txt"
+        LZ4MT_AMD_ENC_PROBE=readback timeout -k 10 200 python3 tools/ktime.py 2>&1 | tail -1 | sed 's/^/read-back /' \
+            | tee -a "$out/probe.txt"
+      done ;;
     fuzz)   # time-boxed random differential campaign (seed 7) against the oracle / liblz4
       timeout -k 10 420 python3 -u tools/fuzz_campaign.py 300 ${FUZZ_SEED:-7} > "$out/fuzz.txt" 2>&1
       tail -2 "$out/fuzz.txt" ;;
