@@ -12,7 +12,7 @@ import lz4mt_amd as L  # noqa: E402
 
 n = 8 << 30
 src = L.gen_synthetic(n)
-sd = L.make_sd(int(os.environ.get("BID", "7")), False, True)
+sd = L.make_sd(int(os.environ.get("BID", "7")), False, os.environ.get("KTIME_BCK", "1") == "1")
 L.lib.lz4mtHipSetTiming(1)
 ms = (ctypes.c_float * 4)()
 enc, dec, wc, wd, xc, xd = 1e9, 1e9, 1e9, 1e9, 1e9, 1e9
