@@ -891,10 +891,146 @@ bool decompress_host(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
 }
 
 // ---------------------------------------------------------------------------
+// Streamed DEVICE decompress (independent 1 / 4 MiB blocks): k_decode_stream
+// is launched once, before the first record is read; the calling thread
+// reads record after record (size word, stored bytes, block checksum) into
+// the staging ring, the persistent grid decodes each one as soon as it is
+// published and pushes the decoded bytes into the output ring, a writer
+// thread writes them in block order and a hasher thread runs the content
+// checksum (FLG.2) over them beside it.  Errors keep the batch engine's
+// order: a block that fails to decode stops the frame before it is written,
+// a block checksum mismatch after it is written, and a read error found
+// while reading applies once every record before it is written.
+// LZ4MT_AMD_STREAM=0 keeps the batch engine below.
+// ---------------------------------------------------------------------------
+bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
+    const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
+    const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
+    int cus = 0, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+        hipSuccess || cus <= 0) {
+        s.quit(LZ4MT_RESULT_ERROR);
+        return false;
+    }
+    const uint32_t waves = (uint32_t)cus * 8;   // a wave per 20 KiB of LDS
+    const uint32_t Rin = (uint32_t)env_int("LZ4MT_AMD_STREAM_IN", 256, 8, 65536);
+    const uint32_t Rout = (uint32_t)env_int("LZ4MT_AMD_STREAM_OUT", 512, 8, 65536);
+    StreamBufs& B = g_stream;
+    if (!B.ensure(bm, waves, Rin, Rout)) { s.quit(LZ4MT_RESULT_ERROR); return false; }
+    uint32_t* g = B.hCtl;
+    uint32_t* inC = g + 8;
+    uint32_t* outC = inC + 4ull * Rin;
+    memset(g, 0, 4ull * (8 + 4ull * Rin + 4ull * Rout));
+    g[0] = 0xFFFFFFFFu;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    if (hipMemsetAsync(B.dNext, 0, 4, B.st) != hipSuccess ||
+        launch_decode_stream(B.hIn, B.hOut, inC, outC, g, B.dNext, B.dIn, B.dSlot, bm, Rin, Rout, waves, bck ? 1 : 0,
+                             B.st) != hipSuccess) {
+        (void)hipGetLastError();
+        s.quit(LZ4MT_RESULT_ERROR);
+        return false;
+    }
+    std::atomic<uint32_t> total{0xFFFFFFFFu};
+    std::atomic<bool> wfail{false};
+    std::atomic<uint32_t> hashed{0};
+    auto gpuFailed = [&] { return ld_acq(g + 4) != 0; };
+    auto stopped = [&] { return gpuFailed() || ld_acq(g + 1) != 0; };
+    // the content checksum over the decoded blocks, in order, beside the writer
+    std::thread hasher;
+    if (sck) {
+        hasher = std::thread([&] {
+            for (uint32_t h = 0;; ++h) {
+                const uint32_t* o = outC + 4ull * (h % Rout);
+                if (!host_wait([&] { return ld_acq(o) == h + 1 || h >= total.load(); }, stopped) || ld_acq(o) != h + 1)
+                    return;
+                const int32_t n = (int32_t)ld_acq(o + 1);
+                if (n < 0 || (ld_acq(o + 2) & 0xFFu) == 18u) return;   // the frame stops at this block
+                xs.update(B.hOut + (uint64_t)(h % Rout) * bm, (size_t)n);
+                hashed.store(h + 1, std::memory_order_release);
+            }
+        });
+    }
+    std::thread writer([&] {
+        for (uint32_t b = 0;; ++b) {
+            uint32_t* o = outC + 4ull * (b % Rout);
+            const bool ok = host_wait([&] { return ld_acq(o) == b + 1 || b >= total.load(); }, stopped);
+            if (!ok || (b >= total.load() && ld_acq(o) != b + 1)) {
+                if (!ok) wfail = true;
+                return;
+            }
+            const int32_t n = (int32_t)ld_acq(o + 1);
+            const uint32_t st = ld_acq(o + 2);
+            if ((st & 0xFFu) == 18u || n < 0) {   // decode failure: stop before writing the block
+                s.quit(LZ4MT_RESULT_DECOMPRESS_FAIL);
+                st_rel(g + 1, 1u);
+                return;
+            }
+            if (sck && !host_wait([&] { return hashed.load(std::memory_order_acquire) > b; }, stopped)) {
+                wfail = true;
+                return;
+            }
+            if (!s.write(B.hOut + (uint64_t)(b % Rout) * bm, n)) {
+                s.quit((st & 0x100u) ? LZ4MT_RESULT_CANNOT_WRITE_DATA_BLOCK : LZ4MT_RESULT_CANNOT_WRITE_DECODED_BLOCK);
+                st_rel(g + 1, 1u);
+                return;
+            }
+            if (st & 16u) {   // checksum mismatch: after the block is written
+                s.quit(LZ4MT_RESULT_BLOCK_CHECKSUM_MISMATCH);
+                st_rel(g + 1, 1u);
+                return;
+            }
+            st_rel(o + 3, b + 1);   // the slot may take block b + Rout
+            st_rel(g + 3, b + 1);   // heartbeat
+        }
+    });
+    // the reader: every read on this thread (the batch engine's record checks)
+    bool eos = false;
+    Lz4MtResult pending = LZ4MT_RESULT_OK;
+    uint32_t b = 0;
+    for (;; ++b) {
+        uint32_t* ic = inC + 4ull * (b % Rin);
+        if (b >= Rin && !host_wait([&] { return ld_acq(ic + 3) == b - Rin + 1; }, stopped)) break;
+        if (stopped() || s.quitting()) break;
+        if (s.readEof()) break;
+        uint32_t bits = 0;
+        if (!s.peekU32(&bits)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_SIZE; break; }
+        if (bits == 0) { eos = true; break; }
+        const uint32_t n = bits & ~kRawBit;
+        if (n > bm) { pending = LZ4MT_RESULT_INVALID_BLOCK_SIZE; break; }
+        if (s.read(B.hIn + (uint64_t)(b % Rin) * bm, (int)n) != (int)n) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_DATA; break; }
+        uint32_t ck = 0;
+        if (bck && !s.peekU32(&ck)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_CHECKSUM; break; }
+        st_rel(ic + 1, bits);
+        st_rel(ic + 2, ck);
+        st_rel(ic, b + 1);
+        st_rel(g + 2, b + 1);   // heartbeat
+    }
+    total = b;
+    st_rel(g, b);   // waves waiting for a block >= b leave
+    writer.join();
+    if (hasher.joinable()) {
+        if (s.error() || s.quitting() || wfail) st_rel(g + 1, 1u);
+        hasher.join();
+    }
+    if (wfail || gpuFailed()) st_rel(g + 1, 1u);
+    const hipError_t e = hipStreamSynchronize(B.st);
+    if (e != hipSuccess || gpuFailed() || (wfail && !s.error())) s.quit(LZ4MT_RESULT_ERROR);
+    if (!(s.mode() & LZ4MT_MODE_DEVICE)) B.release();
+    if (pending != LZ4MT_RESULT_OK && !s.error()) s.quit(pending);
+    return eos;
+}
+
+bool stream_eligible_dec(const Lz4MtStreamDescriptor* sd) {
+    const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
+    return stream_enabled() && sd->flg.blockIndependence && bm >= (1u << 20) && bm <= (4u << 20);
+}
+
+// ---------------------------------------------------------------------------
 // decompress: DEVICE batch engine (the same slot pipeline as compress)
 // ---------------------------------------------------------------------------
 bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
     if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return false; }
+    if (stream_eligible_dec(sd)) return decompress_streamed(s, sd, xs);
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
     // Block-dependent frames (decompressBlockDependency, src/lz4mt.cpp:

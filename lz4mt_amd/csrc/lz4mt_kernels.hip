@@ -3535,6 +3535,93 @@ hipError_t launch_encode_stream(const uint8_t* hin, uint8_t* hout, uint32_t* inC
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Streamed decompress: the mirror of the streamed compress above for
+// lz4mtDecompress over the callbacks (independent 1 / 4 MiB blocks;
+// reference decompress(), src/lz4mt.cpp:593-734).  The host reads each
+// record (size word, stored bytes, block checksum) into in[b % Rin]; a wave
+// takes block b, copies the stored bytes to HBM, frees the slot, hashes them
+// (block XXH32) when the frame carries block checksums, decodes them with
+// the frame decoder's code (LZ4_decompress_safe, cap = blockMax) or takes a
+// raw block as is, waits for out[b % Rout] and pushes the decoded bytes
+// there; a host writer thread writes them in block order.
+//   in[r]  {seq = b + 1, size word, XXH32 from the frame, pulled = b + 1}
+//   out[r] {seq = b + 1, decoded bytes or the decoder's negative result,
+//           status (16 checksum mismatch, 18 decode failure, | 0x100 raw),
+//           written = b + 1}
+// Control words and waits as in k_encode_stream (g[2] heartbeat = records read).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_decode_stream(const uint8_t* __restrict__ hin, uint8_t* __restrict__ hout,
+                                                      uint32_t* inCtl, uint32_t* outCtl, uint32_t* g,
+                                                      uint32_t* __restrict__ next, uint8_t* __restrict__ dIn,
+                                                      uint8_t* __restrict__ dSlot, uint32_t bm, uint32_t Rin,
+                                                      uint32_t Rout, int bck) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kWinAlloc];   /* + dummy write area + hop table */
+    const uint32_t L = laneid();
+    g_u8* din = gptr(dIn) + (uint64_t)blockIdx.x * (bm + 64);
+    g_u8* dsl = gptr(dSlot) + (uint64_t)blockIdx.x * (bm + 64);
+    for (;;) {
+        uint32_t b = 0;
+        if (L == 0) b = atomicAdd(next, 1u);
+        b = rdlane(b, 0);
+        const uint32_t ri = b % Rin, ro = b % Rout;
+        bool ended = false;
+        if (!stream_wait(inCtl + 4 * ri, b + 1, g, 2, b + 1, (int64_t)b, &ended)) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        const uint32_t bits = ld_sys(inCtl + 4 * ri + 1), ck = ld_sys(inCtl + 4 * ri + 2);
+        const uint32_t n = min(bits & 0x7FFFFFFFu, bm);   // (the host refuses n > bm)
+        const bool raw = (bits & 0x80000000u) != 0;
+        wave_copy16(din, gptr(hin) + (uint64_t)ri * bm, n);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (L == 0) st_sys(inCtl + 4 * ri + 3, b + 1);   // the staging slot may be refilled
+        uint32_t status = raw ? 0x100u : 0u;
+        if (bck && xxh32_wave(din, n, (l_u32*)ring) != ck) status |= 16u;
+        WAVE_SYNC();
+        int32_t res = (int32_t)n;
+        g_cu8* outp = din;
+        if (!raw) {
+            Dec<false> D;
+            D.acc = nullptr;
+            D.ts = 0;
+            D.src = din;
+            D.len = n;
+            D.dst = dsl;
+            D.physcap = bm;
+            D.ring = (l_u8*)ring;
+            D.win = (l_u8*)win;
+            D.wlo = INT64_MIN / 4;
+            D.labase = INT64_MIN / 4;
+            D.la = 0;
+            D.flushed = 0;
+            D.completed = 0;
+            D.lowP = 0;
+            res = decode_block(D, (int64_t)bm);   // cap = blockMax (src/lz4mt.cpp:645)
+            outp = dsl;
+            if (res < 0) status = 18u;   // a decode failure wins over the checksum (src/lz4mt.cpp:619-681)
+        }
+        if (b >= Rout && !stream_wait(outCtl + 4 * ro + 3, b - Rout + 1, g, 3, b - Rout + 1, -1, &ended)) return;
+        if (res > 0) wave_copy16(gptr(hout) + (uint64_t)ro * bm, outp, (uint32_t)res);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (L == 0) {
+            st_sys(outCtl + 4 * ro + 1, (uint32_t)res);
+            st_sys(outCtl + 4 * ro + 2, status);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (L == 0) st_sys(outCtl + 4 * ro, b + 1);
+    }
+}
+
+hipError_t launch_decode_stream(const uint8_t* hin, uint8_t* hout, uint32_t* inCtl, uint32_t* outCtl, uint32_t* g,
+                                uint32_t* next, uint8_t* dIn, uint8_t* dSlot, uint32_t bm, uint32_t Rin,
+                                uint32_t Rout, uint32_t waves, int bck, hipStream_t st) {
+    if (bm < 64 || (bm & 15) || !waves || !Rin || !Rout) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_decode_stream, dim3(waves), dim3(64), 0, st, hin, hout, inCtl, outCtl, g, next, dIn, dSlot,
+                       bm, Rin, Rout, bck);
+    return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(64) k_xxh32_frame_blocks(const uint8_t* __restrict__ frame,
                                                            const BlockRec* __restrict__ recs, uint32_t nBlocks,
                                                            uint32_t* __restrict__ digest) {

@@ -170,3 +170,112 @@ def test_streamed_write_failure_drains():
     assert want.startswith(frame) and len(frame) > 7
     r, frame, _ = _callbacks(data, sd)
     assert r == 0 and frame == want
+
+
+# ---------------------------------------------------------------------------
+# The streamed decompress (k_decode_stream): lz4mtDecompress in MODE_DEVICE
+# (and PARALLEL with a null decompress callback) over independent 1 / 4 MiB
+# blocks decodes each record as soon as it is read; same bytes and result
+# codes as the batch engine (LZ4MT_AMD_STREAM=0) and the oracle.
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("row", sorted(APP_F))
+def test_streamed_decompress_known_answers(data256, row):
+    sck, bck, bid = row
+    frame = oracle.compress_frame(data256[:64 << 20], oracle.params(bid, bool(sck), bool(bck)))
+    for m in (L.MODE_DEVICE, L.MODE_PARALLEL):
+        r, out, sd = L.decompress(frame, (64 << 20) + 64, mode=m)
+        assert r == 0, (row, m, L.result_to_string(r))
+        assert out == data256[:64 << 20], (row, m)
+
+
+@pytest.mark.parametrize("rin,rout", [(8, 8), (9, 64), (256, 11)])
+def test_streamed_decompress_tight_rings(data256, monkeypatch, rin, rout):
+    monkeypatch.setenv("LZ4MT_AMD_STREAM_IN", str(rin))
+    monkeypatch.setenv("LZ4MT_AMD_STREAM_OUT", str(rout))
+    for row in ((0, 1, 6), (1, 1, 7)):
+        sck, bck, bid = row
+        frame = oracle.compress_frame(data256[:48 << 20], oracle.params(bid, bool(sck), bool(bck)))
+        r, out, _ = L.decompress(frame, (48 << 20) + 64, mode=L.MODE_DEVICE)
+        assert r == 0 and out == data256[:48 << 20], (rin, rout, row)
+
+
+def _damaged_frames(seed):
+    """Frames with raw and compressed blocks (1 MiB), then damaged: a flipped
+    byte in a compressed block, in a raw block, in a block checksum, in the
+    stream checksum; a size word past blockMax; truncations inside a size
+    word, a block and a checksum; a missing EOS."""
+    rnd = random.Random(seed)
+    data = bytearray(oracle.gen_synthetic(9 << 20, seed))
+    data[3 << 20:(3 << 20) + 900_000] = oracle.gen_random(900_000, seed)   # an incompressible stretch: raw blocks
+    data = bytes(data)
+    out = []
+    for sck, bck in ((True, True), (False, True), (True, False)):
+        f = oracle.compress_frame(data, oracle.params(6, sck, bck))
+        out.append(("intact", sck, bck, f))
+        recs, pos = [], 7
+        while True:   # walk the records
+            w = struct.unpack_from("<I", f, pos)[0]
+            if w == 0:
+                break
+            n = w & 0x7FFFFFFF
+            recs.append((pos, w, n))
+            pos += 4 + n + (4 if bck else 0)
+        comp = [r_ for r_ in recs if not r_[1] & 0x80000000]
+        raw = [r_ for r_ in recs if r_[1] & 0x80000000]
+        p0, _, n0 = comp[rnd.randrange(len(comp))]
+        g = bytearray(f)
+        g[p0 + 4 + rnd.randrange(n0)] ^= 0x5A
+        out.append(("flip-compressed", sck, bck, bytes(g)))
+        if raw:
+            p1, _, n1 = raw[0]
+            g = bytearray(f)
+            g[p1 + 4 + n1 // 2] ^= 1
+            out.append(("flip-raw", sck, bck, bytes(g)))
+        if bck:
+            g = bytearray(f)
+            g[p0 + 4 + n0] ^= 1
+            out.append(("flip-checksum", sck, bck, bytes(g)))
+        if sck:
+            g = bytearray(f)
+            g[-1] ^= 1
+            out.append(("flip-stream-checksum", sck, bck, bytes(g)))
+        g = bytearray(f)
+        struct.pack_into("<I", g, recs[2][0], (1 << 20) + 1)
+        out.append(("size-past-blockmax", sck, bck, bytes(g)))
+        out.append(("cut-size-word", sck, bck, f[:recs[3][0] + 2]))
+        out.append(("cut-block", sck, bck, f[:recs[3][0] + 4 + recs[3][2] // 2]))
+        if bck:
+            out.append(("cut-checksum", sck, bck, f[:recs[3][0] + 4 + recs[3][2] + 2]))
+        out.append(("no-eos", sck, bck, f[:pos]))
+    return data, out
+
+
+def test_streamed_decompress_damaged_frames_match_batch_engine(monkeypatch):
+    """Every damaged frame gives the batch engine's result code and the same
+    bytes written before the error, in MODE_DEVICE."""
+    data, frames = _damaged_frames(11)
+    for label, sck, bck, f in frames:
+        r1, o1, _ = L.decompress(f, len(data) + 64, mode=L.MODE_DEVICE)
+        monkeypatch.setenv("LZ4MT_AMD_STREAM", "0")
+        r2, o2, _ = L.decompress(f, len(data) + 64, mode=L.MODE_DEVICE)
+        monkeypatch.delenv("LZ4MT_AMD_STREAM")
+        assert (r1, o1) == (r2, o2), (label, sck, bck, L.result_to_string(r1), L.result_to_string(r2))
+        if label == "intact":
+            assert r1 == 0 and o1 == data
+
+
+def test_streamed_decompress_concatenated_and_after_error():
+    """Two frames back to back decode as one stream; a failing call leaves
+    the grid drained (the next call works)."""
+    a = oracle.gen_synthetic(6 << 20, 1)
+    b = oracle.gen_synthetic(5 << 20, 2)
+    fa = oracle.compress_frame(a, oracle.params(6, True, True))
+    fb = oracle.compress_frame(b, oracle.params(7, False, True))
+    r, out, _ = L.decompress(fa + fb, len(a) + len(b) + 64, mode=L.MODE_DEVICE)
+    assert r == 0 and out == a + b
+    bad = bytearray(fa)
+    bad[7 + 4 + 100] ^= 0xFF
+    r, _, _ = L.decompress(bytes(bad), len(a) + 64, mode=L.MODE_DEVICE)
+    assert r != 0
+    r, out, _ = L.decompress(fb, len(b) + 64, mode=L.MODE_DEVICE)
+    assert r == 0 and out == b
