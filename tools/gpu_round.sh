@@ -71,7 +71,7 @@ for step in "$@"; do
         timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -T -f csv -d "$out/bid$bid/write_appf" -o write -- \
             python3 tools/kprof.py 8 --bid=$bid > "$out/bid$bid/write.log" 2>&1
       done ;;
-    e2ems)   # end-to-end memory path, streamed compress (default) and the batch engine (LZ4MT_AMD_STREAM=0)
+    e2ems)   # end-to-end memory path, the streamed engines (default) and the batch engine (LZ4MT_AMD_STREAM=0)
       timeout -k 10 300 python3 tools/e2e.py 8 7 > "$out/e2e_mem_stream.txt" 2>&1 || { tail -20 "$out/e2e_mem_stream.txt"; exit 1; }
       LZ4MT_AMD_STREAM=0 timeout -k 10 300 python3 tools/e2e.py 8 7 > "$out/e2e_mem_batch.txt" 2>&1 \
           || { tail -20 "$out/e2e_mem_batch.txt"; exit 1; }
