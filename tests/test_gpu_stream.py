@@ -279,3 +279,38 @@ def test_streamed_decompress_concatenated_and_after_error():
     assert r != 0
     r, out, _ = L.decompress(fb, len(b) + 64, mode=L.MODE_DEVICE)
     assert r == 0 and out == b
+
+
+def test_streamed_decompress_random_frames_vs_batch_engine(monkeypatch):
+    """40 random frames (1 / 4 MiB blocks, every flag combination, sizes up to
+    20 MiB with raw stretches and zero runs), a third of them damaged at a
+    random byte or cut at a random length: the streamed decompress gives the
+    batch engine's result code and bytes, and the oracle's bytes when intact."""
+    rnd = random.Random(2024)
+    for case in range(40):
+        bid = rnd.choice((6, 7))
+        sck, bck, ssz = rnd.random() < 0.5, rnd.random() < 0.5, rnd.random() < 0.3
+        n = rnd.randrange(1, 20 << 20)
+        data = bytearray(oracle.gen_synthetic(n, case))
+        if n > 4 << 20 and rnd.random() < 0.5:
+            z = rnd.randrange(n - (2 << 20))
+            data[z:z + (1 << 20)] = oracle.gen_random(1 << 20, case)
+        if n > 1 << 20 and rnd.random() < 0.3:
+            z = rnd.randrange(n - (1 << 20))
+            data[z:z + (1 << 20)] = bytes(1 << 20)
+        data = bytes(data)
+        f = oracle.compress_frame(data, oracle.params(bid, sck, bck, n if ssz else None))
+        kind = rnd.random()
+        if kind < 0.17:
+            g = bytearray(f)
+            g[rnd.randrange(7, len(g))] ^= 1 << rnd.randrange(8)
+            f = bytes(g)
+        elif kind < 0.33:
+            f = f[:rnd.randrange(7, len(f))]
+        r1, o1, _ = L.decompress(f, n + 64, mode=L.MODE_DEVICE)
+        monkeypatch.setenv("LZ4MT_AMD_STREAM", "0")
+        r2, o2, _ = L.decompress(f, n + 64, mode=L.MODE_DEVICE)
+        monkeypatch.delenv("LZ4MT_AMD_STREAM")
+        assert (r1, o1) == (r2, o2), (case, bid, sck, bck, ssz, n, kind, L.result_to_string(r1), L.result_to_string(r2))
+        if kind >= 0.33:
+            assert r1 == 0 and o1 == data, (case, L.result_to_string(r1))
