@@ -602,6 +602,43 @@ bool host_wait(P pred, Q stop) {
     }
 }
 
+// A wave of the streamed grids gives up a wait after LZ4MT_AMD_STREAM_TIMEOUT_S
+// seconds without progress (so a stuck host never pins the GPU); waiting on the
+// user's read() / write() is progress: while any callback runs, a keepalive
+// thread bumps the liveness word g[5] every 100 ms (a stalled pipe upstream
+// or downstream is not a hang).
+uint64_t stream_wait_ticks() {
+    return (uint64_t)env_int("LZ4MT_AMD_STREAM_TIMEOUT_S", 60, 1, 86400) * 100000000ull;   // 100 MHz
+}
+class Keepalive {
+  public:
+    explicit Keepalive(uint32_t* live) : live_(live), th_([this] { run(); }) {}
+    ~Keepalive() {
+        { std::lock_guard<std::mutex> lk(mu_); stop_ = true; }
+        cv_.notify_all();
+        th_.join();
+    }
+    // one callback in progress for the scope's lifetime
+    struct Scope {
+        Keepalive& k;
+        explicit Scope(Keepalive& k_) : k(k_) { k.busy_.fetch_add(1, std::memory_order_relaxed); }
+        ~Scope() { k.busy_.fetch_sub(1, std::memory_order_relaxed); }
+    };
+
+  private:
+    void run() {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (uint32_t beat = 1; !cv_.wait_for(lk, std::chrono::milliseconds(100), [this] { return stop_; });)
+            if (busy_.load(std::memory_order_relaxed) > 0) __atomic_store_n(live_, beat++, __ATOMIC_RELEASE);
+    }
+    uint32_t* live_;
+    std::atomic<int> busy_{0};
+    std::mutex mu_;
+    std::condition_variable cv_;
+    bool stop_ = false;
+    std::thread th_;   // last: started once the members above exist
+};
+
 bool stream_eligible(const Session& s, const Lz4MtStreamDescriptor* sd) {
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     return stream_enabled() && sd->flg.blockIndependence && s.level() < 3 && bm >= (1u << 20) && bm <= (4u << 20);
@@ -631,7 +668,7 @@ void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
     std::atomic_thread_fence(std::memory_order_seq_cst);
     if (hipMemsetAsync(B.dNext, 0, 4, B.st) != hipSuccess ||
         launch_encode_stream(B.hIn, B.hOut, inC, outC, g, B.dNext, B.dIn, B.dSlot, bm, Rin, Rout, waves, bck ? 1 : 0,
-                             B.st) != hipSuccess) {
+                             stream_wait_ticks(), B.st) != hipSuccess) {
         (void)hipGetLastError();
         s.quit(LZ4MT_RESULT_ERROR);
         return;
@@ -639,6 +676,7 @@ void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
     std::atomic<uint32_t> total{0xFFFFFFFFu};   // blocks in the stream, once known
     std::atomic<bool> wfail{false};
     auto gpuFailed = [&] { return ld_acq(g + 4) != 0; };
+    Keepalive ka(g + 5);
     std::thread writer([&] {
         for (uint32_t b = 0;; ++b) {
             uint32_t* o = outC + 4ull * (b % Rout);
@@ -650,7 +688,12 @@ void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
             }
             const uint32_t word = ld_acq(o + 1), len = word & ~kRawBit, sum = ld_acq(o + 2);
             const uint8_t* payload = B.hOut + (uint64_t)(b % Rout) * bm;
-            if (!s.writeU32(word) || !s.write(payload, (int)len) || (bck && !s.writeU32(sum))) {
+            bool wok;
+            {
+                Keepalive::Scope cb(ka);
+                wok = s.writeU32(word) && s.write(payload, (int)len) && (!bck || s.writeU32(sum));
+            }
+            if (!wok) {
                 wfail = true;
                 st_rel(g + 1, 1u);   // abort: the grid and the reader stop
                 return;
@@ -688,7 +731,11 @@ void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
             break;
         if (ld_acq(g + 1) != 0 || gpuFailed()) break;   // the writer or the grid stopped
         uint8_t* dst = B.hIn + (uint64_t)(b % Rin) * bm;
-        const int n = s.read(dst, (int)bm);
+        int n;
+        {
+            Keepalive::Scope cb(ka);
+            n = s.read(dst, (int)bm);
+        }
         if (n <= 0) break;
         st_rel(ic + 1, (uint32_t)n);
         st_rel(ic, b + 1);
@@ -925,7 +972,7 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
     std::atomic_thread_fence(std::memory_order_seq_cst);
     if (hipMemsetAsync(B.dNext, 0, 4, B.st) != hipSuccess ||
         launch_decode_stream(B.hIn, B.hOut, inC, outC, g, B.dNext, B.dIn, B.dSlot, bm, Rin, Rout, waves, bck ? 1 : 0,
-                             B.st) != hipSuccess) {
+                             stream_wait_ticks(), B.st) != hipSuccess) {
         (void)hipGetLastError();
         s.quit(LZ4MT_RESULT_ERROR);
         return false;
@@ -935,6 +982,7 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
     std::atomic<uint32_t> hashed{0};
     auto gpuFailed = [&] { return ld_acq(g + 4) != 0; };
     auto stopped = [&] { return gpuFailed() || ld_acq(g + 1) != 0; };
+    Keepalive ka(g + 5);
     // the content checksum over the decoded blocks, in order, beside the writer
     std::thread hasher;
     if (sck) {
@@ -969,7 +1017,12 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
                 wfail = true;
                 return;
             }
-            if (!s.write(B.hOut + (uint64_t)(b % Rout) * bm, n)) {
+            bool wok;
+            {
+                Keepalive::Scope cb(ka);
+                wok = s.write(B.hOut + (uint64_t)(b % Rout) * bm, n);
+            }
+            if (!wok) {
                 s.quit((st & 0x100u) ? LZ4MT_RESULT_CANNOT_WRITE_DATA_BLOCK : LZ4MT_RESULT_CANNOT_WRITE_DECODED_BLOCK);
                 st_rel(g + 1, 1u);
                 return;
@@ -991,6 +1044,7 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
         uint32_t* ic = inC + 4ull * (b % Rin);
         if (b >= Rin && !host_wait([&] { return ld_acq(ic + 3) == b - Rin + 1; }, stopped)) break;
         if (stopped() || s.quitting()) break;
+        Keepalive::Scope cb(ka);   // the record's read() calls
         if (s.readEof()) break;
         uint32_t bits = 0;
         if (!s.peekU32(&bits)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_SIZE; break; }

@@ -3418,13 +3418,16 @@ __global__ void __launch_bounds__(64) k_xxh32_stored(const uint8_t* __restrict__
 //     and publishes size word, checksum and b + 1;
 //   * a host writer thread calls write() record by record in block order as
 //     they appear.
-// Every wait gives up after kStreamWaitTicks without progress of the other
-// side (a heartbeat word), so the grid always drains; the host sets the
-// block count once read() returns 0 and every wave still waiting leaves.
+// Every wait gives up after `ticks` (LZ4MT_AMD_STREAM_TIMEOUT_S, 60 s by
+// default) without progress of the other side -- its heartbeat word, or the
+// host's liveness word, which a host thread bumps while a read() / write()
+// callback is running (a slow pipe is not a hang) -- so the grid always
+// drains; the host sets the block count once read() returns 0 and every wave
+// still waiting leaves.
 // Control words (u32, coherent pinned host memory):
 //   g[0] blocks in the stream (0xFFFFFFFF until known)  g[1] abort (host)
 //   g[2] blocks read (heartbeat)  g[3] records written (heartbeat)
-//   g[4] error (GPU: a wait timed out)
+//   g[4] error (GPU: a wait timed out)  g[5] host liveness (inside a callback)
 //   in[r]  {seq = b + 1, length, pulled = b + 1}   (4 words per slot)
 //   out[r] {seq = b + 1, size word, XXH32, written = b + 1}
 // A waiting wave sleeps in proportion to how far the awaited heartbeat is
@@ -3432,7 +3435,6 @@ __global__ void __launch_bounds__(64) k_xxh32_stored(const uint8_t* __restrict__
 // waves waiting for blocks far ahead of the reader cost the PCIe link only a
 // few hundred thousand small reads per second.
 // ---------------------------------------------------------------------------
-constexpr uint64_t kStreamWaitTicks = 60ull * 100000000ull;   // s_memrealtime: 100 MHz -> 60 s
 __device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -3455,20 +3457,21 @@ __device__ __forceinline__ void wave_copy16(g_u8* d, g_cu8* s, uint32_t n) {
 }
 // Waits until *w == want.  hb: the heartbeat (2 = blocks read, 3 = records
 // written) that reaches `target` when *w is about to change.  false on
-// abort, on a timeout (g[4] set), or -- endAt >= 0 -- once the stream is
-// known to hold no block endAt (*ended).
+// abort, on a timeout (`ticks` of s_memrealtime, 100 MHz, without a change of
+// the heartbeat or of the host's liveness word g[5]; g[4] set), or --
+// endAt >= 0 -- once the stream is known to hold no block endAt (*ended).
 __device__ __forceinline__ bool stream_wait(const uint32_t* w, uint32_t want, uint32_t* g, uint32_t hb,
-                                            uint32_t target, int64_t endAt, bool* ended) {
+                                            uint32_t target, int64_t endAt, bool* ended, uint64_t ticks) {
     uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t beat = ld_sys(g + hb);
+    uint32_t beat = ld_sys(g + hb), alive = ld_sys(g + 5);
     for (;;) {
         if (ld_sys(w) == want) return true;
-        const uint32_t total = ld_sys(g), abort = ld_sys(g + 1), now = ld_sys(g + hb);
+        const uint32_t total = ld_sys(g), abort = ld_sys(g + 1), now = ld_sys(g + hb), live = ld_sys(g + 5);
         if (endAt >= 0 && (uint64_t)endAt >= total) { *ended = true; return false; }
         if (abort) return false;
         const uint64_t t = __builtin_amdgcn_s_memrealtime();
-        if (now != beat) { beat = now; t0 = t; }
-        else if (t - t0 > kStreamWaitTicks) {
+        if (now != beat || live != alive) { beat = now; alive = live; t0 = t; }
+        else if (t - t0 > ticks) {
             if (laneid() == 0) st_sys(g + 4, 1u);
             return false;
         }
@@ -3482,7 +3485,7 @@ __global__ void __launch_bounds__(64) k_encode_stream(const uint8_t* __restrict_
                                                       uint32_t* inCtl, uint32_t* outCtl, uint32_t* g,
                                                       uint32_t* __restrict__ next, uint8_t* __restrict__ dIn,
                                                       uint8_t* __restrict__ dSlot, uint32_t bm, uint32_t Rin,
-                                                      uint32_t Rout, int bck) {
+                                                      uint32_t Rout, int bck, uint64_t ticks) {
     ENCODE_LDS
     const uint32_t L = laneid();
     g_u8* din = gptr(dIn) + (uint64_t)blockIdx.x * (bm + 64);
@@ -3493,7 +3496,7 @@ __global__ void __launch_bounds__(64) k_encode_stream(const uint8_t* __restrict_
         b = rdlane(b, 0);
         const uint32_t ri = b % Rin, ro = b % Rout;
         bool ended = false;
-        if (!stream_wait(inCtl + 4 * ri, b + 1, g, 2, b + 1, (int64_t)b, &ended)) return;
+        if (!stream_wait(inCtl + 4 * ri, b + 1, g, 2, b + 1, (int64_t)b, &ended, ticks)) return;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const uint32_t n = ld_sys(inCtl + 4 * ri + 1);
         wave_copy16(din, gptr(hin) + (uint64_t)ri * bm, n);
@@ -3511,7 +3514,7 @@ __global__ void __launch_bounds__(64) k_encode_stream(const uint8_t* __restrict_
         const uint32_t sl = r > 0 ? (uint32_t)r : n;
         const uint32_t sum = bck ? xxh32_wave(stored, sl, (l_u32*)T) : 0u;
         // the record's slot in host memory: free once the writer wrote block b - Rout
-        if (b >= Rout && !stream_wait(outCtl + 4 * ro + 3, b - Rout + 1, g, 3, b - Rout + 1, -1, &ended)) return;
+        if (b >= Rout && !stream_wait(outCtl + 4 * ro + 3, b - Rout + 1, g, 3, b - Rout + 1, -1, &ended, ticks)) return;
         wave_copy16(gptr(hout) + (uint64_t)ro * bm, stored, sl);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -3526,12 +3529,12 @@ __global__ void __launch_bounds__(64) k_encode_stream(const uint8_t* __restrict_
 
 hipError_t launch_encode_stream(const uint8_t* hin, uint8_t* hout, uint32_t* inCtl, uint32_t* outCtl, uint32_t* g,
                                 uint32_t* next, uint8_t* dIn, uint8_t* dSlot, uint32_t bm, uint32_t Rin,
-                                uint32_t Rout, uint32_t waves, int bck, hipStream_t st) {
+                                uint32_t Rout, uint32_t waves, int bck, uint64_t ticks, hipStream_t st) {
     bool xc = true;
     if (const hipError_t r = encoder_path(st, &xc); r != hipSuccess) return r;
     if (bm < (uint32_t)kLimit64K || bm > (1u << kPosBits) || !waves || !Rin || !Rout) return hipErrorInvalidValue;
     hipLaunchKernelGGL(xc ? k_encode_stream<true> : k_encode_stream<false>, dim3(waves), dim3(64), 0, st, hin, hout,
-                       inCtl, outCtl, g, next, dIn, dSlot, bm, Rin, Rout, bck);
+                       inCtl, outCtl, g, next, dIn, dSlot, bm, Rin, Rout, bck, ticks);
     return hipGetLastError();
 }
 
@@ -3555,7 +3558,7 @@ __global__ void __launch_bounds__(64) k_decode_stream(const uint8_t* __restrict_
                                                       uint32_t* inCtl, uint32_t* outCtl, uint32_t* g,
                                                       uint32_t* __restrict__ next, uint8_t* __restrict__ dIn,
                                                       uint8_t* __restrict__ dSlot, uint32_t bm, uint32_t Rin,
-                                                      uint32_t Rout, int bck) {
+                                                      uint32_t Rout, int bck, uint64_t ticks) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
     __shared__ __attribute__((aligned(16))) uint8_t win[kWinAlloc];   /* + dummy write area + hop table */
     const uint32_t L = laneid();
@@ -3567,7 +3570,7 @@ __global__ void __launch_bounds__(64) k_decode_stream(const uint8_t* __restrict_
         b = rdlane(b, 0);
         const uint32_t ri = b % Rin, ro = b % Rout;
         bool ended = false;
-        if (!stream_wait(inCtl + 4 * ri, b + 1, g, 2, b + 1, (int64_t)b, &ended)) return;
+        if (!stream_wait(inCtl + 4 * ri, b + 1, g, 2, b + 1, (int64_t)b, &ended, ticks)) return;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const uint32_t bits = ld_sys(inCtl + 4 * ri + 1), ck = ld_sys(inCtl + 4 * ri + 2);
         const uint32_t n = min(bits & 0x7FFFFFFFu, bm);   // (the host refuses n > bm)
@@ -3600,7 +3603,7 @@ __global__ void __launch_bounds__(64) k_decode_stream(const uint8_t* __restrict_
             outp = dsl;
             if (res < 0) status = 18u;   // a decode failure wins over the checksum (src/lz4mt.cpp:619-681)
         }
-        if (b >= Rout && !stream_wait(outCtl + 4 * ro + 3, b - Rout + 1, g, 3, b - Rout + 1, -1, &ended)) return;
+        if (b >= Rout && !stream_wait(outCtl + 4 * ro + 3, b - Rout + 1, g, 3, b - Rout + 1, -1, &ended, ticks)) return;
         if (res > 0) wave_copy16(gptr(hout) + (uint64_t)ro * bm, outp, (uint32_t)res);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -3615,10 +3618,10 @@ __global__ void __launch_bounds__(64) k_decode_stream(const uint8_t* __restrict_
 
 hipError_t launch_decode_stream(const uint8_t* hin, uint8_t* hout, uint32_t* inCtl, uint32_t* outCtl, uint32_t* g,
                                 uint32_t* next, uint8_t* dIn, uint8_t* dSlot, uint32_t bm, uint32_t Rin,
-                                uint32_t Rout, uint32_t waves, int bck, hipStream_t st) {
+                                uint32_t Rout, uint32_t waves, int bck, uint64_t ticks, hipStream_t st) {
     if (bm < 64 || (bm & 15) || !waves || !Rin || !Rout) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_decode_stream, dim3(waves), dim3(64), 0, st, hin, hout, inCtl, outCtl, g, next, dIn, dSlot,
-                       bm, Rin, Rout, bck);
+                       bm, Rin, Rout, bck, ticks);
     return hipGetLastError();
 }
 

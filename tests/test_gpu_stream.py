@@ -314,3 +314,56 @@ def test_streamed_decompress_random_frames_vs_batch_engine(monkeypatch):
         assert (r1, o1) == (r2, o2), (case, bid, sck, bck, ssz, n, kind, L.result_to_string(r1), L.result_to_string(r2))
         if kind >= 0.33:
             assert r1 == 0 and o1 == data, (case, L.result_to_string(r1))
+
+
+def _slow_io(fn, data, sd, mode, slow_read=None, slow_write=None, delay=2.5):
+    """lz4mtCompress / lz4mtDecompress with Python callbacks, one of which
+    blocks for `delay` seconds at its slow_read-th / slow_write-th call (a
+    stalled pipe upstream or downstream)."""
+    import time
+    from lz4mt_amd import _abi
+    src = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+    st = {"pos": 0, "r": 0, "w": 0}
+    out = []
+
+    def rd(ctx, dst, n):
+        st["r"] += 1
+        if st["r"] == slow_read:
+            time.sleep(delay)
+        k = min(n, len(data) - st["pos"])
+        ctypes.memmove(dst, ctypes.addressof(src) + st["pos"], k)
+        st["pos"] += k
+        return k
+
+    def wr(ctx, p, n):
+        st["w"] += 1
+        if st["w"] == slow_write:
+            time.sleep(delay)
+        out.append(ctypes.string_at(p, n))
+        return n
+
+    keep = [_abi.READ_FN(rd), _abi.WRITE_FN(wr)]
+    ctx = L.init_context()
+    ctx.mode = mode
+    ctx.read = ctypes.cast(keep[0], ctypes.c_void_p)
+    ctx.write = ctypes.cast(keep[1], ctypes.c_void_p)
+    r = fn(ctypes.byref(ctx), ctypes.byref(sd))
+    return r, b"".join(out)
+
+
+def test_streamed_slow_callbacks_are_not_a_timeout(monkeypatch):
+    """With the grids' wait limit at 1 s (LZ4MT_AMD_STREAM_TIMEOUT_S), a read()
+    or write() that blocks 2.5 s (the whole grid waiting on it) still ends in
+    the right frame / bytes: time inside a callback is progress (the
+    keepalive word), only a host that stops without being in one times out."""
+    monkeypatch.setenv("LZ4MT_AMD_STREAM_TIMEOUT_S", "1")
+    monkeypatch.setenv("LZ4MT_AMD_STREAM_IN", "8")
+    monkeypatch.setenv("LZ4MT_AMD_STREAM_OUT", "8")
+    data = oracle.gen_synthetic(24 << 20, 4)
+    want = oracle.compress_frame(data, oracle.params(6, True, True))
+    for slow in ({"slow_read": 3}, {"slow_write": 12}):
+        r, frame = _slow_io(L.lib.lz4mtCompress, data, L.make_sd(6, True, True), L.MODE_DEVICE, **slow)
+        assert r == 0 and frame == want, (slow, L.result_to_string(r))
+    for slow in ({"slow_read": 9}, {"slow_write": 4}):
+        r, out = _slow_io(L.lib.lz4mtDecompress, want, L.init_stream_descriptor(), L.MODE_DEVICE, **slow)
+        assert r == 0 and out == data, (slow, L.result_to_string(r))
