@@ -558,12 +558,18 @@ struct StreamBufs {
     uint32_t bm = 0, waves = 0, Rin = 0, Rout = 0;
     hipStream_t st = nullptr;
     int dev = -1;
+    // (DEVICE-mode calls keep the rings per thread; a thread's exit frees them)
+    ~StreamBufs() { release(); }
     void release() {
         if (st) hipStreamSynchronize(st);
         hipHostFree(hIn); hipHostFree(hOut); hipHostFree(hCtl);
         hipFree(dIn); hipFree(dSlot); hipFree(dNext);
         if (st) hipStreamDestroy(st);
-        *this = StreamBufs();
+        hIn = hOut = dIn = dSlot = nullptr;
+        hCtl = dNext = nullptr;
+        bm = waves = Rin = Rout = 0;
+        st = nullptr;
+        dev = -1;
     }
     bool ensure(uint32_t bm_, uint32_t waves_, uint32_t rin, uint32_t rout) {
         int d = -1;

@@ -367,3 +367,63 @@ def test_streamed_slow_callbacks_are_not_a_timeout(monkeypatch):
     for slow in ({"slow_read": 9}, {"slow_write": 4}):
         r, out = _slow_io(L.lib.lz4mtDecompress, want, L.init_stream_descriptor(), L.MODE_DEVICE, **slow)
         assert r == 0 and out == data, (slow, L.result_to_string(r))
+
+
+def test_streamed_concurrent_calls_from_threads():
+    """Three host threads compress and decompress at once in MODE_DEVICE
+    (each thread's call launches its own persistent grid; grids that share a
+    hardware queue or the CUs run one after the other): every frame and
+    every decode is right, nothing waits on another call."""
+    import threading
+    inputs = [oracle.gen_synthetic((9 << 20) + 777 * k, 20 + k) for k in range(3)]
+    sds = [(6, True, True), (7, False, True), (6, False, False)]
+    res = [None] * 3
+
+    def work(k):
+        try:
+            bid, sck, bck = sds[k]
+            r, frame = L.compress(inputs[k], L.make_sd(bid, sck, bck), mode=L.MODE_DEVICE)
+            r2, out, _ = L.decompress(frame, len(inputs[k]) + 64, mode=L.MODE_DEVICE)
+            res[k] = (r, frame, r2, out)
+        except Exception as e:   # reported below
+            res[k] = e
+
+    ths = [threading.Thread(target=work, args=(k,)) for k in range(3)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(240)
+    for k in range(3):
+        assert not isinstance(res[k], Exception) and res[k] is not None, (k, res[k])
+        r, frame, r2, out = res[k]
+        bid, sck, bck = sds[k]
+        assert r == 0 and frame == oracle.compress_frame(inputs[k], oracle.params(bid, sck, bck)), k
+        assert r2 == 0 and out == inputs[k], k
+
+
+def _rss_bytes():
+    with open("/proc/self/statm") as f:
+        import os
+        return int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE")
+
+
+def test_streamed_rings_freed_at_thread_exit():
+    """A DEVICE-mode call keeps its streamed rings (pinned host memory, ~0.8
+    GiB at 1 MiB blocks) per thread for the next call; a thread that exits
+    frees them: four short-lived threads in turn leave the resident set where
+    the first one left it."""
+    import threading
+    data = oracle.gen_synthetic(3 << 20, 8)
+    sd = L.make_sd(6, False, True)
+
+    def one():
+        r, _ = L.compress(data, sd, mode=L.MODE_DEVICE)
+        assert r == 0
+
+    rss = []
+    for _ in range(4):
+        t = threading.Thread(target=one)
+        t.start()
+        t.join(120)
+        rss.append(_rss_bytes())
+    assert rss[-1] - rss[0] < (512 << 20), [x >> 20 for x in rss]
