@@ -81,7 +81,7 @@ public:
         if (!c_->read) return 0;
         const int r = c_->read(c_, d, n);
         if (r < n) eofHint_ = true;
-        return r < 0 ? 0 : r;
+        return r < 0 ? 0 : (r > n ? n : r);   // (a callback claiming more than it was given n bytes for)
     }
     bool readEof() { return c_->readEof ? c_->readEof(c_) != 0 : eofHint_; }
     // readU32: a short read sets ERROR (reference Ctx::readU32)

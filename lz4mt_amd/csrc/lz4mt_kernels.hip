@@ -3498,7 +3498,7 @@ __global__ void __launch_bounds__(64) k_encode_stream(const uint8_t* __restrict_
         bool ended = false;
         if (!stream_wait(inCtl + 4 * ri, b + 1, g, 2, b + 1, (int64_t)b, &ended, ticks)) return;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        const uint32_t n = ld_sys(inCtl + 4 * ri + 1);
+        const uint32_t n = min(ld_sys(inCtl + 4 * ri + 1), bm);   // (the host never publishes more)
         wave_copy16(din, gptr(hin) + (uint64_t)ri * bm, n);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (L == 0) st_sys(inCtl + 4 * ri + 2, b + 1);   // the staging slot may be refilled

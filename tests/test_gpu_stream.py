@@ -427,3 +427,45 @@ def test_streamed_rings_freed_at_thread_exit():
         t.join(120)
         rss.append(_rss_bytes())
     assert rss[-1] - rss[0] < (512 << 20), [x >> 20 for x in rss]
+
+
+def test_read_callback_claiming_more_than_asked():
+    """A read() that returns more than the n bytes it was asked for (a broken
+    callback) is taken as n bytes: no engine reads or copies past its
+    buffers; streamed DEVICE, batch DEVICE and PARALLEL frames all hold the
+    bytes actually delivered, n per read."""
+    from lz4mt_amd import _abi
+    data = oracle.gen_synthetic(5 << 20, 12)
+    for mode, stream in ((L.MODE_DEVICE, "1"), (L.MODE_DEVICE, "0"), (L.MODE_PARALLEL, "0")):
+        src = ctypes.create_string_buffer(data, len(data))
+        st = {"pos": 0}
+        out = []
+
+        def rd(ctx, dst, n):
+            k = min(n, len(data) - st["pos"])
+            ctypes.memmove(dst, ctypes.addressof(src) + st["pos"], k)
+            st["pos"] += k
+            return k + 4096 if k else 0   # claims 4 KiB more than it wrote
+
+        def wr(ctx, p, n):
+            out.append(ctypes.string_at(p, n))
+            return n
+
+        import os
+        old = os.environ.get("LZ4MT_AMD_STREAM")
+        os.environ["LZ4MT_AMD_STREAM"] = stream
+        try:
+            keep = [_abi.READ_FN(rd), _abi.WRITE_FN(wr)]
+            ctx = L.init_context()
+            ctx.mode = mode
+            ctx.read = ctypes.cast(keep[0], ctypes.c_void_p)
+            ctx.write = ctypes.cast(keep[1], ctypes.c_void_p)
+            sd = L.make_sd(6, True, True)
+            r = L.lib.lz4mtCompress(ctypes.byref(ctx), ctypes.byref(sd))
+        finally:
+            if old is None:
+                del os.environ["LZ4MT_AMD_STREAM"]
+            else:
+                os.environ["LZ4MT_AMD_STREAM"] = old
+        assert r == 0, (mode, stream, L.result_to_string(r))
+        assert b"".join(out) == oracle.compress_frame(data, oracle.params(6, True, True)), (mode, stream)
