@@ -469,3 +469,57 @@ def test_read_callback_claiming_more_than_asked():
                 os.environ["LZ4MT_AMD_STREAM"] = old
         assert r == 0, (mode, stream, L.result_to_string(r))
         assert b"".join(out) == oracle.compress_frame(data, oracle.params(6, True, True)), (mode, stream)
+
+
+def _dec_fail_write(frame, fail_at):
+    """lz4mtDecompress in MODE_DEVICE with a write() that fails at its
+    fail_at-th call; returns (result, bytes written before it)."""
+    from lz4mt_amd import _abi
+    src = ctypes.create_string_buffer(frame, len(frame))
+    st = {"pos": 0, "w": 0}
+    out = []
+
+    def rd(ctx, dst, n):
+        k = min(n, len(frame) - st["pos"])
+        ctypes.memmove(dst, ctypes.addressof(src) + st["pos"], k)
+        st["pos"] += k
+        return k
+
+    def wr(ctx, p, n):
+        st["w"] += 1
+        if st["w"] == fail_at:
+            return n - 1
+        out.append(ctypes.string_at(p, n))
+        return n
+
+    keep = [_abi.READ_FN(rd), _abi.WRITE_FN(wr)]
+    ctx = L.init_context()
+    ctx.mode = L.MODE_DEVICE
+    ctx.read = ctypes.cast(keep[0], ctypes.c_void_p)
+    ctx.write = ctypes.cast(keep[1], ctypes.c_void_p)
+    sd = L.init_stream_descriptor()
+    r = L.lib.lz4mtDecompress(ctypes.byref(ctx), ctypes.byref(sd))
+    return r, b"".join(out)
+
+
+def test_streamed_decompress_write_failure(monkeypatch):
+    """A write() that fails on a decoded block and on a raw (stored) block:
+    the streamed decompress ends with the batch engine's result code
+    (CANNOT_WRITE_DECODED_BLOCK / CANNOT_WRITE_DATA_BLOCK, the reference's
+    codes) and the same bytes before it; the grid drains and the next call
+    decodes the whole frame."""
+    data = bytearray(oracle.gen_synthetic(12 << 20, 31))
+    data[5 << 20:6 << 20] = oracle.gen_random(1 << 20, 31)   # block 5 is stored raw
+    data = bytes(data)
+    frame = oracle.compress_frame(data, oracle.params(6, True, True))
+    want = {3: L.Result.CANNOT_WRITE_DECODED_BLOCK, 6: L.Result.CANNOT_WRITE_DATA_BLOCK}
+    for k, code in want.items():
+        r1, o1 = _dec_fail_write(frame, k)
+        monkeypatch.setenv("LZ4MT_AMD_STREAM", "0")
+        r2, o2 = _dec_fail_write(frame, k)
+        monkeypatch.delenv("LZ4MT_AMD_STREAM")
+        assert (r1, o1) == (r2, o2), (k, L.result_to_string(r1), L.result_to_string(r2))
+        assert r1 == code, (k, L.result_to_string(r1))
+        assert o1 == data[:(k - 1) << 20], k
+    r, out = _dec_fail_write(frame, None)
+    assert r == 0 and out == data
