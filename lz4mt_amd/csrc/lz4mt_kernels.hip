@@ -3233,11 +3233,6 @@ __device__ __forceinline__ uint32_t xround(uint32_t acc, uint32_t w) { return ro
 // next round's add into one v_mad_u64_u32: the chain is alignbit + mad;
 // an unfused v_mul_lo_u32 + v_add_u32 was slower, profiles/r03n_xxh32_ab.txt)
 __device__ __forceinline__ uint32_t xround_pm(uint32_t acc, uint32_t wp) { return rotl32(acc + wp, 13) * kP1; }
-// LZ4MT_XXH_FULL: a whole 1 KiB chunk's LDS reads in flight before its 64
-// rounds (k_xxh32_stored 4.05 -> 3.78 ms at 8 GiB; profiles/r03n_xxh32_ab.txt)
-#ifndef LZ4MT_XXH_FULL
-#define LZ4MT_XXH_FULL 1
-#endif
 
 // One wavefront hashes one byte range: the range streams through LDS in
 // 1 KiB chunks (64 lanes x 16 B, loaded one chunk ahead), lanes 0..3 run
@@ -3274,8 +3269,10 @@ __device__ uint32_t xxh32_wave(g_cu8* p, uint64_t len, l_u32* __restrict__ buf /
             const uint32_t m = (uint32_t)min<uint64_t>(64, ns - ch * 64);
             const l_u32* cb = buf + cur * 256 + L;
             uint32_t i = 0;
-#if LZ4MT_XXH_FULL
-            if (m == 64) {   // a whole chunk: every read issued before the chain starts
+            // a whole 1 KiB chunk: all 64 LDS reads in flight before its rounds
+            // (k_xxh32_stored 4.05 -> 3.78 ms at 8 GiB, profiles/r03n_xxh32_ab.txt;
+            // full-rate 24-bit multiplies for the round: 5.83 ms, r05ad_xxh32_m24_ab.txt)
+            if (m == 64) {
                 uint32_t w[64];
 #pragma unroll
                 for (int u = 0; u < 64; ++u) w[u] = cb[4 * u];
@@ -3283,7 +3280,6 @@ __device__ uint32_t xxh32_wave(g_cu8* p, uint64_t len, l_u32* __restrict__ buf /
                 for (int u = 0; u < 64; ++u) v = xround_pm(v, w[u]);
                 i = 64;
             }
-#endif
             for (; i + 8 <= m; i += 8) {
                 uint32_t w[8];
 #pragma unroll
