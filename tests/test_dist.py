@@ -179,7 +179,8 @@ def _run_roundtrip(world, n, block_id, corrupt_rank=None):
     return res
 
 
-@pytest.mark.parametrize("world,n,block_id", [(2, 17 * 65536 + 12345, 4), (3, 7 * 262144 + 5, 5), (3, 65536 + 9, 4)])
+@pytest.mark.parametrize("world,n,block_id", [(2, 17 * 65536 + 12345, 4), (3, 7 * 262144 + 5, 5), (3, 65536 + 9, 4),
+                                             (4, 9 * 65536 + 3, 4)])
 def test_gather_verify_scatter_roundtrip(world, n, block_id):
     res = _run_roundtrip(world, n, block_id)
     assert all(ok for _, ok, _, _ in res), res           # stitched frame matches every shard
