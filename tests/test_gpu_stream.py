@@ -523,3 +523,35 @@ def test_streamed_decompress_write_failure(monkeypatch):
         assert o1 == data[:(k - 1) << 20], k
     r, out = _dec_fail_write(frame, None)
     assert r == 0 and out == data
+
+
+@pytest.mark.parametrize("bid,sck,bck", [(6, True, True), (6, False, True), (7, True, False)])
+def test_streamed_decompress_damaged_vs_oracle(bid, sck, bck):
+    """Randomly damaged 1 / 4 MiB-block frames through the streamed
+    decompress (lz4mtDecompress, MODE_DEVICE): the oracle's result code
+    (its restatement of src/lz4mt.cpp:593-734, 938-1011) and the oracle's
+    bytes -- on success, and the bytes written before an error."""
+    rnd = random.Random(bid * 100 + sck * 10 + bck)
+    n = (9 << 20) + 4321 if bid == 7 else (3 << 20) + 777
+    data = bytearray(oracle.gen_synthetic(n, bid))
+    data[n // 3:n // 3 + 300_000] = oracle.gen_random(300_000, bid)
+    data = bytes(data)
+    f = oracle.compress_frame(data, oracle.params(bid, sck, bck))
+    cap = n + (4 << 20)
+    for it in range(40 if bid == 6 else 16):
+        b = bytearray(f)
+        kind = rnd.randrange(4)
+        if kind == 0:
+            for _ in range(rnd.randrange(1, 4)):
+                b[rnd.randrange(len(b))] ^= 1 << rnd.randrange(8)
+        elif kind == 1:
+            del b[rnd.randrange(4, len(b)):]
+        elif kind == 2:
+            a = rnd.randrange(7, len(b) - 4)
+            b[a:a + 4] = rnd.randrange(1 << 32).to_bytes(4, "little")
+        else:
+            b += bytes(rnd.randrange(256) for _ in range(rnd.randrange(1, 12)))
+        r, out, _ = L.decompress(bytes(b), cap, mode=L.MODE_DEVICE)
+        rw, ow = oracle.decompress_frame(bytes(b), cap)
+        assert r == rw, (it, kind, L.result_to_string(r), L.result_to_string(rw))
+        assert out == ow, (it, kind, L.result_to_string(r), len(out), len(ow))
