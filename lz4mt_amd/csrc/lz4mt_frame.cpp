@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <cstring>
 
 #include <algorithm>
 #include <chrono>
@@ -1331,6 +1332,15 @@ extern "C" Lz4MtResult lz4mtDecompress(Lz4MtContext* ctx, Lz4MtStreamDescriptor*
     return s.result();
 }
 
+// A caller may pass any int (the reference's table answers "Unknown code"):
+// take the argument's bits without an enum-typed load of a value outside the
+// enumeration's range (UB in C++; UBSan -fsanitize=enum).
+static int result_bits(const Lz4MtResult* r) {
+    int v;
+    std::memcpy(&v, r, sizeof v);
+    return v;
+}
+
 extern "C" const char* lz4mtResultToString(Lz4MtResult r) {
     // Exactly the reference's table (src/lz4mt_result.cpp:4-89): it has no
     // case for BLOCK_CHECKSUM_MISMATCH (16), INVALID_HEADER_SKIPPABLE_SIZE_
@@ -1344,14 +1354,14 @@ extern "C" const char* lz4mtResultToString(Lz4MtResult r) {
         "CANNOT_READ_STREAM_CHECKSUM", nullptr, "STREAM_CHECKSUM_MISMATCH", "DECOMPRESS_FAIL",
         "BAD_ARG", "INVALID_BLOCK_SIZE", "INVALID_HEADER_RESERVED1", "INVALID_HEADER_RESERVED2",
         "INVALID_HEADER_RESERVED3", nullptr, nullptr, "CANNOT_WRITE_DATA_BLOCK", "CANNOT_WRITE_DECODED_BLOCK"};
-    const unsigned i = (unsigned)r;
+    const unsigned i = (unsigned)result_bits(&r);
     const char* s = i < sizeof(names) / sizeof(names[0]) ? names[i] : nullptr;
     return s ? s : "Unknown code";
 }
 
 extern "C" int lz4mtResultToLz4cExitCode(Lz4MtResult r) {
     // lz4c exit codes per result (reference src/lz4mt_result.cpp:92-270)
-    switch (r) {
+    switch (result_bits(&r)) {
         case LZ4MT_RESULT_OK: return 0;
         case LZ4MT_RESULT_INVALID_MAGIC_NUMBER: return 44;
         case LZ4MT_RESULT_INVALID_HEADER_SKIPPABLE_SIZE_UNREADABLE: return 42;
