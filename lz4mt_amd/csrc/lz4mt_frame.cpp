@@ -614,37 +614,116 @@ bool host_wait(P pred, Q stop) {
 // user's read() / write() is progress: while any callback runs, a keepalive
 // thread bumps the liveness word g[5] every 100 ms (a stalled pipe upstream
 // or downstream is not a hang).
+// Parking: a grid holds every CU's LDS for as long as it runs.  When one
+// read() has been blocked for LZ4MT_AMD_STREAM_PARK_MS (200 ms by default),
+// the same thread sets the park word g[7]: every wave waiting for a block that
+// is not published yet leaves (waves working on published blocks finish
+// them first), so other work on the device -- a callback's own GPU calls
+// included -- can run.  When that read() returns with data, the reader waits
+// for the parked grid to drain, points the block counter at the block it is
+// about to publish (every block below it was taken and finished: waves take
+// numbers in order and only leave on unpublished ones) and launches the grid
+// again.  The park word is only ever set while the reader is inside read(),
+// under the mutex it leaves read() with, so a block published after that
+// read() can never meet a parked wave.
 uint64_t stream_wait_ticks() {
     return (uint64_t)env_int("LZ4MT_AMD_STREAM_TIMEOUT_S", 60, 1, 86400) * 100000000ull;   // 100 MHz
 }
-class Keepalive {
+class StreamMonitor {
   public:
-    explicit Keepalive(uint32_t* live) : live_(live), th_([this] { run(); }) {}
-    ~Keepalive() {
+    StreamMonitor(uint32_t* live, uint32_t* park)
+        : live_(live), park_(park),
+          parkAfter_(std::chrono::milliseconds(env_int("LZ4MT_AMD_STREAM_PARK_MS", 200, 1, 86400000))),
+          th_([this] { run(); }) {}
+    ~StreamMonitor() {
         { std::lock_guard<std::mutex> lk(mu_); stop_ = true; }
         cv_.notify_all();
         th_.join();
     }
-    // one callback in progress for the scope's lifetime
+    // one write() in progress for the scope's lifetime
     struct Scope {
-        Keepalive& k;
-        explicit Scope(Keepalive& k_) : k(k_) { k.busy_.fetch_add(1, std::memory_order_relaxed); }
+        StreamMonitor& k;
+        explicit Scope(StreamMonitor& k_) : k(k_) { k.busy_.fetch_add(1, std::memory_order_relaxed); }
         ~Scope() { k.busy_.fetch_sub(1, std::memory_order_relaxed); }
     };
+    // the reader's read() calls for one block; leave() (or the destructor)
+    // ends them and says whether the grid was parked meanwhile
+    class ReadScope {
+      public:
+        explicit ReadScope(StreamMonitor& k) : k_(k) {
+            k_.busy_.fetch_add(1, std::memory_order_relaxed);
+            std::lock_guard<std::mutex> lk(k_.mu_);
+            k_.readSince_ = std::chrono::steady_clock::now();
+            k_.reading_ = true;
+        }
+        bool leave() {
+            if (done_) return parked_;
+            done_ = true;
+            {
+                std::lock_guard<std::mutex> lk(k_.mu_);
+                k_.reading_ = false;
+                parked_ = k_.parked_;
+            }
+            k_.busy_.fetch_sub(1, std::memory_order_relaxed);
+            return parked_;
+        }
+        ~ReadScope() { leave(); }
+
+      private:
+        StreamMonitor& k_;
+        bool done_ = false, parked_ = false;
+    };
+    // after the parked grid drained, before it is launched again
+    void unpark() {
+        std::lock_guard<std::mutex> lk(mu_);
+        __atomic_store_n(park_, 0u, __ATOMIC_RELEASE);
+        parked_ = false;
+    }
+    uint32_t parks() const { return parks_.load(std::memory_order_relaxed); }
 
   private:
     void run() {
         std::unique_lock<std::mutex> lk(mu_);
-        for (uint32_t beat = 1; !cv_.wait_for(lk, std::chrono::milliseconds(100), [this] { return stop_; });)
-            if (busy_.load(std::memory_order_relaxed) > 0) __atomic_store_n(live_, beat++, __ATOMIC_RELEASE);
+        uint32_t beat = 1;
+        for (uint32_t tick = 0; !cv_.wait_for(lk, std::chrono::milliseconds(10), [this] { return stop_; }); ++tick) {
+            if (tick % 10 == 0 && busy_.load(std::memory_order_relaxed) > 0)
+                __atomic_store_n(live_, beat++, __ATOMIC_RELEASE);
+            if (reading_ && !parked_ && std::chrono::steady_clock::now() - readSince_ >= parkAfter_) {
+                __atomic_store_n(park_, 1u, __ATOMIC_RELEASE);
+                parked_ = true;
+                parks_.fetch_add(1, std::memory_order_relaxed);
+            }
+        }
     }
     uint32_t* live_;
+    uint32_t* park_;
+    std::chrono::steady_clock::duration parkAfter_;
     std::atomic<int> busy_{0};
+    std::atomic<uint32_t> parks_{0};
     std::mutex mu_;
     std::condition_variable cv_;
-    bool stop_ = false;
+    bool stop_ = false, reading_ = false, parked_ = false;   // (under mu_)
+    std::chrono::steady_clock::time_point readSince_;
     std::thread th_;   // last: started once the members above exist
 };
+
+// waits for a parked grid to drain and launches it again at block `b`;
+// false when the call is stopping (abort, GPU error) instead
+template <class Launch>
+bool stream_relaunch(StreamBufs& B, uint32_t* g, StreamMonitor& mon, uint32_t b, Launch launch) {
+    if (hipStreamSynchronize(B.st) != hipSuccess || __atomic_load_n(g + 4, __ATOMIC_ACQUIRE) != 0 ||
+        __atomic_load_n(g + 1, __ATOMIC_ACQUIRE) != 0)
+        return false;
+    mon.unpark();
+    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(B.dNext), (int)b, 1, B.st) != hipSuccess ||
+        launch() != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (const char* t = getenv("LZ4MT_AMD_PIPE_TRACE"); t && atoi(t) != 0)   // (read per event: rare)
+        fprintf(stderr, "lz4mt_amd: streamed grid parked while read() stalled; relaunched at block %u\n", b);
+    return true;
+}
 
 bool stream_eligible(const Session& s, const Lz4MtStreamDescriptor* sd) {
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
@@ -673,17 +752,21 @@ void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
     memset(g, 0, 4ull * (8 + 4ull * Rin + 4ull * Rout));
     g[0] = 0xFFFFFFFFu;
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    if (hipMemsetAsync(B.dNext, 0, 4, B.st) != hipSuccess ||
-        launch_encode_stream(B.hIn, B.hOut, inC, outC, g, B.dNext, B.dIn, B.dSlot, bm, Rin, Rout, waves, bck ? 1 : 0,
-                             stream_wait_ticks(), B.st) != hipSuccess) {
+    const uint64_t ticks = stream_wait_ticks();
+    auto launch = [&] {
+        return launch_encode_stream(B.hIn, B.hOut, inC, outC, g, B.dNext, B.dIn, B.dSlot, bm, Rin, Rout, waves,
+                                    bck ? 1 : 0, ticks, B.st);
+    };
+    if (hipMemsetAsync(B.dNext, 0, 4, B.st) != hipSuccess || launch() != hipSuccess) {
         (void)hipGetLastError();
         s.quit(LZ4MT_RESULT_ERROR);
         return;
     }
     std::atomic<uint32_t> total{0xFFFFFFFFu};   // blocks in the stream, once known
     std::atomic<bool> wfail{false};
+    bool relaunchFail = false;
     auto gpuFailed = [&] { return ld_acq(g + 4) != 0; };
-    Keepalive ka(g + 5);
+    StreamMonitor ka(g + 5, g + 7);
     std::thread writer([&] {
         for (uint32_t b = 0;; ++b) {
             uint32_t* o = outC + 4ull * (b % Rout);
@@ -697,7 +780,7 @@ void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
             const uint8_t* payload = B.hOut + (uint64_t)(b % Rout) * bm;
             bool wok;
             {
-                Keepalive::Scope cb(ka);
+                StreamMonitor::Scope cb(ka);
                 wok = s.writeU32(word) && s.write(payload, (int)len) && (!bck || s.writeU32(sum));
             }
             if (!wok) {
@@ -739,11 +822,18 @@ void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
         if (ld_acq(g + 1) != 0 || gpuFailed()) break;   // the writer or the grid stopped
         uint8_t* dst = B.hIn + (uint64_t)(b % Rin) * bm;
         int n;
+        bool parked;
         {
-            Keepalive::Scope cb(ka);
+            StreamMonitor::ReadScope rs(ka);
             n = s.read(dst, (int)bm);
+            parked = rs.leave();
         }
         if (n <= 0) break;
+        if (parked && !stream_relaunch(B, g, ka, b, launch)) {   // the read stalled: the grid left the device
+            relaunchFail = true;
+            st_rel(g + 1, 1u);
+            break;
+        }
         st_rel(ic + 1, (uint32_t)n);
         st_rel(ic, b + 1);
         st_rel(g + 2, b + 1);   // heartbeat
@@ -754,7 +844,7 @@ void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
     writer.join();
     if (wfail || gpuFailed()) st_rel(g + 1, 1u);
     const hipError_t e = hipStreamSynchronize(B.st);
-    if (e != hipSuccess || gpuFailed() || (wfail && !s.error())) s.quit(LZ4MT_RESULT_ERROR);
+    if (e != hipSuccess || gpuFailed() || ((wfail || relaunchFail) && !s.error())) s.quit(LZ4MT_RESULT_ERROR);
     if (!(s.mode() & LZ4MT_MODE_DEVICE)) B.release();
 }
 
@@ -977,9 +1067,12 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
     memset(g, 0, 4ull * (8 + 4ull * Rin + 4ull * Rout));
     g[0] = 0xFFFFFFFFu;
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    if (hipMemsetAsync(B.dNext, 0, 4, B.st) != hipSuccess ||
-        launch_decode_stream(B.hIn, B.hOut, inC, outC, g, B.dNext, B.dIn, B.dSlot, bm, Rin, Rout, waves, bck ? 1 : 0,
-                             stream_wait_ticks(), B.st) != hipSuccess) {
+    const uint64_t ticks = stream_wait_ticks();
+    auto launch = [&] {
+        return launch_decode_stream(B.hIn, B.hOut, inC, outC, g, B.dNext, B.dIn, B.dSlot, bm, Rin, Rout, waves,
+                                    bck ? 1 : 0, ticks, B.st);
+    };
+    if (hipMemsetAsync(B.dNext, 0, 4, B.st) != hipSuccess || launch() != hipSuccess) {
         (void)hipGetLastError();
         s.quit(LZ4MT_RESULT_ERROR);
         return false;
@@ -987,9 +1080,10 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
     std::atomic<uint32_t> total{0xFFFFFFFFu};
     std::atomic<bool> wfail{false};
     std::atomic<uint32_t> hashed{0};
+    bool relaunchFail = false;
     auto gpuFailed = [&] { return ld_acq(g + 4) != 0; };
     auto stopped = [&] { return gpuFailed() || ld_acq(g + 1) != 0; };
-    Keepalive ka(g + 5);
+    StreamMonitor ka(g + 5, g + 7);
     // the content checksum over the decoded blocks, in order, beside the writer
     std::thread hasher;
     if (sck) {
@@ -1026,7 +1120,7 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
             }
             bool wok;
             {
-                Keepalive::Scope cb(ka);
+                StreamMonitor::Scope cb(ka);
                 wok = s.write(B.hOut + (uint64_t)(b % Rout) * bm, n);
             }
             if (!wok) {
@@ -1051,7 +1145,7 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
         uint32_t* ic = inC + 4ull * (b % Rin);
         if (b >= Rin && !host_wait([&] { return ld_acq(ic + 3) == b - Rin + 1; }, stopped)) break;
         if (stopped() || s.quitting()) break;
-        Keepalive::Scope cb(ka);   // the record's read() calls
+        StreamMonitor::ReadScope rs(ka);   // the record's read() calls
         if (s.readEof()) break;
         uint32_t bits = 0;
         if (!s.peekU32(&bits)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_SIZE; break; }
@@ -1061,6 +1155,11 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
         if (s.read(B.hIn + (uint64_t)(b % Rin) * bm, (int)n) != (int)n) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_DATA; break; }
         uint32_t ck = 0;
         if (bck && !s.peekU32(&ck)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_CHECKSUM; break; }
+        if (rs.leave() && !stream_relaunch(B, g, ka, b, launch)) {   // a read stalled: the grid left the device
+            relaunchFail = true;
+            st_rel(g + 1, 1u);
+            break;
+        }
         st_rel(ic + 1, bits);
         st_rel(ic + 2, ck);
         st_rel(ic, b + 1);
@@ -1075,7 +1174,7 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
     }
     if (wfail || gpuFailed()) st_rel(g + 1, 1u);
     const hipError_t e = hipStreamSynchronize(B.st);
-    if (e != hipSuccess || gpuFailed() || (wfail && !s.error())) s.quit(LZ4MT_RESULT_ERROR);
+    if (e != hipSuccess || gpuFailed() || ((wfail || relaunchFail) && !s.error())) s.quit(LZ4MT_RESULT_ERROR);
     if (!(s.mode() & LZ4MT_MODE_DEVICE)) B.release();
     if (pending != LZ4MT_RESULT_OK && !s.error()) s.quit(pending);
     return eos;

@@ -3424,6 +3424,8 @@ __global__ void __launch_bounds__(64) k_xxh32_stored(const uint8_t* __restrict__
 //   g[0] blocks in the stream (0xFFFFFFFF until known)  g[1] abort (host)
 //   g[2] blocks read (heartbeat)  g[3] records written (heartbeat)
 //   g[4] error (GPU: a wait timed out)  g[5] host liveness (inside a callback)
+//   g[7] park (host: a read() stalled -- waves waiting for an unpublished
+//        block leave; the host relaunches the grid at the next block)
 //   in[r]  {seq = b + 1, length, pulled = b + 1}   (4 words per slot)
 //   out[r] {seq = b + 1, size word, XXH32, written = b + 1}
 // A waiting wave sleeps in proportion to how far the awaited heartbeat is
@@ -3465,6 +3467,7 @@ __device__ __forceinline__ bool stream_wait(const uint32_t* w, uint32_t want, ui
         const uint32_t total = ld_sys(g), abort = ld_sys(g + 1), now = ld_sys(g + hb), live = ld_sys(g + 5);
         if (endAt >= 0 && (uint64_t)endAt >= total) { *ended = true; return false; }
         if (abort) return false;
+        if (hb == 2 && ld_sys(g + 7)) return false;   // parked (the block is not published: nothing is lost)
         const uint64_t t = __builtin_amdgcn_s_memrealtime();
         if (now != beat || live != alive) { beat = now; alive = live; t0 = t; }
         else if (t - t0 > ticks) {

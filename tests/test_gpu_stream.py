@@ -555,3 +555,83 @@ def test_streamed_decompress_damaged_vs_oracle(bid, sck, bck):
         rw, ow = oracle.decompress_frame(bytes(b), cap)
         assert r == rw, (it, kind, L.result_to_string(r), L.result_to_string(rw))
         assert out == ow, (it, kind, L.result_to_string(r), len(out), len(ow))
+
+
+def _hook_io(fn, data, sd, hooks):
+    """lz4mtCompress / lz4mtDecompress (MODE_DEVICE) with Python callbacks;
+    hooks[k] runs inside the k-th read() call (1-based) before it returns."""
+    from lz4mt_amd import _abi
+    src = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+    st = {"pos": 0, "r": 0}
+    out = []
+
+    def rd(ctx, dst, n):
+        st["r"] += 1
+        if st["r"] in hooks:
+            hooks[st["r"]]()
+        k = min(n, len(data) - st["pos"])
+        ctypes.memmove(dst, ctypes.addressof(src) + st["pos"], k)
+        st["pos"] += k
+        return k
+
+    def wr(ctx, p, n):
+        out.append(ctypes.string_at(p, n))
+        return n
+
+    keep = [_abi.READ_FN(rd), _abi.WRITE_FN(wr)]
+    ctx = L.init_context()
+    ctx.mode = L.MODE_DEVICE
+    ctx.read = ctypes.cast(keep[0], ctypes.c_void_p)
+    ctx.write = ctypes.cast(keep[1], ctypes.c_void_p)
+    r = fn(ctypes.byref(ctx), ctypes.byref(sd))
+    return r, b"".join(out)
+
+
+def _lds_heavy_gpu_work():
+    """GPU work that needs LDS (a GEMM and a radix sort), waited for."""
+    a = torch.randn(2048, 2048, device="cuda")
+    x = torch.sort(torch.rand(1 << 22, device="cuda"))[0]
+    return float((a @ a).sum().item()) + float(x[-1].item())
+
+
+def test_streamed_reader_stall_parks_the_grid(monkeypatch, capfd):
+    """A read() that stalls past LZ4MT_AMD_STREAM_PARK_MS parks the streamed
+    grid: its waiting waves leave the device, so GPU work that needs LDS --
+    here launched and waited for INSIDE the stalled read() -- runs (the grid
+    holds every CU's LDS while it waits, so without parking this callback
+    could never return); the reader then relaunches the grid at the next
+    block and the frames and bytes are exact.  Compress and decompress,
+    stalls early and late, a stall in the final read() (no relaunch), tight
+    rings."""
+    import time
+    monkeypatch.setenv("LZ4MT_AMD_STREAM_PARK_MS", "50")
+    monkeypatch.setenv("LZ4MT_AMD_PIPE_TRACE", "1")
+    waits = []
+
+    def timed_work():
+        t = time.time()
+        _lds_heavy_gpu_work()
+        waits.append(time.time() - t)
+
+    _lds_heavy_gpu_work()   # warm-up: libraries loaded, kernels compiled
+    data = oracle.gen_synthetic(24 << 20, 41)
+    frame = oracle.compress_frame(data, oracle.params(6, True, True))
+    for rings in ((256, 512), (8, 8)):
+        monkeypatch.setenv("LZ4MT_AMD_STREAM_IN", str(rings[0]))
+        monkeypatch.setenv("LZ4MT_AMD_STREAM_OUT", str(rings[1]))
+        for hooks in ({3: timed_work}, {2: timed_work, 17: timed_work},
+                      {25: lambda: time.sleep(0.2)}):   # read 25 returns 0: a stall at the end
+            t0 = time.time()
+            r, got = _hook_io(L.lib.lz4mtCompress, data, L.make_sd(6, True, True), hooks)
+            assert r == 0 and got == frame, (rings, sorted(hooks), L.result_to_string(r))
+            assert time.time() - t0 < 60
+        # decompress: three read() calls per record (size word, data, checksum)
+        for hooks in ({4: timed_work}, {2: timed_work, 30: timed_work}):
+            r, got = _hook_io(L.lib.lz4mtDecompress, frame, L.init_stream_descriptor(), hooks)
+            assert r == 0 and got == data, (rings, sorted(hooks), L.result_to_string(r))
+    err = capfd.readouterr().err
+    relaunches = err.count("relaunched at block")
+    with capfd.disabled():
+        print(f"hook waits (s): {[round(w, 3) for w in waits]}; relaunches: {relaunches}")
+    # every hook that ran while a grid was up had to wait for the park (>= 50 ms)
+    assert relaunches >= 8 and sum(w >= 0.045 for w in waits) >= 8, (waits, relaunches)
