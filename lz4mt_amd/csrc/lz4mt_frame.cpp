@@ -679,7 +679,6 @@ class StreamMonitor {
         __atomic_store_n(park_, 0u, __ATOMIC_RELEASE);
         parked_ = false;
     }
-    uint32_t parks() const { return parks_.load(std::memory_order_relaxed); }
 
   private:
     void run() {
@@ -691,7 +690,6 @@ class StreamMonitor {
             if (reading_ && !parked_ && std::chrono::steady_clock::now() - readSince_ >= parkAfter_) {
                 __atomic_store_n(park_, 1u, __ATOMIC_RELEASE);
                 parked_ = true;
-                parks_.fetch_add(1, std::memory_order_relaxed);
             }
         }
     }
@@ -699,7 +697,6 @@ class StreamMonitor {
     uint32_t* park_;
     std::chrono::steady_clock::duration parkAfter_;
     std::atomic<int> busy_{0};
-    std::atomic<uint32_t> parks_{0};
     std::mutex mu_;
     std::condition_variable cv_;
     bool stop_ = false, reading_ = false, parked_ = false;   // (under mu_)
