@@ -17,10 +17,12 @@ $(BUILD):
 
 # One source, two objects: the decoder's dependent-load chains schedule
 # better under max-ilp (decode kernel 31.8 -> 30.1 ms at 8 GiB; 33.2 ms with
-# the default scheduler); the encoder is fastest under iterative-ilp (8 GiB
-# B7: 182.4 / 182.7 ms vs 184.5 / 185.0 under max-memory-clause, 182.9 /
-# 183.7 default, 183.5 / 184.1 max-ilp; profiles/r03p_sched_ab.txt).
-ENC_SCHED ?= -mllvm --amdgpu-sched-strategy=iterative-ilp
+# the default scheduler).  The encoder object was fastest under iterative-ilp
+# in round 3 (profiles/r03p_sched_ab.txt); on the round-5 window it is
+# fastest under max-memory-clause at every block size (8 GiB k_encode B7
+# 151.4 vs 155.2 ms, B6 140.8 vs 144.4, B5 126.3 vs 128.2, B4 208.7 vs 213.4;
+# profiles/r05sch_sched_ab.txt).
+ENC_SCHED ?= -mllvm --amdgpu-sched-strategy=max-memory-clause
 $(BUILD)/lz4mt_kernels_enc.o: $(CSRC)/lz4mt_kernels.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DLZ4MT_PART=1 $(ENC_SCHED) -c -o $@ $<
 
