@@ -21,8 +21,10 @@ $(BUILD):
 # in round 3 (profiles/r03p_sched_ab.txt); on the round-5 window it is
 # fastest under max-memory-clause at every block size (8 GiB k_encode B7
 # 151.4 vs 155.2 ms, B6 140.8 vs 144.4, B5 126.3 vs 128.2, B4 208.7 vs 213.4;
-# profiles/r05sch_sched_ab.txt).
-ENC_SCHED ?= -mllvm --amdgpu-sched-strategy=max-memory-clause
+# profiles/r05sch_sched_ab.txt), and a further ~1 % at B7 / B6 without the
+# machine scheduler's memory-op clustering (150.2-150.8 vs 151.9-152.1 ms;
+# profiles/r05flg_flags_ab.txt).
+ENC_SCHED ?= -mllvm --amdgpu-sched-strategy=max-memory-clause -mllvm --misched-cluster=false
 $(BUILD)/lz4mt_kernels_enc.o: $(CSRC)/lz4mt_kernels.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DLZ4MT_PART=1 $(ENC_SCHED) -c -o $@ $<
 
