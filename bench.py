@@ -38,7 +38,10 @@ import os
 import socket
 import subprocess
 import sys
+import tempfile
+import threading
 import time
+import traceback
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -49,6 +52,7 @@ sys.path.insert(0, ROOT)
 torch = dist = L = D = None
 
 GiB = float(1 << 30)
+METRIC = "device-resident LZ4 GiB/s (compress, decompress) on 4 MiB blocks at 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 GOLDEN = 0x9E3779B97F4A7C15
 # the headline's PMC profile; the sweep points' are profiles/pmc_b<id>.json
@@ -263,18 +267,207 @@ def frame_encoder(bm):
     return "k_encode"
 
 
-def workload_id(world, block_id, sck=False, level=0, bd=False):
+class RunGuard:
+    """Bounded, diagnosable N > 1 runs.
+
+    Every rank names the stage it is in (init, input, setup, step, check,
+    report).  Whatever ends a rank early -- an exception in any stage, or
+    the run passing its deadline (LZ4MT_BENCH_DEADLINE_S, default 300 s from
+    the moment torch is imported; a collective that never returns counts) --
+    ends the WHOLE run the same way: rank 0 prints ONE JSON line
+    (``status: "failed"``, the failing ``stage``, ``transport``, ``error``,
+    and every rank's report in ``failures``) and exits non-zero.
+      * a non-root rank writes its report into a per-run directory (all
+        ranks of one node share it: /tmp keyed by the rendezvous port and
+        the launcher's pid) and waits up to 20 s for rank 0 to acknowledge;
+      * rank 0 polls that directory from a thread, so it reports even while
+        its main thread is blocked inside a collective that waits for the
+        failed rank; on its own exception it first waits ~2 s for the other
+        ranks' reports (its error may be the echo of theirs, e.g. a gloo
+        connection closed by a dead peer);
+      * the earliest report is the cause (``stage``/``error``).
+    Processes end with os._exit, so no process-group destructor can stall
+    the exit.  The process groups' timeout is set above the deadline
+    (bench.py), so the guard, not a watchdog abort, ends a hung collective.
+    LZ4MT_BENCH_FAULT="<stage>:<rank>[:hang]" injects a failure (or a hang)
+    at a stage on one rank, for the tests."""
+
+    STAGES = ("init", "input", "setup", "step", "check", "report")
+
+    def __init__(self, rank, world, n_gpus, enabled, deadline_s=None):
+        self.rank, self.world, self.n_gpus, self.enabled = rank, world, n_gpus, enabled
+        self.stage, self.transport = "init", None
+        self.deadline_s = float(deadline_s if deadline_s is not None else
+                                os.environ.get("LZ4MT_BENCH_DEADLINE_S", "300"))
+        self.t0 = time.monotonic()
+        self._lock = threading.Lock()
+        self._reported = False
+        key = f"{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}"
+        self.dir = os.path.join(tempfile.gettempdir(), f"lz4mt_bench_{key}")
+        f = os.environ.get("LZ4MT_BENCH_FAULT", "").split(":")
+        self.fault = (f[0], int(f[1]) if len(f) > 1 and f[1].isdigit() else 0, len(f) > 2 and f[2] == "hang") \
+            if f[0] else None
+        if enabled:
+            os.makedirs(self.dir, exist_ok=True)
+            threading.Thread(target=self._deadline, daemon=True).start()
+            if rank == 0 and world > 1:
+                threading.Thread(target=self._poll, daemon=True).start()
+
+    def remaining_s(self):
+        return self.deadline_s - (time.monotonic() - self.t0)
+
+    def enter(self, stage, point=None):
+        """Now in ``stage``; ``point`` names a place inside it (a fault can
+        be injected there: e.g. "gather", between a step's gather and its
+        scatter, while the other ranks sit in a collective)."""
+        self.stage = stage
+        if self.fault and self.fault[0] == (point or stage) and self.fault[1] == self.rank:
+            if self.fault[2]:
+                print(f"bench.py: rank {self.rank}: injected hang in stage {stage}", file=sys.stderr, flush=True)
+                while True:
+                    time.sleep(3600)
+            raise RuntimeError(f"injected fault (LZ4MT_BENCH_FAULT) in stage {stage} on rank {self.rank}")
+
+    def _record(self, error):
+        return {"rank": self.rank, "stage": self.stage, "transport": self.transport, "error": error,
+                "t": time.time(), "elapsed_s": round(time.monotonic() - self.t0, 3)}
+
+    def _reports(self):
+        out = []
+        try:
+            names = sorted(os.listdir(self.dir))
+        except OSError:
+            return out
+        for nm in names:
+            if nm.startswith("fail_") and nm.endswith(".json"):
+                try:
+                    out.append(json.load(open(os.path.join(self.dir, nm))))
+                except (OSError, ValueError):
+                    pass
+        return out
+
+    def failed(self, error):
+        """This rank cannot go on: report (rank 0: the JSON line) and exit 1."""
+        rec = self._record(error)
+        print(f"bench.py: rank {self.rank} failed in stage {self.stage}: {error}", file=sys.stderr, flush=True)
+        if self.rank == 0:
+            time.sleep(2.0)   # the other ranks' reports, if this error echoes theirs
+            self._report_root([rec] + self._reports())
+        else:
+            try:
+                os.makedirs(self.dir, exist_ok=True)
+                tmp = os.path.join(self.dir, f".fail_{self.rank}.tmp")
+                with open(tmp, "w") as fh:
+                    json.dump(rec, fh)
+                os.replace(tmp, os.path.join(self.dir, f"fail_{self.rank}.json"))
+            except OSError:
+                pass
+            ack = os.path.join(self.dir, "ack")
+            t_end = time.monotonic() + 20.0
+            while time.monotonic() < t_end and not os.path.exists(ack):
+                time.sleep(0.1)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(1)
+
+    def _report_root(self, recs):
+        with self._lock:
+            if self._reported:
+                return
+            self._reported = True
+        recs = sorted(recs, key=lambda r: r.get("t", 0.0))
+        first = recs[0]
+        line = {"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": self.n_gpus, "status": "failed",
+                "stage": first.get("stage"), "transport": first.get("transport") or self.transport,
+                "error": first.get("error"), "failed_rank": first.get("rank"), "root_stage": self.stage,
+                "elapsed_s": round(time.monotonic() - self.t0, 3), "deadline_s": self.deadline_s,
+                "failures": [{k: r.get(k) for k in ("rank", "stage", "transport", "error", "elapsed_s")}
+                             for r in recs]}
+        print(json.dumps(line), flush=True)
+        try:
+            open(os.path.join(self.dir, "ack"), "w").close()
+        except OSError:
+            pass
+
+    def _poll(self):
+        while True:
+            time.sleep(0.2)
+            with self._lock:
+                if self._reported:
+                    return
+            recs = self._reports()
+            if recs:
+                time.sleep(1.0)   # the rest of a cascade
+                self._report_root(self._reports() + [self._record("(rank 0 was still running this stage)")])
+                sys.stdout.flush()
+                sys.stderr.flush()
+                os._exit(1)
+
+    def _deadline(self):
+        while self.remaining_s() > 0:
+            time.sleep(min(1.0, max(0.05, self.remaining_s())))
+        with self._lock:
+            done = self._reported
+        if done:   # the result is out; only the teardown (process-group destroy) is late
+            print("bench.py: teardown passed the deadline; exiting", file=sys.stderr, flush=True)
+            sys.stdout.flush()
+            os._exit(self._exit_code)
+        self.failed(f"deadline exceeded: the run passed LZ4MT_BENCH_DEADLINE_S = {self.deadline_s:g} s "
+                    f"in stage {self.stage} (a collective or a peer that never answered)")
+
+    _exit_code = 0
+
+    def succeeded(self, ok=True):
+        """The run's result is final on this rank; rank 0 prints its line only
+        when this returns True (under the same lock as a failure line: never
+        two lines).  The deadline still bounds the teardown after it."""
+        with self._lock:
+            if self._reported:
+                return False
+            self._reported = True
+            self._exit_code = 0 if ok else 1
+        return True
+
+    def cleanup(self):
+        if self.enabled and self.rank == 0:
+            import shutil
+            shutil.rmtree(self.dir, ignore_errors=True)
+
+
+def workload_id(world, block_id, sck=False, level=0, bd=False, n_total=None, strong=False):
     """configs[1] is the 4 MiB -Sx -BX headline; other block sizes are the
-    configs[4] sweep; N > 1 is configs[3].  The content checksum (default
-    flags), LZ4-HC levels and -BD are modes BASELINE.json names no config
-    for: labelled as such, never as configs[1]."""
+    configs[4] sweep.  N > 1 is labelled configs[3] only when the run IS
+    configs[3] -- 64 GiB in total of 4 MiB -Sx -BX blocks (weak scaling at
+    8 GPUs x 8 GiB, or --total-gib 64 at any N); any other N > 1 run says
+    what it is.  The content checksum (default flags),
+    LZ4-HC levels and -BD are modes BASELINE.json names no config for:
+    labelled as such, never as configs[1]."""
     if sck or level >= 3 or bd:
         mode = ", ".join(m for m, on in (("default flags (FLG.2 content checksum)", sck),
                                          (f"LZ4-HC level {level}", level >= 3), ("-BD", bd)) if on)
         return f"off-baseline mode ({mode}; not a BASELINE.json config)"
-    if world > 1:
-        return "configs[3]"
+    if world > 1 or strong:
+        shape = (f"strong scaling, one {n_total / GiB:g} GiB buffer over {world} GPU(s)" if strong else
+                 f"weak scaling, {n_total / world / GiB:g} GiB/GPU x {world} = {n_total / GiB:g} GiB")
+        if n_total == 64 * (1 << 30) and block_id == 7:
+            return f"configs[3] ({shape})"
+        return f"configs[3]-style scaling point, not configs[3] itself ({shape}; configs[3] is 64 GiB in total)"
     return "configs[1]" if block_id == 7 else "configs[4] (block-size sweep)"
+
+
+def parallelism_label(world, distributed, streamed, transport_name, backend):
+    """What actually moved the records (no 'RCCL gather'
+    when the IPC push did it)."""
+    s = f"block-sharded x{world}"
+    if not distributed:
+        return s
+    if streamed:
+        how = ("copy-engine IPC push into the root's receive buffers, round sizes over gloo"
+               if transport_name == "ipc" else
+               f"{'RCCL' if backend == 'nccl' else backend} point-to-point ({transport_name})")
+        return s + f", records gathered to one frame on rank 0 beside the encodes by {how}"
+    return s + f", records gathered to one frame on rank 0 after the encode by " \
+               f"{'RCCL' if backend == 'nccl' else backend} point-to-point"
 
 
 def _free_port():
@@ -305,6 +498,23 @@ def main():
     import torch as _torch
     import torch.distributed as _dist
     torch, dist = _torch, _dist
+    # LZ4MT_BENCH_DIST=1 runs the N > 1 path (process group, streamed gather,
+    # scatter, stitched-frame check) at world size 1 too: the nccl backend on
+    # a one-GPU box (RCCL allows one rank per device)
+    distributed = world > 1 or os.environ.get("LZ4MT_BENCH_DIST") == "1"
+    guard = RunGuard(rank, world, a.gpus, enabled=distributed)
+    try:
+        run(a, guard, world, rank, local, distributed)
+    except BaseException as e:   # noqa: B902 -- every way out of a rank ends the run the same way
+        if not guard.enabled or (isinstance(e, SystemExit) and (e.code in (0, None) or guard._reported)):
+            raise   # (a result line is out already: its exit status stands)
+        err = f"{type(e).__name__}: {e}"
+        traceback.print_exc(file=sys.stderr)
+        guard.failed(err)
+
+
+def run(a, guard, world, rank, local, distributed):
+    global L, D
     import lz4mt_amd as _L
     from lz4mt_amd import dist as _D
     L, D = _L, _D
@@ -312,21 +522,23 @@ def main():
     # ranks sharing the GPUs there are (gloo moves CUDA tensors through the
     # host); the measured multi-GPU path is RCCL, one rank per GPU
     backend = os.environ.get("LZ4MT_BENCH_BACKEND", "nccl")
-    # LZ4MT_BENCH_DIST=1 runs the N > 1 path (process group, streamed gather,
-    # scatter, stitched-frame check) at world size 1 too: the nccl backend on
-    # a one-GPU box (RCCL allows one rank per device)
-    distributed = world > 1 or os.environ.get("LZ4MT_BENCH_DIST") == "1"
     local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
     torch.cuda.set_device(local)
     if distributed:
+        guard.enter("init")
+        # an explicit timeout: a rank that stops answering ends the run
+        # non-zero instead of stalling it for torch's 30 min default; set
+        # above the guard's deadline, so the guard (one JSON line) and not
+        # the RCCL watchdog's abort ends a collective that never returns
+        import datetime
+        pg_timeout = max(D.dist_timeout(), datetime.timedelta(seconds=guard.deadline_s + 60))
         with stdout_to_stderr():
-            # an explicit timeout: a rank that stops answering ends the run
-            # non-zero instead of stalling it for torch's 30 min default
             if backend == "nccl":
-                dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=D.dist_timeout())
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=pg_timeout)
             else:
-                dist.init_process_group(backend, timeout=D.dist_timeout())
+                dist.init_process_group(backend, timeout=pg_timeout)
                 dist.barrier()   # (gloo connects its mesh here at the latest)
+        guard.enter("input")
     dev = torch.device("cuda", local)
     stream = torch.cuda.current_stream()
 
@@ -391,6 +603,9 @@ def main():
         torch.cuda.synchronize()
     own_body = 0
     transport = transport_name = None
+    if distributed:
+        guard.transport = (a.transport if streamed else f"{backend} point-to-point (gather after the encode)")
+        guard.enter("setup")
     if streamed:   # the shard engine's streams and workspace, the control group and transport, made once
         eng = D.HipShardEngine(dev)
         shard_ws = L.shard_workspace(n, sd, device=dev)
@@ -408,7 +623,10 @@ def main():
             print(f"bench.py: IPC PUSH UNAVAILABLE ({e}); streamed gather falls back to RCCL point-to-point",
                   file=sys.stderr, flush=True)
             transport, transport_name = D.RcclTransport(), f"rccl (IPC setup failed: {e})"
+            guard.transport = transport_name
             D.prepare_transport(transport, eng, n, sd, ctrl=ctrl)
+    if distributed:
+        guard.enter("step")
 
     def run_steps(transport):
         """W untimed + K timed steps; returns the accumulated timings and the last step's frames."""
@@ -449,6 +667,7 @@ def main():
                 tgr = time.perf_counter() - tl if distributed else 0.0
             full = R["full"]
             if distributed:
+                guard.enter("step", point="gather")
                 sst = {}
                 R["piece"] = D.scatter_frame(full if rank == 0 else None, full.numel() if rank == 0 else 0, src=0,
                                              device=dev, stats=sst)
@@ -493,6 +712,7 @@ def main():
     R = run_steps(transport)
     mem = None
     if distributed:
+        guard.enter("check")
         # the root's device memory at its peak: torch's allocator (sources,
         # workspaces, mirrors, the stitched frame, pieces) and the device as
         # a whole (hipMemGetInfo: + the IPC receive buffers, library scratch)
@@ -508,8 +728,12 @@ def main():
               file=sys.stderr, flush=True)
         transport.close()
         transport, transport_name = D.RcclTransport(), "rccl (IPC push gave a wrong stitched frame; re-run)"
+        guard.transport = transport_name
+        guard.enter("setup")
         D.prepare_transport(transport, eng, n, sd, ctrl=ctrl)
+        guard.enter("step")
         R = run_steps(transport)
+        guard.enter("check")
         ok, stitched_ok = check(R)
     tc, td, ts, tg = R["tc"], R["td"], R["ts"], R["tg"]
     enc_ms, dec_ms, frame_len, exposed_ms = R["enc_ms"], R["dec_ms"], R["frame_len"], R["exposed_ms"]
@@ -520,6 +744,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         tc, td, ts, tg, bad = t.tolist()
         ok = bad == 0.0 and stitched_ok
+        guard.enter("report")
     K = a.steps
     total = n_total * K
     comp_gibps = None if a.decompress_only else total / GiB / tc
@@ -571,15 +796,16 @@ def main():
             "config": {"workload": (f"configs[2]: {a.gib:g} GiB/GPU pre-compressed synthetic stream, "
                                     f"{bm >> 10} KiB blocks, decompress+XXH32 verify only, device-resident")
                                    if a.decompress_only else
-                                   (f"configs[3]: ONE {a.total_gib:g} GiB synthetic buffer block-sharded over "
+                                   (f"{workload_id(world, a.block_id, sck, a.level, a.block_dependent, n_total, True)}: "
+                                    f"ONE {a.total_gib:g} GiB synthetic buffer block-sharded over "
                                     f"{world} GPU(s), {bm >> 10} KiB independent blocks, {flags} frame, "
                                     f"compress+decompress+XXH32, device-resident")
                                    if a.total_gib is not None else
-                                   (f"{workload_id(world, a.block_id, sck, a.level, a.block_dependent)}: {a.gib:g} GiB/GPU synthetic, {bm >> 10} KiB "
+                                   (f"{workload_id(world, a.block_id, sck, a.level, a.block_dependent, n_total)}: "
+                                    f"{a.gib:g} GiB/GPU synthetic, {bm >> 10} KiB "
                                     f"independent blocks, {flags} frame, compress+decompress+XXH32, device-resident"),
                        "bytes_per_gpu": n, "bytes_total": n_total, "block_bytes": bm,
-                       "parallelism": f"block-sharded x{world}" + (", RCCL gather to one frame on rank 0 (in compress)"
-                                                                   if distributed else "")},
+                       "parallelism": parallelism_label(world, distributed, streamed, transport_name, backend)},
             "compress_GiBps": round(comp_gibps, 3) if comp_gibps else None,
             "decompress_GiBps": round(decomp_gibps, 3),
             "ratio": round((n_total / frame_len) if streamed else (n / frame_len), 4), "frame_bytes": frame_len,
@@ -604,12 +830,17 @@ def main():
                                               "host_staged": bool(scat and scat[0]["host_staged"])},
                          "root_memory": mem, "peer_access": peers if streamed else D.peer_access_matrix(),
                          "stitched_frame_bytes": full.numel(), "stitched_frame_ok": stitched_ok,
-                         "roundtrip_with_scatter_GiBps": round(total / GiB / (tc + ts + td), 3)})
-        print(json.dumps(line), flush=True)
+                         "roundtrip_with_scatter_GiBps": round(total / GiB / (tc + ts + td), 3),
+                         "deadline_s": guard.deadline_s, "elapsed_s": round(time.monotonic() - guard.t0, 3)})
+        if guard.succeeded(ok):
+            print(json.dumps(line), flush=True)
+    else:
+        guard.succeeded(ok)
     if streamed:
         transport.close()
     if distributed:
         dist.destroy_process_group()
+    guard.cleanup()
     if not ok:
         sys.exit(1)
 

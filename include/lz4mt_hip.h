@@ -163,6 +163,10 @@ Lz4MtResult lz4mtHipShardReset(uint64_t n, const Lz4MtStreamDescriptor* sd, void
  * must have been reset (lz4mtHipShardReset) after its previous use. */
 Lz4MtResult lz4mtHipShardEncode(const void* d_src, uint64_t n, const Lz4MtStreamDescriptor* sd, void* d_ws,
                                 uint64_t wsSize, void* stream);
+/* Forgets the call-order state kept for the workspace at d_ws (its next use
+ * needs lz4mtHipShardReset first).  Call it when the workspace is freed, so
+ * that a new allocation at the same address starts unknown. */
+void lz4mtHipShardRelease(const void* d_ws);
 /* One round into d_pack (capacity >= lz4mtHipShardPackBound): final = 0 while
  * the encode may still run (stream-ordered anywhere), final = 1 once it is
  * done (stream-ordered after it; repeat until the header's flags bit 0 is

@@ -12,6 +12,7 @@ libamdhip64 (identical soname); there is no CPU fallback: on a machine
 without a HIP device every compute entry point returns an error.
 """
 import ctypes
+import weakref
 
 import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
@@ -284,7 +285,12 @@ def shard_workspace(n, sd, device=None):
     nbytes = int(lib.lz4mtHipShardWorkspaceSize(int(n), ctypes.byref(sd)))
     if nbytes == 0:
         raise Lz4MtError(Result.BAD_ARG, "lz4mtHipShardWorkspaceSize (the descriptor does not shard)")
-    return torch.empty(nbytes, dtype=torch.uint8, device=device or "cuda")
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=device or "cuda")
+    # the library keeps the Reset -> Encode -> Pack order per workspace
+    # address: forget it when the tensor goes, so a later allocation at the
+    # same address never inherits "encoded" 
+    weakref.finalize(ws, lib.lz4mtHipShardRelease, ctypes.c_void_p(ws.data_ptr()))
+    return ws
 
 
 def shard_pack_bound(n, sd, per_block_cap):

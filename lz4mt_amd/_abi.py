@@ -119,6 +119,7 @@ PROTOTYPES = {
     "lz4mtHipFrameHeader": (c_int, [SD_P, c_void_p]),
     "lz4mtHipShardReset": (c_int, [c_uint64, SD_P, c_void_p, c_uint64, c_void_p]),
     "lz4mtHipShardEncode": (c_int, [c_void_p, c_uint64, SD_P, c_void_p, c_uint64, c_void_p]),
+    "lz4mtHipShardRelease": (None, [c_void_p]),
     "lz4mtHipShardPack": (c_int, [c_void_p, c_uint64, SD_P, c_void_p, c_uint64, c_void_p, c_uint64, c_uint32, c_int,
                                   c_void_p]),
     "lz4mtHipShardUnpack": (c_int, [c_void_p, c_uint64, SD_P, c_void_p, c_uint64, c_void_p]),

@@ -96,13 +96,15 @@ hipError_t launch_encode_pub(const uint8_t* src, uint64_t srcSize, uint32_t bloc
 hipError_t launch_decode(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax,
                          uint8_t* out, uint64_t outCap, int32_t* dsize, hipStream_t st);
 // the streamed compress's persistent encoder (lz4mt_kernels.hip, k_encode_stream);
-// ticks: a wait's limit without progress (s_memrealtime, 100 MHz)
+// ticks: a wait's limit without progress (s_memrealtime, 100 MHz); pend:
+// 4 words per wave, a block parked on its output slot (zeroed before the
+// first launch of a call; a relaunch finishes those blocks first)
 hipError_t launch_encode_stream(const uint8_t* hin, uint8_t* hout, uint32_t* inCtl, uint32_t* outCtl, uint32_t* g,
-                                uint32_t* next, uint8_t* dIn, uint8_t* dSlot, uint32_t bm, uint32_t Rin,
+                                uint32_t* next, uint32_t* pend, uint8_t* dIn, uint8_t* dSlot, uint32_t bm, uint32_t Rin,
                                 uint32_t Rout, uint32_t waves, int bck, uint64_t ticks, hipStream_t st);
 // the streamed decompress's persistent decoder (lz4mt_kernels.hip, k_decode_stream)
 hipError_t launch_decode_stream(const uint8_t* hin, uint8_t* hout, uint32_t* inCtl, uint32_t* outCtl, uint32_t* g,
-                                uint32_t* next, uint8_t* dIn, uint8_t* dSlot, uint32_t bm, uint32_t Rin,
+                                uint32_t* next, uint32_t* pend, uint8_t* dIn, uint8_t* dSlot, uint32_t bm, uint32_t Rin,
                                 uint32_t Rout, uint32_t waves, int bck, uint64_t ticks, hipStream_t st);
 hipError_t launch_xxh32_stored(const uint8_t* src, const uint8_t* slots, uint64_t srcSize, uint32_t blockSize,
                                uint32_t nBlocks, const int32_t* csize, uint32_t* digest, hipStream_t st);

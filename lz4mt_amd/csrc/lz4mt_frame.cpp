@@ -556,6 +556,7 @@ struct StreamBufs {
     uint8_t *hIn = nullptr, *hOut = nullptr, *dIn = nullptr, *dSlot = nullptr;
     uint32_t* hCtl = nullptr;       // g[8] | in[4 Rin] | out[4 Rout]  (coherent pinned)
     uint32_t* dNext = nullptr;      // the grid's block counter
+    uint32_t* dPend = nullptr;      // per wave: a block parked on its output slot {b + 1, word, sum, 0}
     uint32_t bm = 0, waves = 0, Rin = 0, Rout = 0;
     hipStream_t st = nullptr;
     int dev = -1;
@@ -564,10 +565,10 @@ struct StreamBufs {
     void release() {
         if (st) hipStreamSynchronize(st);
         hipHostFree(hIn); hipHostFree(hOut); hipHostFree(hCtl);
-        hipFree(dIn); hipFree(dSlot); hipFree(dNext);
+        hipFree(dIn); hipFree(dSlot); hipFree(dNext); hipFree(dPend);
         if (st) hipStreamDestroy(st);
         hIn = hOut = dIn = dSlot = nullptr;
-        hCtl = dNext = nullptr;
+        hCtl = dNext = dPend = nullptr;
         bm = waves = Rin = Rout = 0;
         st = nullptr;
         dev = -1;
@@ -585,7 +586,8 @@ struct StreamBufs {
             hipHostMalloc(reinterpret_cast<void**>(&hCtl), 4ull * (8 + 4ull * Rin + 4ull * Rout), hf) != hipSuccess ||
             hipMalloc(reinterpret_cast<void**>(&dIn), (uint64_t)waves * (bm + 64)) != hipSuccess ||
             hipMalloc(reinterpret_cast<void**>(&dSlot), (uint64_t)waves * (bm + 64)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&dNext), 64) != hipSuccess) {
+            hipMalloc(reinterpret_cast<void**>(&dNext), 64) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&dPend), 16ull * waves) != hipSuccess) {
             (void)hipGetLastError();
             release();
             return false;
@@ -594,6 +596,14 @@ struct StreamBufs {
     }
 };
 thread_local StreamBufs g_stream;
+
+// Waves of the streamed grids: LZ4MT_AMD_STREAM_WAVES_PER_CU (1..8) per CU.
+// Every wave owns two bm-byte HBM buffers (its block's input and output), so
+// this sets the engine's HBM footprint: waves x 2 x (bm + 64) per calling
+// thread.
+uint32_t stream_waves(int cus) {
+    return (uint32_t)cus * (uint32_t)env_int("LZ4MT_AMD_STREAM_WAVES_PER_CU", 4, 1, 8);
+}
 
 inline uint32_t ld_acq(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 inline void st_rel(uint32_t* p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
@@ -614,25 +624,29 @@ bool host_wait(P pred, Q stop) {
 // user's read() / write() is progress: while any callback runs, a keepalive
 // thread bumps the liveness word g[5] every 100 ms (a stalled pipe upstream
 // or downstream is not a hang).
-// Parking: a grid holds every CU's LDS for as long as it runs.  When one
-// read() has been blocked for LZ4MT_AMD_STREAM_PARK_MS (200 ms by default),
-// the same thread sets the park word g[7]: every wave waiting for a block that
-// is not published yet leaves (waves working on published blocks finish
-// them first), so other work on the device -- a callback's own GPU calls
-// included -- can run.  When that read() returns with data, the reader waits
-// for the parked grid to drain, points the block counter at the block it is
-// about to publish (every block below it was taken and finished: waves take
-// numbers in order and only leave on unpublished ones) and launches the grid
-// again.  The park word is only ever set while the reader is inside read(),
-// under the mutex it leaves read() with, so a block published after that
-// read() can never meet a parked wave.
+// Parking: a grid holds the LDS of every CU it runs on for as long as it
+// runs.  When one read() or one write() has been blocked for
+// LZ4MT_AMD_STREAM_PARK_MS (200 ms by default), the monitor sets the park
+// word g[7] and the grid leaves the device: a wave waiting for a block that
+// is not published leaves (it re-reads the block's word after seeing the
+// park, so a block published before the park is always taken); a wave whose
+// block is encoded (decoded) but whose output slot is still taken leaves its
+// block in its own HBM buffers with a descriptor in dPend; waves working on
+// a block finish it and then do one of the two.  While parked the reader
+// publishes nothing (publish() below), so every block below the reader's
+// next one was taken.  Other work on the device -- a callback's own GPU
+// calls included -- can then run.  The grid is launched again, at the
+// reader's next block, once no callback is stalled any more: by the reader
+// before it publishes, or by whichever thread's stalled callback returns
+// last; each wave first finishes the block it parked with.
 uint64_t stream_wait_ticks() {
     return (uint64_t)env_int("LZ4MT_AMD_STREAM_TIMEOUT_S", 60, 1, 86400) * 100000000ull;   // 100 MHz
 }
 class StreamMonitor {
   public:
-    StreamMonitor(uint32_t* live, uint32_t* park)
-        : live_(live), park_(park),
+    template <class Launch>
+    StreamMonitor(StreamBufs& B, uint32_t* g, Launch launch)
+        : B_(B), g_(g), launch_(launch),
           parkAfter_(std::chrono::milliseconds(env_int("LZ4MT_AMD_STREAM_PARK_MS", 200, 1, 86400000))),
           th_([this] { run(); }) {}
     ~StreamMonitor() {
@@ -640,109 +654,155 @@ class StreamMonitor {
         cv_.notify_all();
         th_.join();
     }
-    // one write() in progress for the scope's lifetime
-    struct Scope {
-        StreamMonitor& k;
-        explicit Scope(StreamMonitor& k_) : k(k_) { k.busy_.fetch_add(1, std::memory_order_relaxed); }
-        ~Scope() { k.busy_.fetch_sub(1, std::memory_order_relaxed); }
-    };
-    // the reader's read() calls for one block; leave() (or the destructor)
-    // ends them and says whether the grid was parked meanwhile
-    class ReadScope {
+    // one callback in progress for the scope's lifetime; the writer's and the
+    // reader's are timed for parking
+    class Scope {
       public:
-        explicit ReadScope(StreamMonitor& k) : k_(k) {
+        Scope(StreamMonitor& k, bool reader) : k_(k), reader_(reader) {
             k_.busy_.fetch_add(1, std::memory_order_relaxed);
             std::lock_guard<std::mutex> lk(k_.mu_);
-            k_.readSince_ = std::chrono::steady_clock::now();
-            k_.reading_ = true;
+            (reader_ ? k_.readSince_ : k_.writeSince_) = std::chrono::steady_clock::now();
+            (reader_ ? k_.reading_ : k_.writing_) = true;
         }
-        bool leave() {
-            if (done_) return parked_;
+        void leave() {
+            if (done_) return;
             done_ = true;
             {
                 std::lock_guard<std::mutex> lk(k_.mu_);
-                k_.reading_ = false;
-                parked_ = k_.parked_;
+                (reader_ ? k_.reading_ : k_.writing_) = false;
             }
             k_.busy_.fetch_sub(1, std::memory_order_relaxed);
-            return parked_;
         }
-        ~ReadScope() { leave(); }
+        ~Scope() { leave(); }
 
       private:
         StreamMonitor& k_;
-        bool done_ = false, parked_ = false;
+        bool reader_, done_ = false;
     };
-    // after the parked grid drained, before it is launched again
-    void unpark() {
-        std::lock_guard<std::mutex> lk(mu_);
-        __atomic_store_n(park_, 0u, __ATOMIC_RELEASE);
-        parked_ = false;
+    // The reader publishes block b through fn() -- never while the grid is
+    // parked: then it relaunches the grid at b itself, or, while another
+    // callback is still stalled, waits for that thread to.  false: the call
+    // is stopping (abort, GPU error, failed relaunch).
+    template <class F, class Stop>
+    bool publish(uint32_t b, F fn, Stop stop) {
+        for (;;) {
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (!parked_) {
+                    fn();
+                    nextPub_ = b + 1;
+                    return true;
+                }
+                if (!stalled_locked()) {
+                    if (!relaunch_locked()) return false;
+                    continue;
+                }
+            }
+            if (stop()) return false;
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
     }
+    // After a callback returned (and at the end of the input): a parked grid
+    // is launched again unless another callback is still stalled.  false:
+    // the relaunch failed.
+    bool resume() {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!parked_ || stalled_locked()) return true;
+        return relaunch_locked();
+    }
+    bool parked() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return parked_;
+    }
+    uint32_t parks() const { return parks_.load(std::memory_order_relaxed); }
 
   private:
+    bool stalled_locked() const {
+        const auto now = std::chrono::steady_clock::now();
+        return (reading_ && now - readSince_ >= parkAfter_) || (writing_ && now - writeSince_ >= parkAfter_);
+    }
+    // (mu_ held: nothing is published and nothing parks meanwhile) waits for
+    // the parked grid to drain -- every wave leaves by itself -- and launches
+    // it again at the reader's next block
+    bool relaunch_locked() {
+        if (hipStreamSynchronize(B_.st) != hipSuccess || __atomic_load_n(g_ + 4, __ATOMIC_ACQUIRE) != 0 ||
+            __atomic_load_n(g_ + 1, __ATOMIC_ACQUIRE) != 0) {
+            (void)hipGetLastError();
+            return false;
+        }
+        __atomic_store_n(g_ + 7, 0u, __ATOMIC_RELEASE);
+        parked_ = false;
+        if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(B_.dNext), (int)nextPub_, 1, B_.st) != hipSuccess ||
+            launch_() != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (const char* t = getenv("LZ4MT_AMD_PIPE_TRACE"); t && atoi(t) != 0)   // (read per event: rare)
+            fprintf(stderr, "lz4mt_amd: streamed grid parked while a %s stalled; relaunched at block %u\n",
+                    lastWhy_, nextPub_);
+        return true;
+    }
     void run() {
         std::unique_lock<std::mutex> lk(mu_);
         uint32_t beat = 1;
         for (uint32_t tick = 0; !cv_.wait_for(lk, std::chrono::milliseconds(10), [this] { return stop_; }); ++tick) {
             if (tick % 10 == 0 && busy_.load(std::memory_order_relaxed) > 0)
-                __atomic_store_n(live_, beat++, __ATOMIC_RELEASE);
-            if (reading_ && !parked_ && std::chrono::steady_clock::now() - readSince_ >= parkAfter_) {
-                __atomic_store_n(park_, 1u, __ATOMIC_RELEASE);
+                __atomic_store_n(g_ + 5, beat++, __ATOMIC_RELEASE);
+            if (!parked_ && stalled_locked()) {
+                const auto now = std::chrono::steady_clock::now();
+                lastWhy_ = (reading_ && now - readSince_ >= parkAfter_) ? "read()" : "write()";
+                __atomic_store_n(g_ + 7, 1u, __ATOMIC_RELEASE);
                 parked_ = true;
+                parks_.fetch_add(1, std::memory_order_relaxed);
             }
         }
     }
-    uint32_t* live_;
-    uint32_t* park_;
+    StreamBufs& B_;
+    uint32_t* g_;
+    std::function<hipError_t()> launch_;
     std::chrono::steady_clock::duration parkAfter_;
     std::atomic<int> busy_{0};
+    std::atomic<uint32_t> parks_{0};
     std::mutex mu_;
     std::condition_variable cv_;
-    bool stop_ = false, reading_ = false, parked_ = false;   // (under mu_)
-    std::chrono::steady_clock::time_point readSince_;
+    // (under mu_)
+    bool stop_ = false, reading_ = false, writing_ = false, parked_ = false;
+    uint32_t nextPub_ = 0;
+    const char* lastWhy_ = "read()";
+    std::chrono::steady_clock::time_point readSince_, writeSince_;
     std::thread th_;   // last: started once the members above exist
 };
 
-// waits for a parked grid to drain and launches it again at block `b`;
-// false when the call is stopping (abort, GPU error) instead
-template <class Launch>
-bool stream_relaunch(StreamBufs& B, uint32_t* g, StreamMonitor& mon, uint32_t b, Launch launch) {
-    if (hipStreamSynchronize(B.st) != hipSuccess || __atomic_load_n(g + 4, __ATOMIC_ACQUIRE) != 0 ||
-        __atomic_load_n(g + 1, __ATOMIC_ACQUIRE) != 0)
-        return false;
-    mon.unpark();
-    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(B.dNext), (int)b, 1, B.st) != hipSuccess ||
-        launch() != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    if (const char* t = getenv("LZ4MT_AMD_PIPE_TRACE"); t && atoi(t) != 0)   // (read per event: rare)
-        fprintf(stderr, "lz4mt_amd: streamed grid parked while read() stalled; relaunched at block %u\n", b);
-    return true;
-}
-
+// every block size of independent blocks at levels < 3 (64 KiB blocks on
+// the byU16 stream kernel); LZ4-HC levels keep the batch engine
 bool stream_eligible(const Session& s, const Lz4MtStreamDescriptor* sd) {
-    const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
-    return stream_enabled() && sd->flg.blockIndependence && s.level() < 3 && bm >= (1u << 20) && bm <= (4u << 20);
+    return stream_enabled() && sd->flg.blockIndependence && s.level() < 3;
 }
 
-void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
+// Ring slots: LZ4MT_AMD_STREAM_IN / _OUT, else 1 GiB / 2 GiB of pinned
+// memory whatever the block size (256 / 512 slots of 4 MiB; 64 KiB blocks
+// get 16384 / 32768 slots, so as many bytes stay in flight)
+uint32_t stream_slots(const char* var, uint64_t bytes, uint32_t bm) {
+    const uint64_t def = std::min<uint64_t>(65536, std::max<uint64_t>(8, bytes / bm));
+    return (uint32_t)env_int(var, (int)def, 8, 65536);
+}
+
+// false: the engine could not start (its buffers, the device): nothing was
+// read, and the caller takes the batch engine instead
+bool compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
     int cus = 0, dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-        hipSuccess || cus <= 0) {
-        s.quit(LZ4MT_RESULT_ERROR);
-        return;
-    }
-    // a wave per 20 KiB of LDS: 8 per CU; the staging ring only has to stay
-    // ahead of the pulls (~1 ms per block), the output ring behind the writer
-    const uint32_t waves = (uint32_t)cus * 8;
-    const uint32_t Rin = (uint32_t)env_int("LZ4MT_AMD_STREAM_IN", 256, 8, 65536);
-    const uint32_t Rout = (uint32_t)env_int("LZ4MT_AMD_STREAM_OUT", 512, 8, 65536);
+        hipSuccess || cus <= 0)
+        return false;
+    // the staging ring only has to stay ahead of the pulls (~1 ms per
+    // block), the output ring behind the writer
+    const uint32_t waves = stream_waves(cus);
+    const uint32_t Rin = stream_slots("LZ4MT_AMD_STREAM_IN", 1ull << 30, bm);
+    const uint32_t Rout = stream_slots("LZ4MT_AMD_STREAM_OUT", 2ull << 30, bm);
     StreamBufs& B = g_stream;
-    if (!B.ensure(bm, waves, Rin, Rout)) { s.quit(LZ4MT_RESULT_ERROR); return; }
+    if (!B.ensure(bm, waves, Rin, Rout)) return false;
     uint32_t* g = B.hCtl;
     uint32_t* inC = g + 8;
     uint32_t* outC = inC + 4ull * Rin;
@@ -751,24 +811,24 @@ void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
     std::atomic_thread_fence(std::memory_order_seq_cst);
     const uint64_t ticks = stream_wait_ticks();
     auto launch = [&] {
-        return launch_encode_stream(B.hIn, B.hOut, inC, outC, g, B.dNext, B.dIn, B.dSlot, bm, Rin, Rout, waves,
-                                    bck ? 1 : 0, ticks, B.st);
+        return launch_encode_stream(B.hIn, B.hOut, inC, outC, g, B.dNext, B.dPend, B.dIn, B.dSlot, bm, Rin, Rout,
+                                    waves, bck ? 1 : 0, ticks, B.st);
     };
-    if (hipMemsetAsync(B.dNext, 0, 4, B.st) != hipSuccess || launch() != hipSuccess) {
+    if (hipMemsetAsync(B.dNext, 0, 4, B.st) != hipSuccess || hipMemsetAsync(B.dPend, 0, 16ull * waves, B.st) !=
+        hipSuccess || launch() != hipSuccess) {
         (void)hipGetLastError();
-        s.quit(LZ4MT_RESULT_ERROR);
-        return;
+        hipStreamSynchronize(B.st);
+        return false;
     }
     std::atomic<uint32_t> total{0xFFFFFFFFu};   // blocks in the stream, once known
-    std::atomic<bool> wfail{false};
-    bool relaunchFail = false;
+    std::atomic<bool> wfail{false}, relaunchFail{false};
     auto gpuFailed = [&] { return ld_acq(g + 4) != 0; };
-    StreamMonitor ka(g + 5, g + 7);
+    auto stopped = [&] { return gpuFailed() || ld_acq(g + 1) != 0; };
+    StreamMonitor ka(B, g, launch);
     std::thread writer([&] {
         for (uint32_t b = 0;; ++b) {
             uint32_t* o = outC + 4ull * (b % Rout);
-            const bool ok = host_wait([&] { return ld_acq(o) == b + 1 || b >= total.load(); },
-                                      [&] { return gpuFailed() || ld_acq(g + 1) != 0; });
+            const bool ok = host_wait([&] { return ld_acq(o) == b + 1 || b >= total.load(); }, stopped);
             if (!ok || (b >= total.load() && ld_acq(o) != b + 1)) {
                 if (!ok) wfail = true;
                 return;
@@ -777,7 +837,7 @@ void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
             const uint8_t* payload = B.hOut + (uint64_t)(b % Rout) * bm;
             bool wok;
             {
-                StreamMonitor::Scope cb(ka);
+                StreamMonitor::Scope cb(ka, false);
                 wok = s.writeU32(word) && s.write(payload, (int)len) && (!bck || s.writeU32(sum));
             }
             if (!wok) {
@@ -787,6 +847,11 @@ void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
             }
             st_rel(o + 3, b + 1);   // the slot may take block b + Rout
             st_rel(g + 3, b + 1);   // heartbeat
+            if (!ka.resume()) {     // a write() stall parked the grid: back on the device
+                relaunchFail = true;
+                st_rel(g + 1, 1u);
+                return;
+            }
         }
     });
     // the content checksum (FLG.2) is one serial XXH32 chain: a hasher
@@ -798,8 +863,7 @@ void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
         hasher = std::thread([&] {
             for (uint32_t h = 0;; ++h) {
                 const uint32_t* ic = inC + 4ull * (h % Rin);
-                if (!host_wait([&] { return ld_acq(ic) == h + 1 || h >= total.load(); },
-                               [&] { return gpuFailed() || ld_acq(g + 1) != 0; }) ||
+                if (!host_wait([&] { return ld_acq(ic) == h + 1 || h >= total.load(); }, stopped) ||
                     ld_acq(ic) != h + 1)
                     return;
                 xs.update(B.hIn + (uint64_t)(h % Rin) * bm, ld_acq(ic + 1));
@@ -814,40 +878,47 @@ void compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
         uint32_t* ic = inC + 4ull * (b % Rin);
         if (b >= Rin && !host_wait([&] { return ld_acq(ic + 2) == b - Rin + 1 &&
                                                 (!sck || hashed.load(std::memory_order_acquire) > b - Rin); },
-                                   [&] { return gpuFailed() || ld_acq(g + 1) != 0; }))
+                                   stopped))
             break;
-        if (ld_acq(g + 1) != 0 || gpuFailed()) break;   // the writer or the grid stopped
+        if (stopped()) break;   // the writer or the grid stopped
         uint8_t* dst = B.hIn + (uint64_t)(b % Rin) * bm;
         int n;
-        bool parked;
         {
-            StreamMonitor::ReadScope rs(ka);
+            StreamMonitor::Scope rs(ka, true);
             n = s.read(dst, (int)bm);
-            parked = rs.leave();
         }
         if (n <= 0) break;
-        if (parked && !stream_relaunch(B, g, ka, b, launch)) {   // the read stalled: the grid left the device
-            relaunchFail = true;
+        // never while the grid is parked (a read() or write() stalled): the
+        // reader relaunches it at b first, or waits for the writer to
+        if (!ka.publish(b, [&] {
+                st_rel(ic + 1, (uint32_t)n);
+                st_rel(ic, b + 1);
+                st_rel(g + 2, b + 1);   // heartbeat
+            }, stopped)) {
+            if (!stopped()) relaunchFail = true;
             st_rel(g + 1, 1u);
             break;
         }
-        st_rel(ic + 1, (uint32_t)n);
-        st_rel(ic, b + 1);
-        st_rel(g + 2, b + 1);   // heartbeat
     }
     total = b;
     st_rel(g, b);   // waves waiting for a block >= b leave
+    // a grid parked by the last read() holds blocks that still go out
+    if (!stopped() && !ka.resume()) {
+        relaunchFail = true;
+        st_rel(g + 1, 1u);
+    }
     if (hasher.joinable()) hasher.join();
     writer.join();
     if (wfail || gpuFailed()) st_rel(g + 1, 1u);
     const hipError_t e = hipStreamSynchronize(B.st);
     if (e != hipSuccess || gpuFailed() || ((wfail || relaunchFail) && !s.error())) s.quit(LZ4MT_RESULT_ERROR);
     if (!(s.mode() & LZ4MT_MODE_DEVICE)) B.release();
+    return true;
 }
 
 void compress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
     if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return; }
-    if (stream_eligible(s, sd)) { compress_streamed(s, sd, xs); return; }
+    if (stream_eligible(s, sd) && compress_streamed(s, sd, xs)) return;
     // LZ4-HC on independent blocks: levels 3..9 the hashChain parser, 10..12
     // (and above, clamped) the optimal parser.  Block-dependent frames at any
     // level >= 3 are the reference's HC stream, at level 9 (HcBdSim).
@@ -1044,20 +1115,20 @@ bool decompress_host(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs)
 // while reading applies once every record before it is written.
 // LZ4MT_AMD_STREAM=0 keeps the batch engine below.
 // ---------------------------------------------------------------------------
-bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
+// false: the engine could not start (nothing was read); *eos: the EOS mark
+// was reached
+bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs, bool* eosOut) {
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
     int cus = 0, dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-        hipSuccess || cus <= 0) {
-        s.quit(LZ4MT_RESULT_ERROR);
+        hipSuccess || cus <= 0)
         return false;
-    }
-    const uint32_t waves = (uint32_t)cus * 8;   // a wave per 20 KiB of LDS
-    const uint32_t Rin = (uint32_t)env_int("LZ4MT_AMD_STREAM_IN", 256, 8, 65536);
-    const uint32_t Rout = (uint32_t)env_int("LZ4MT_AMD_STREAM_OUT", 512, 8, 65536);
+    const uint32_t waves = stream_waves(cus);
+    const uint32_t Rin = stream_slots("LZ4MT_AMD_STREAM_IN", 1ull << 30, bm);
+    const uint32_t Rout = stream_slots("LZ4MT_AMD_STREAM_OUT", 2ull << 30, bm);
     StreamBufs& B = g_stream;
-    if (!B.ensure(bm, waves, Rin, Rout)) { s.quit(LZ4MT_RESULT_ERROR); return false; }
+    if (!B.ensure(bm, waves, Rin, Rout)) return false;
     uint32_t* g = B.hCtl;
     uint32_t* inC = g + 8;
     uint32_t* outC = inC + 4ull * Rin;
@@ -1066,21 +1137,21 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
     std::atomic_thread_fence(std::memory_order_seq_cst);
     const uint64_t ticks = stream_wait_ticks();
     auto launch = [&] {
-        return launch_decode_stream(B.hIn, B.hOut, inC, outC, g, B.dNext, B.dIn, B.dSlot, bm, Rin, Rout, waves,
-                                    bck ? 1 : 0, ticks, B.st);
+        return launch_decode_stream(B.hIn, B.hOut, inC, outC, g, B.dNext, B.dPend, B.dIn, B.dSlot, bm, Rin, Rout,
+                                    waves, bck ? 1 : 0, ticks, B.st);
     };
-    if (hipMemsetAsync(B.dNext, 0, 4, B.st) != hipSuccess || launch() != hipSuccess) {
+    if (hipMemsetAsync(B.dNext, 0, 4, B.st) != hipSuccess || hipMemsetAsync(B.dPend, 0, 16ull * waves, B.st) !=
+        hipSuccess || launch() != hipSuccess) {
         (void)hipGetLastError();
-        s.quit(LZ4MT_RESULT_ERROR);
+        hipStreamSynchronize(B.st);
         return false;
     }
     std::atomic<uint32_t> total{0xFFFFFFFFu};
-    std::atomic<bool> wfail{false};
+    std::atomic<bool> wfail{false}, relaunchFail{false};
     std::atomic<uint32_t> hashed{0};
-    bool relaunchFail = false;
     auto gpuFailed = [&] { return ld_acq(g + 4) != 0; };
     auto stopped = [&] { return gpuFailed() || ld_acq(g + 1) != 0; };
-    StreamMonitor ka(g + 5, g + 7);
+    StreamMonitor ka(B, g, launch);
     // the content checksum over the decoded blocks, in order, beside the writer
     std::thread hasher;
     if (sck) {
@@ -1117,7 +1188,7 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
             }
             bool wok;
             {
-                StreamMonitor::Scope cb(ka);
+                StreamMonitor::Scope cb(ka, false);
                 wok = s.write(B.hOut + (uint64_t)(b % Rout) * bm, n);
             }
             if (!wok) {
@@ -1132,6 +1203,11 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
             }
             st_rel(o + 3, b + 1);   // the slot may take block b + Rout
             st_rel(g + 3, b + 1);   // heartbeat
+            if (!ka.resume()) {     // a write() stall parked the grid: back on the device
+                relaunchFail = true;
+                st_rel(g + 1, 1u);
+                return;
+            }
         }
     });
     // the reader: every read on this thread (the batch engine's record checks)
@@ -1142,28 +1218,38 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
         uint32_t* ic = inC + 4ull * (b % Rin);
         if (b >= Rin && !host_wait([&] { return ld_acq(ic + 3) == b - Rin + 1; }, stopped)) break;
         if (stopped() || s.quitting()) break;
-        StreamMonitor::ReadScope rs(ka);   // the record's read() calls
-        if (s.readEof()) break;
-        uint32_t bits = 0;
-        if (!s.peekU32(&bits)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_SIZE; break; }
-        if (bits == 0) { eos = true; break; }
-        const uint32_t n = bits & ~kRawBit;
-        if (n > bm) { pending = LZ4MT_RESULT_INVALID_BLOCK_SIZE; break; }
-        if (s.read(B.hIn + (uint64_t)(b % Rin) * bm, (int)n) != (int)n) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_DATA; break; }
-        uint32_t ck = 0;
-        if (bck && !s.peekU32(&ck)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_CHECKSUM; break; }
-        if (rs.leave() && !stream_relaunch(B, g, ka, b, launch)) {   // a read stalled: the grid left the device
-            relaunchFail = true;
+        uint32_t bits = 0, ck = 0;
+        {
+            StreamMonitor::Scope rs(ka, true);   // the record's read() calls
+            if (s.readEof()) break;
+            if (!s.peekU32(&bits)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_SIZE; break; }
+            if (bits == 0) { eos = true; break; }
+            const uint32_t n = bits & ~kRawBit;
+            if (n > bm) { pending = LZ4MT_RESULT_INVALID_BLOCK_SIZE; break; }
+            if (s.read(B.hIn + (uint64_t)(b % Rin) * bm, (int)n) != (int)n) {
+                pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_DATA;
+                break;
+            }
+            if (bck && !s.peekU32(&ck)) { pending = LZ4MT_RESULT_CANNOT_READ_BLOCK_CHECKSUM; break; }
+        }
+        if (!ka.publish(b, [&] {
+                st_rel(ic + 1, bits);
+                st_rel(ic + 2, ck);
+                st_rel(ic, b + 1);
+                st_rel(g + 2, b + 1);   // heartbeat
+            }, stopped)) {
+            if (!stopped()) relaunchFail = true;
             st_rel(g + 1, 1u);
             break;
         }
-        st_rel(ic + 1, bits);
-        st_rel(ic + 2, ck);
-        st_rel(ic, b + 1);
-        st_rel(g + 2, b + 1);   // heartbeat
     }
     total = b;
     st_rel(g, b);   // waves waiting for a block >= b leave
+    // a grid parked by the last read() holds blocks that still go out
+    if (!stopped() && !ka.resume()) {
+        relaunchFail = true;
+        st_rel(g + 1, 1u);
+    }
     writer.join();
     if (hasher.joinable()) {
         if (s.error() || s.quitting() || wfail) st_rel(g + 1, 1u);
@@ -1174,12 +1260,12 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
     if (e != hipSuccess || gpuFailed() || ((wfail || relaunchFail) && !s.error())) s.quit(LZ4MT_RESULT_ERROR);
     if (!(s.mode() & LZ4MT_MODE_DEVICE)) B.release();
     if (pending != LZ4MT_RESULT_OK && !s.error()) s.quit(pending);
-    return eos;
+    *eosOut = eos;
+    return true;
 }
 
 bool stream_eligible_dec(const Lz4MtStreamDescriptor* sd) {
-    const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
-    return stream_enabled() && sd->flg.blockIndependence && bm >= (1u << 20) && bm <= (4u << 20);
+    return stream_enabled() && sd->flg.blockIndependence;
 }
 
 // ---------------------------------------------------------------------------
@@ -1187,7 +1273,7 @@ bool stream_eligible_dec(const Lz4MtStreamDescriptor* sd) {
 // ---------------------------------------------------------------------------
 bool decompress_device(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& xs) {
     if (lz4mtHipDeviceCount() <= 0) { s.quit(LZ4MT_RESULT_ERROR); return false; }
-    if (stream_eligible_dec(sd)) return decompress_streamed(s, sd, xs);
+    if (bool eos = false; stream_eligible_dec(sd) && decompress_streamed(s, sd, xs, &eos)) return eos;
     const uint32_t bm = (uint32_t)block_max_bytes(sd->bd.blockMaximumSize);
     const bool bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
     // Block-dependent frames (decompressBlockDependency, src/lz4mt.cpp:

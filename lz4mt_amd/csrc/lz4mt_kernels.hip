@@ -3424,8 +3424,11 @@ __global__ void __launch_bounds__(64) k_xxh32_stored(const uint8_t* __restrict__
 //   g[0] blocks in the stream (0xFFFFFFFF until known)  g[1] abort (host)
 //   g[2] blocks read (heartbeat)  g[3] records written (heartbeat)
 //   g[4] error (GPU: a wait timed out)  g[5] host liveness (inside a callback)
-//   g[7] park (host: a read() stalled -- waves waiting for an unpublished
-//        block leave; the host relaunches the grid at the next block)
+//   g[7] park (host: a read() or a write() stalled -- waves waiting for an
+//        unpublished block leave, waves waiting for an output slot leave
+//        their block in their HBM buffers with a descriptor in pend[]; the
+//        host relaunches the grid at its next block once the stall ends, and
+//        each wave first finishes the block it parked with)
 //   in[r]  {seq = b + 1, length, pulled = b + 1}   (4 words per slot)
 //   out[r] {seq = b + 1, size word, XXH32, written = b + 1}
 // A waiting wave sleeps in proportion to how far the awaited heartbeat is
@@ -3454,71 +3457,121 @@ __device__ __forceinline__ void wave_copy16(g_u8* d, g_cu8* s, uint32_t n) {
     for (uint32_t i = (n16 << 4) + L; i < n; i += 64) d[i] = s[i];
 }
 // Waits until *w == want.  hb: the heartbeat (2 = blocks read, 3 = records
-// written) that reaches `target` when *w is about to change.  false on
-// abort, on a timeout (`ticks` of s_memrealtime, 100 MHz, without a change of
-// the heartbeat or of the host's liveness word g[5]; g[4] set), or --
-// endAt >= 0 -- once the stream is known to hold no block endAt (*ended).
-__device__ __forceinline__ bool stream_wait(const uint32_t* w, uint32_t want, uint32_t* g, uint32_t hb,
-                                            uint32_t target, int64_t endAt, bool* ended, uint64_t ticks) {
+// written) that reaches `target` when *w is about to change.  kWaitOk, or
+// kWaitStop on abort, on a timeout (`ticks` of s_memrealtime, 100 MHz,
+// without a change of the heartbeat or of the host's liveness word g[5]; g[4]
+// set), or -- endAt >= 0 -- once the stream is known to hold no block endAt
+// (*ended); kWaitPark when the host parked the grid (g[7]): an input wait
+// (hb 2) re-reads *w after seeing the park word, so a block published before
+// the park is always taken (the host publishes nothing while parked).
+constexpr int kWaitStop = 0, kWaitOk = 1, kWaitPark = 2;
+__device__ __forceinline__ int stream_wait(const uint32_t* w, uint32_t want, uint32_t* g, uint32_t hb,
+                                           uint32_t target, int64_t endAt, bool* ended, uint64_t ticks) {
     uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t beat = ld_sys(g + hb), alive = ld_sys(g + 5);
     for (;;) {
-        if (ld_sys(w) == want) return true;
+        if (ld_sys(w) == want) return kWaitOk;
         const uint32_t total = ld_sys(g), abort = ld_sys(g + 1), now = ld_sys(g + hb), live = ld_sys(g + 5);
-        if (endAt >= 0 && (uint64_t)endAt >= total) { *ended = true; return false; }
-        if (abort) return false;
-        if (hb == 2 && ld_sys(g + 7)) return false;   // parked (the block is not published: nothing is lost)
+        if (endAt >= 0 && (uint64_t)endAt >= total) { *ended = true; return kWaitStop; }
+        if (abort) return kWaitStop;
+        if (ld_sys(g + 7)) {   // parked
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            return hb == 2 && ld_sys(w) == want ? kWaitOk : kWaitPark;
+        }
         const uint64_t t = __builtin_amdgcn_s_memrealtime();
         if (now != beat || live != alive) { beat = now; alive = live; t0 = t; }
         else if (t - t0 > ticks) {
             if (laneid() == 0) st_sys(g + 4, 1u);
-            return false;
+            return kWaitStop;
         }
         const uint32_t dist = target > now ? min(target - now, 64u) : 0u;
         for (uint32_t k = 0; k < 8 * dist + 2; ++k) __builtin_amdgcn_s_sleep(127);
     }
 }
 
-template <bool XC>
+// A wave's block parked on its output slot: {b + 1, word, sum} (lane 0's
+// vector store; read back by the wave's relaunch, a kernel boundary later)
+__device__ __forceinline__ void pend_store(uint32_t* pend, uint32_t b, uint32_t word, uint32_t sum) {
+    if (laneid() == 0) {
+        v4u v;
+        v.x = b + 1;
+        v.y = word;
+        v.z = sum;
+        v.w = 0;
+        *(g_u4*)(gptr((uint8_t*)(pend + 4 * blockIdx.x))) = v;
+    }
+}
+
+// B16: 64 KiB blocks (every block < 65 547 B): k_encode16's byU16 split
+// table and LDS layout (26.3 KiB, 6 waves per CU); else k_encode's (1 MiB /
+// 4 MiB, and 256 KiB blocks on the same v5 table: p17's sweeps would need
+// their own instantiation for a path bound by the host's read())
+template <bool XC, bool B16>
 __global__ void __launch_bounds__(64) k_encode_stream(const uint8_t* __restrict__ hin, uint8_t* __restrict__ hout,
                                                       uint32_t* inCtl, uint32_t* outCtl, uint32_t* g,
-                                                      uint32_t* __restrict__ next, uint8_t* __restrict__ dIn,
-                                                      uint8_t* __restrict__ dSlot, uint32_t bm, uint32_t Rin,
-                                                      uint32_t Rout, int bck, uint64_t ticks) {
-    ENCODE_LDS
+                                                      uint32_t* __restrict__ next, uint32_t* pend,
+                                                      uint8_t* __restrict__ dIn, uint8_t* __restrict__ dSlot,
+                                                      uint32_t bm, uint32_t Rin, uint32_t Rout, int bck,
+                                                      uint64_t ticks) {
+    constexpr uint32_t kWords = B16 ? kE16Words : 5120;
+    __shared__ __attribute__((aligned(16))) uint32_t ELDS[kWords];
+    uint32_t* const T = ELDS;
+    uint8_t* const S = (uint8_t*)(ELDS + 4096);
+    uint32_t* const X = ELDS + 4352;
     const uint32_t L = laneid();
     g_u8* din = gptr(dIn) + (uint64_t)blockIdx.x * (bm + 64);
     g_u8* dsl = gptr(dSlot) + (uint64_t)blockIdx.x * (bm + 64);
+    // a relaunch after a park: first the block this wave parked with
+    uint32_t resumeB = pend[4 * blockIdx.x];
     for (;;) {
-        uint32_t b = 0;
-        if (L == 0) b = atomicAdd(next, 1u);
-        b = rdlane(b, 0);
-        const uint32_t ri = b % Rin, ro = b % Rout;
+        uint32_t b, word, sum;
         bool ended = false;
-        if (!stream_wait(inCtl + 4 * ri, b + 1, g, 2, b + 1, (int64_t)b, &ended, ticks)) return;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        const uint32_t n = min(ld_sys(inCtl + 4 * ri + 1), bm);   // (the host never publishes more)
-        wave_copy16(din, gptr(hin) + (uint64_t)ri * bm, n);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (L == 0) st_sys(inCtl + 4 * ri + 2, b + 1);   // the staging slot may be refilled
-        int32_t r;
-        if (n < (uint32_t)kLimit64K)
-            r = encode_block<true, false, false>(din, n, dsl, n, (l_u32*)T, (l_u8*)S, (l_u32*)X, (l_u8*)X + kRingE,
-                                                 nullptr);
-        else
-            [[clang::always_inline]] r = encode_block_v5<false, false, false, false, false, false, false, XC, true>(
-                din, n, dsl, n, (l_u32*)T, (l_u8*)X, nullptr);
-        WAVE_SYNC();
-        g_cu8* stored = r > 0 ? dsl : din;
-        const uint32_t sl = r > 0 ? (uint32_t)r : n;
-        const uint32_t sum = bck ? xxh32_wave(stored, sl, (l_u32*)T) : 0u;
+        if (resumeB) {
+            b = resumeB - 1;
+            word = pend[4 * blockIdx.x + 1];
+            sum = pend[4 * blockIdx.x + 2];
+            resumeB = 0;
+            pend_store(pend, 0xFFFFFFFFu, 0u, 0u);   // (seq 0: consumed)
+        } else {
+            b = 0;
+            if (L == 0) b = atomicAdd(next, 1u);
+            b = rdlane(b, 0);
+            const uint32_t ri = b % Rin;
+            if (stream_wait(inCtl + 4 * ri, b + 1, g, 2, b + 1, (int64_t)b, &ended, ticks) != kWaitOk) return;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            const uint32_t n = min(ld_sys(inCtl + 4 * ri + 1), bm);   // (the host never publishes more)
+            wave_copy16(din, gptr(hin) + (uint64_t)ri * bm, n);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (L == 0) st_sys(inCtl + 4 * ri + 2, b + 1);   // the staging slot may be refilled
+            int32_t r;
+            if constexpr (B16)
+                [[clang::always_inline]] r = encode_block_v5<false, true, true, false, false, false, false, XC, true>(
+                    din, n, dsl, n, (l_u32*)ELDS, (l_u8*)(ELDS + kE16TabWords), nullptr);
+            else if (n < (uint32_t)kLimit64K)
+                r = encode_block<true, false, false>(din, n, dsl, n, (l_u32*)T, (l_u8*)S, (l_u32*)X,
+                                                     (l_u8*)X + kRingE, nullptr);
+            else
+                [[clang::always_inline]] r = encode_block_v5<false, false, false, false, false, false, false, XC,
+                                                             true>(din, n, dsl, n, (l_u32*)T, (l_u8*)X, nullptr);
+            WAVE_SYNC();
+            word = r > 0 ? (uint32_t)r : (n | 0x80000000u);
+            sum = bck ? xxh32_wave(r > 0 ? dsl : din, r > 0 ? (uint32_t)r : n, (l_u32*)T) : 0u;
+        }
+        const uint32_t ro = b % Rout;
         // the record's slot in host memory: free once the writer wrote block b - Rout
-        if (b >= Rout && !stream_wait(outCtl + 4 * ro + 3, b - Rout + 1, g, 3, b - Rout + 1, -1, &ended, ticks)) return;
-        wave_copy16(gptr(hout) + (uint64_t)ro * bm, stored, sl);
+        if (b >= Rout) {
+            const int wr = stream_wait(outCtl + 4 * ro + 3, b - Rout + 1, g, 3, b - Rout + 1, -1, &ended, ticks);
+            if (wr != kWaitOk) {
+                if (wr == kWaitPark) pend_store(pend, b, word, sum);   // the block stays in din / dsl
+                return;
+            }
+        }
+        g_cu8* stored = (word & 0x80000000u) ? din : dsl;
+        wave_copy16(gptr(hout) + (uint64_t)ro * bm, stored, word & 0x7FFFFFFFu);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         if (L == 0) {
-            st_sys(outCtl + 4 * ro + 1, r > 0 ? (uint32_t)r : (n | 0x80000000u));
+            st_sys(outCtl + 4 * ro + 1, word);
             st_sys(outCtl + 4 * ro + 2, sum);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -3527,13 +3580,17 @@ __global__ void __launch_bounds__(64) k_encode_stream(const uint8_t* __restrict_
 }
 
 hipError_t launch_encode_stream(const uint8_t* hin, uint8_t* hout, uint32_t* inCtl, uint32_t* outCtl, uint32_t* g,
-                                uint32_t* next, uint8_t* dIn, uint8_t* dSlot, uint32_t bm, uint32_t Rin,
-                                uint32_t Rout, uint32_t waves, int bck, uint64_t ticks, hipStream_t st) {
+                                uint32_t* next, uint32_t* pend, uint8_t* dIn, uint8_t* dSlot, uint32_t bm,
+                                uint32_t Rin, uint32_t Rout, uint32_t waves, int bck, uint64_t ticks,
+                                hipStream_t st) {
     bool xc = true;
     if (const hipError_t r = encoder_path(st, &xc); r != hipSuccess) return r;
-    if (bm < (uint32_t)kLimit64K || bm > (1u << kPosBits) || !waves || !Rin || !Rout) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(xc ? k_encode_stream<true> : k_encode_stream<false>, dim3(waves), dim3(64), 0, st, hin, hout,
-                       inCtl, outCtl, g, next, dIn, dSlot, bm, Rin, Rout, bck, ticks);
+    if (bm < (64u << 10) || bm > (1u << kPosBits) || !waves || !Rin || !Rout || !pend) return hipErrorInvalidValue;
+    const bool b16 = bm < (uint32_t)kLimit64K;
+    const auto k = b16 ? (xc ? k_encode_stream<true, true> : k_encode_stream<false, true>)
+                       : (xc ? k_encode_stream<true, false> : k_encode_stream<false, false>);
+    hipLaunchKernelGGL(k, dim3(waves), dim3(64), 0, st, hin, hout, inCtl, outCtl, g, next, pend, dIn, dSlot, bm, Rin,
+                       Rout, bck, ticks);
     return hipGetLastError();
 }
 
@@ -3555,54 +3612,73 @@ hipError_t launch_encode_stream(const uint8_t* hin, uint8_t* hout, uint32_t* inC
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) k_decode_stream(const uint8_t* __restrict__ hin, uint8_t* __restrict__ hout,
                                                       uint32_t* inCtl, uint32_t* outCtl, uint32_t* g,
-                                                      uint32_t* __restrict__ next, uint8_t* __restrict__ dIn,
-                                                      uint8_t* __restrict__ dSlot, uint32_t bm, uint32_t Rin,
-                                                      uint32_t Rout, int bck, uint64_t ticks) {
+                                                      uint32_t* __restrict__ next, uint32_t* pend,
+                                                      uint8_t* __restrict__ dIn, uint8_t* __restrict__ dSlot,
+                                                      uint32_t bm, uint32_t Rin, uint32_t Rout, int bck,
+                                                      uint64_t ticks) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
     __shared__ __attribute__((aligned(16))) uint8_t win[kWinAlloc];   /* + dummy write area + hop table */
     const uint32_t L = laneid();
     g_u8* din = gptr(dIn) + (uint64_t)blockIdx.x * (bm + 64);
     g_u8* dsl = gptr(dSlot) + (uint64_t)blockIdx.x * (bm + 64);
+    // a relaunch after a park: first the block this wave parked with
+    uint32_t resumeB = pend[4 * blockIdx.x];
     for (;;) {
-        uint32_t b = 0;
-        if (L == 0) b = atomicAdd(next, 1u);
-        b = rdlane(b, 0);
-        const uint32_t ri = b % Rin, ro = b % Rout;
+        uint32_t b, status;
+        int32_t res;
         bool ended = false;
-        if (!stream_wait(inCtl + 4 * ri, b + 1, g, 2, b + 1, (int64_t)b, &ended, ticks)) return;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        const uint32_t bits = ld_sys(inCtl + 4 * ri + 1), ck = ld_sys(inCtl + 4 * ri + 2);
-        const uint32_t n = min(bits & 0x7FFFFFFFu, bm);   // (the host refuses n > bm)
-        const bool raw = (bits & 0x80000000u) != 0;
-        wave_copy16(din, gptr(hin) + (uint64_t)ri * bm, n);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (L == 0) st_sys(inCtl + 4 * ri + 3, b + 1);   // the staging slot may be refilled
-        uint32_t status = raw ? 0x100u : 0u;
-        if (bck && xxh32_wave(din, n, (l_u32*)ring) != ck) status |= 16u;
-        WAVE_SYNC();
-        int32_t res = (int32_t)n;
-        g_cu8* outp = din;
-        if (!raw) {
-            Dec<false> D;
-            D.acc = nullptr;
-            D.ts = 0;
-            D.src = din;
-            D.len = n;
-            D.dst = dsl;
-            D.physcap = bm;
-            D.ring = (l_u8*)ring;
-            D.win = (l_u8*)win;
-            D.wlo = INT64_MIN / 4;
-            D.labase = INT64_MIN / 4;
-            D.la = 0;
-            D.flushed = 0;
-            D.completed = 0;
-            D.lowP = 0;
-            res = decode_block(D, (int64_t)bm);   // cap = blockMax (src/lz4mt.cpp:645)
-            outp = dsl;
-            if (res < 0) status = 18u;   // a decode failure wins over the checksum (src/lz4mt.cpp:619-681)
+        if (resumeB) {
+            b = resumeB - 1;
+            res = (int32_t)pend[4 * blockIdx.x + 1];
+            status = pend[4 * blockIdx.x + 2];
+            resumeB = 0;
+            pend_store(pend, 0xFFFFFFFFu, 0u, 0u);   // (seq 0: consumed)
+        } else {
+            b = 0;
+            if (L == 0) b = atomicAdd(next, 1u);
+            b = rdlane(b, 0);
+            const uint32_t ri = b % Rin;
+            if (stream_wait(inCtl + 4 * ri, b + 1, g, 2, b + 1, (int64_t)b, &ended, ticks) != kWaitOk) return;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            const uint32_t bits = ld_sys(inCtl + 4 * ri + 1), ck = ld_sys(inCtl + 4 * ri + 2);
+            const uint32_t n = min(bits & 0x7FFFFFFFu, bm);   // (the host refuses n > bm)
+            const bool raw = (bits & 0x80000000u) != 0;
+            wave_copy16(din, gptr(hin) + (uint64_t)ri * bm, n);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (L == 0) st_sys(inCtl + 4 * ri + 3, b + 1);   // the staging slot may be refilled
+            status = raw ? 0x100u : 0u;
+            if (bck && xxh32_wave(din, n, (l_u32*)ring) != ck) status |= 16u;
+            WAVE_SYNC();
+            res = (int32_t)n;
+            if (!raw) {
+                Dec<false> D;
+                D.acc = nullptr;
+                D.ts = 0;
+                D.src = din;
+                D.len = n;
+                D.dst = dsl;
+                D.physcap = bm;
+                D.ring = (l_u8*)ring;
+                D.win = (l_u8*)win;
+                D.wlo = INT64_MIN / 4;
+                D.labase = INT64_MIN / 4;
+                D.la = 0;
+                D.flushed = 0;
+                D.completed = 0;
+                D.lowP = 0;
+                res = decode_block(D, (int64_t)bm);   // cap = blockMax (src/lz4mt.cpp:645)
+                if (res < 0) status = 18u;   // a decode failure wins over the checksum (src/lz4mt.cpp:619-681)
+            }
         }
-        if (b >= Rout && !stream_wait(outCtl + 4 * ro + 3, b - Rout + 1, g, 3, b - Rout + 1, -1, &ended, ticks)) return;
+        const uint32_t ro = b % Rout;
+        if (b >= Rout) {
+            const int wr = stream_wait(outCtl + 4 * ro + 3, b - Rout + 1, g, 3, b - Rout + 1, -1, &ended, ticks);
+            if (wr != kWaitOk) {
+                if (wr == kWaitPark) pend_store(pend, b, (uint32_t)res, status);   // the block stays in din / dsl
+                return;
+            }
+        }
+        g_cu8* outp = (status & 0x100u) ? din : dsl;
         if (res > 0) wave_copy16(gptr(hout) + (uint64_t)ro * bm, outp, (uint32_t)res);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -3616,11 +3692,12 @@ __global__ void __launch_bounds__(64) k_decode_stream(const uint8_t* __restrict_
 }
 
 hipError_t launch_decode_stream(const uint8_t* hin, uint8_t* hout, uint32_t* inCtl, uint32_t* outCtl, uint32_t* g,
-                                uint32_t* next, uint8_t* dIn, uint8_t* dSlot, uint32_t bm, uint32_t Rin,
-                                uint32_t Rout, uint32_t waves, int bck, uint64_t ticks, hipStream_t st) {
-    if (bm < 64 || (bm & 15) || !waves || !Rin || !Rout) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_decode_stream, dim3(waves), dim3(64), 0, st, hin, hout, inCtl, outCtl, g, next, dIn, dSlot,
-                       bm, Rin, Rout, bck, ticks);
+                                uint32_t* next, uint32_t* pend, uint8_t* dIn, uint8_t* dSlot, uint32_t bm,
+                                uint32_t Rin, uint32_t Rout, uint32_t waves, int bck, uint64_t ticks,
+                                hipStream_t st) {
+    if (bm < 64 || (bm & 15) || !waves || !Rin || !Rout || !pend) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_decode_stream, dim3(waves), dim3(64), 0, st, hin, hout, inCtl, outCtl, g, next, pend, dIn,
+                       dSlot, bm, Rin, Rout, bck, ticks);
     return hipGetLastError();
 }
 

@@ -311,6 +311,10 @@ bool ws_advance(const void* ws, WsState need, WsState next) {
     it->second = next;
     return true;
 }
+void ws_forget(const void* ws) {
+    std::lock_guard<std::mutex> g(g_ws_mu);
+    g_ws_state.erase(ws);
+}
 bool ws_is(const void* ws, WsState st) {
     std::lock_guard<std::mutex> g(g_ws_mu);
     auto it = g_ws_state.find(ws);
@@ -361,6 +365,11 @@ extern "C" Lz4MtResult lz4mtHipShardReset(uint64_t n, const Lz4MtStreamDescripto
     return LZ4MT_RESULT_OK;
 }
 
+namespace {
+Lz4MtResult shard_encode_launches(const uint8_t* src, uint64_t n, const Lz4MtStreamDescriptor* sd, const ShardWs& w,
+                                  uint32_t bm, uint64_t nb, hipStream_t st);
+}  // namespace
+
 extern "C" Lz4MtResult lz4mtHipShardEncode(const void* d_src, uint64_t n, const Lz4MtStreamDescriptor* sd, void* d_ws,
                                            uint64_t wsSize, void* stream) {
     uint32_t bm = 0;
@@ -374,7 +383,18 @@ extern "C" Lz4MtResult lz4mtHipShardEncode(const void* d_src, uint64_t n, const 
     const hipStream_t st = static_cast<hipStream_t>(stream);
     const ShardWs w = carve(static_cast<uint8_t*>(d_ws), nb, bm);
     const uint8_t* src = static_cast<const uint8_t*>(d_src);
-    if (!ws_advance(d_ws, WsState::kReset, WsState::kEncoded)) return LZ4MT_RESULT_BAD_ARG;   // not reset
+    if (!ws_is(d_ws, WsState::kReset)) return LZ4MT_RESULT_BAD_ARG;   // not reset
+    // encoded only once every launch went in: a failed launch
+    // forgets the workspace, so only a new reset makes it usable again
+    const Lz4MtResult r = shard_encode_launches(src, n, sd, w, bm, nb, st);
+    if (r == LZ4MT_RESULT_OK) ws_advance(d_ws, WsState::kReset, WsState::kEncoded);
+    else ws_forget(d_ws);
+    return r;
+}
+
+namespace {
+Lz4MtResult shard_encode_launches(const uint8_t* src, uint64_t n, const Lz4MtStreamDescriptor* sd, const ShardWs& w,
+                                  uint32_t bm, uint64_t nb, hipStream_t st) {
     if (nb == 0) return LZ4MT_RESULT_OK;
     // block checksums hashed beside the encode (k_xxh32_follow on a side
     // stream; `stream` waits for it, so the shard is complete on `stream`)
@@ -396,6 +416,13 @@ extern "C" Lz4MtResult lz4mtHipShardEncode(const void* d_src, uint64_t n, const 
     }
     return LZ4MT_RESULT_OK;
 }
+}  // namespace
+
+// Forgets a workspace's call-order state: a freed workspace
+// whose address a new allocation reuses must not inherit "encoded".  The
+// Python binding calls it when the workspace tensor is freed; a forgotten
+// workspace needs a reset before its next encode.
+extern "C" void lz4mtHipShardRelease(const void* d_ws) { ws_forget(d_ws); }
 
 extern "C" Lz4MtResult lz4mtHipShardPack(const void* d_src, uint64_t n, const Lz4MtStreamDescriptor* sd, void* d_ws,
                                          uint64_t wsSize, void* d_pack, uint64_t packCap, uint32_t perBlockCap,
@@ -510,8 +537,11 @@ extern "C" int lz4mtHipIpcAllocKind(uint64_t bytes, void** d_ptr, void* handle64
     return -1;
 }
 
+// Plain hipMalloc memory, as before lz4mtHipIpcAllocKind existed (ADVICE r05:
+// a caller that computes on the buffer keeps its L2); the push transport asks
+// for uncached memory through lz4mtHipIpcAllocKind.
 extern "C" int lz4mtHipIpcAlloc(uint64_t bytes, void** d_ptr, void* handle64) {
-    return lz4mtHipIpcAllocKind(bytes, d_ptr, handle64, 2, nullptr);
+    return lz4mtHipIpcAllocKind(bytes, d_ptr, handle64, 0, nullptr);
 }
 
 // PCI bus id ("dddd:bb:dd.f") of device `dev`, and the ordinal of the visible

@@ -574,10 +574,12 @@ class IpcPushTransport:
 
     Visibility on the root: a peer's copy-engine writes land in the root's
     HBM behind the back of its XCD L2s.  The receive buffers are uncached
-    device memory where the runtime exports such memory by IPC (no L2 line
-    of them is ever held; ``kind`` says which memory was taken), and the
-    root's k_shard_unpack starts every workgroup with a system-scope acquire
-    (buffer_inv sc0 sc1).  The setup then PROVES the path end to end: every
+    device memory (no L2 line of them is ever held); a runtime that cannot
+    export uncached memory by IPC fails the setup (IpcSetupError -> RCCL),
+    since a cached buffer could serve stale lines of an earlier round that
+    no set-up check can provoke.  The root's k_shard_unpack
+    also starts every workgroup with a system-scope acquire (buffer_inv sc0
+    sc1).  The setup then PROVES the path end to end: every
     sender pushes a seeded pattern into both of its buffers and the root
     compares the XXH32 of every 1 MiB piece with the sender's; any mismatch
     (or a failed map / peer-access check) raises IpcSetupError on every rank
@@ -620,6 +622,7 @@ class IpcPushTransport:
                         continue
                     nbytes = L.shard_pack_bound(sizes[r], sd, cap)
                     pair = []
+                    self.bufs[r] = pair
                     for _ in range(2):
                         ptr, h, k = ctypes.c_void_p(), (ctypes.c_uint8 * 64)(), ctypes.c_int(-1)
                         if L.lib.lz4mtHipIpcAllocKind(nbytes, ctypes.byref(ptr), h, 2, ctypes.byref(k)) != 0:
@@ -627,7 +630,16 @@ class IpcPushTransport:
                         pair.append(ptr.value)
                         kinds.append(k.value)
                         handles.setdefault(r, []).append(bytes(h))
-                    self.bufs[r] = pair
+                        if k.value != 2:
+                            # a cached (fine- or coarse-grained)
+                            # receive buffer can hold L2 lines from the root's
+                            # unpack two rounds back, which a system-scope
+                            # acquire does not drop for coarse-grained memory
+                            # on gfx942/950, and the set-up pattern check runs
+                            # before any such line exists -- so it cannot prove
+                            # those kinds; only uncached memory is taken
+                            raise IpcSetupError(f"the runtime exported no uncached receive buffer (got kind "
+                                                f"{k.value}); cached kinds are not used for the IPC push")
             except IpcSetupError as e:
                 err, handles = e, None
         obj = [handles, _bus_id(L, me) if rank == dst else None, min(kinds) if kinds else None]

@@ -98,6 +98,8 @@ def small_batches(monkeypatch):
     monkeypatch.setenv("LZ4MT_AMD_BATCH0_MIB", "16")
     monkeypatch.setenv("LZ4MT_AMD_BATCH_MIB", "32")
     monkeypatch.setenv("LZ4MT_AMD_SLOTS", "2")
+    # the batch engine (every block size streams by default since round 6)
+    monkeypatch.setenv("LZ4MT_AMD_STREAM", "0")
 
 
 @pytest.mark.parametrize("mode", ["DEVICE", "PARALLEL"])

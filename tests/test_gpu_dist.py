@@ -305,7 +305,7 @@ def test_ipc_setup_pattern_check_passes():
     buffers' memory kind; a streamed gather then runs over it."""
     got = _run_two(_ipc_setup_rank, False)
     assert got[0][0] == "ok" and got[1][0] == "ok", got
-    assert got[0][1] in ("uncached", "fine-grained", "coarse-grained")
+    assert got[0][1] == "uncached"   # ADVICE r05: the push takes uncached receive buffers or none
     assert got[0][2] is True
 
 
@@ -336,6 +336,48 @@ def test_bench_corrupt_ipc_falls_back_to_rccl():
                 os.environ[k] = v
     assert line["transport"].startswith("rccl (IPC setup failed") and "pattern check failed" in line["transport"]
     assert line["stitched_frame_ok"] is True and line["roundtrip_ok"] is True
+
+
+def _bench_fail(fault, deadline=300, timeout=300):
+    """bench.py --gpus 2 (gloo, both ranks on the test GPU) with a fault
+    injected by LZ4MT_BENCH_FAULT: returns (exit code, the one JSON line,
+    wall seconds)."""
+    import time
+    env = dict(os.environ, LZ4MT_BENCH_BACKEND="gloo", LZ4MT_BENCH_FAULT=fault,
+               LZ4MT_BENCH_DEADLINE_S=str(deadline))
+    env.pop("WORLD_SIZE", None)
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--gib", "0.25", "--steps", "1",
+                        "--warmup", "0", "--no-cpu-baseline"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=timeout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    return r.returncode, json.loads(lines[0]), time.monotonic() - t0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fault,stage", [("setup:1", "setup"), ("gather:1", "step"), ("step:0", "step")])
+def test_bench_n2_failure_is_one_json_line(fault, stage):
+    """an exception on any rank at N > 1 -- at set-up,
+    or mid-step between the gather and the scatter while the root waits in a
+    collective -- ends the run non-zero with ONE JSON line on rank 0 naming
+    the stage, the transport and the error, well within the deadline."""
+    rc, line, dt = _bench_fail(fault)
+    assert rc != 0
+    assert line["status"] == "failed" and line["value"] is None and line["n_gpus"] == 2
+    assert line["stage"] == stage and line["failed_rank"] == int(fault.split(":")[1])
+    assert line["transport"] == "ipc" and "injected fault" in line["error"]
+    assert line["elapsed_s"] < 120 and dt < 240
+
+
+@pytest.mark.gpu
+def test_bench_n2_hang_ends_at_the_deadline():
+    """A rank that hangs mid-step (no exception, no collective error) is
+    ended by the deadline: the same one line, 'deadline exceeded'."""
+    rc, line, dt = _bench_fail("gather:1:hang", deadline=45)
+    assert rc != 0
+    assert line["status"] == "failed" and line["stage"] == "step" and "deadline exceeded" in line["error"]
+    assert line["elapsed_s"] < 90 and dt < 240
 
 
 @pytest.mark.gpu

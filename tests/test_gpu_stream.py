@@ -27,6 +27,8 @@ L = None
 APP_F = {  # SURVEY.md App. F, 256 MiB seed 42: (sck, bck, bid) -> (frame bytes, XXH32(frame))
     (1, 0, 7): (133159140, 0x157099A8), (0, 0, 7): (133159136, 0x8AC5DBC8), (1, 1, 7): (133159396, 0xC532D9D2),
     (0, 1, 7): (133159392, 0x1686045A), (1, 0, 6): (133770948, 0x7D1BC1BA), (0, 1, 6): (133771968, 0x535404A3),
+    # round 6: 64 and 256 KiB blocks stream too (k_encode_stream's byU16 / v5 tables)
+    (1, 0, 4): (131940148, 0xFC3A55A1), (0, 1, 5): (136145906, 0xE62BB3AC),
 }
 
 
@@ -64,7 +66,7 @@ def test_streamed_tight_rings(data256, monkeypatch, rin, rout):
     codecs takes the same engine."""
     monkeypatch.setenv("LZ4MT_AMD_STREAM_IN", str(rin))
     monkeypatch.setenv("LZ4MT_AMD_STREAM_OUT", str(rout))
-    for row, m in (((0, 1, 6), L.MODE_DEVICE), ((1, 0, 7), L.MODE_PARALLEL)):
+    for row, m in (((0, 1, 6), L.MODE_DEVICE), ((1, 0, 7), L.MODE_PARALLEL), ((1, 0, 4), L.MODE_DEVICE)):
         sck, bck, bid = row
         r, frame = L.compress(data256, L.make_sd(bid, bool(sck), bool(bck)), mode=m)
         assert r == 0 and (len(frame), xxhash.xxh32(frame).intdigest()) == APP_F[row], (rin, rout, row)
@@ -82,7 +84,7 @@ def test_streamed_equals_batched(monkeypatch):
         z, k = s + 3_000_000, rnd.randrange(1, 900_000)
         data[z:z + k] = bytes(k)
     data = bytes(data[:(40 << 20) - 12345])
-    for bid, sck, bck in ((6, True, True), (7, False, True), (6, False, False)):
+    for bid, sck, bck in ((6, True, True), (7, False, True), (6, False, False), (4, False, True), (5, True, True)):
         sd = L.make_sd(bid, sck, bck)
         r1, f1 = L.compress(data, sd, mode=L.MODE_DEVICE)
         monkeypatch.setenv("LZ4MT_AMD_STREAM", "0")
@@ -557,13 +559,15 @@ def test_streamed_decompress_damaged_vs_oracle(bid, sck, bck):
         assert out == ow, (it, kind, L.result_to_string(r), len(out), len(ow))
 
 
-def _hook_io(fn, data, sd, hooks):
+def _hook_io(fn, data, sd, hooks, whooks=None):
     """lz4mtCompress / lz4mtDecompress (MODE_DEVICE) with Python callbacks;
-    hooks[k] runs inside the k-th read() call (1-based) before it returns."""
+    hooks[k] runs inside the k-th read() call (1-based) before it returns,
+    whooks[k] inside the k-th write() call."""
     from lz4mt_amd import _abi
     src = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
-    st = {"pos": 0, "r": 0}
+    st = {"pos": 0, "r": 0, "w": 0}
     out = []
+    whooks = whooks or {}
 
     def rd(ctx, dst, n):
         st["r"] += 1
@@ -575,6 +579,9 @@ def _hook_io(fn, data, sd, hooks):
         return k
 
     def wr(ctx, p, n):
+        st["w"] += 1
+        if st["w"] in whooks:
+            whooks[st["w"]]()
         out.append(ctypes.string_at(p, n))
         return n
 
@@ -606,6 +613,9 @@ def test_streamed_reader_stall_parks_the_grid(monkeypatch, capfd):
     import time
     monkeypatch.setenv("LZ4MT_AMD_STREAM_PARK_MS", "50")
     monkeypatch.setenv("LZ4MT_AMD_PIPE_TRACE", "1")
+    # every CU's LDS held by the grid (the default, 4 waves per CU, leaves
+    # half of it free, and the callback's GPU work would not need the park)
+    monkeypatch.setenv("LZ4MT_AMD_STREAM_WAVES_PER_CU", "8")
     waits = []
 
     def timed_work():
@@ -635,3 +645,131 @@ def test_streamed_reader_stall_parks_the_grid(monkeypatch, capfd):
         print(f"hook waits (s): {[round(w, 3) for w in waits]}; relaunches: {relaunches}")
     # every hook that ran while a grid was up had to wait for the park (>= 50 ms)
     assert relaunches >= 8 and sum(w >= 0.045 for w in waits) >= 8, (waits, relaunches)
+
+
+def test_streamed_writer_stall_parks_the_grid(monkeypatch, capfd):
+    """VERDICT r05 item 4 / ADVICE r05: a write() that stalls past
+    LZ4MT_AMD_STREAM_PARK_MS parks the grid too.  Waves whose block is done
+    but whose output slot is taken leave it in their HBM buffers (a pend
+    descriptor per wave), waiting waves leave, the reader publishes nothing
+    meanwhile; GPU work that needs LDS -- launched and waited for INSIDE the
+    stalled write() -- runs; when the write() returns the grid is relaunched
+    and every parked block goes out first.  With 8 waves per CU (every CU's
+    LDS held) this callback could not return without the park.  Compress and
+    decompress, tight rings (the output ring full while the writer stalls),
+    stalls early and late, a read() and a write() stalled at once."""
+    import time
+    monkeypatch.setenv("LZ4MT_AMD_STREAM_PARK_MS", "50")
+    monkeypatch.setenv("LZ4MT_AMD_STREAM_WAVES_PER_CU", "8")
+    monkeypatch.setenv("LZ4MT_AMD_PIPE_TRACE", "1")
+    waits = []
+
+    def timed_work():
+        t = time.time()
+        _lds_heavy_gpu_work()
+        waits.append(time.time() - t)
+
+    def slow_then_work():
+        time.sleep(0.1)
+        timed_work()
+
+    _lds_heavy_gpu_work()
+    data = oracle.gen_synthetic(24 << 20, 43)
+    frame = oracle.compress_frame(data, oracle.params(6, True, True))
+    for rings in ((256, 512), (8, 8)):
+        monkeypatch.setenv("LZ4MT_AMD_STREAM_IN", str(rings[0]))
+        monkeypatch.setenv("LZ4MT_AMD_STREAM_OUT", str(rings[1]))
+        # compress: three write() calls per record (size word, payload, checksum) after the header's
+        # the reader is kept busy (10 ms per read(), below the park threshold),
+        # so the grid's idle waves sit in their input waits -- holding the LDS
+        # -- while the writer stalls, as in a real pipe
+        for rh, wh in (({}, {2: timed_work}), ({}, {5: timed_work, 40: timed_work}),
+                       ({6: slow_then_work}, {8: timed_work}), ({}, {62: timed_work})):
+            rh = dict({k: (lambda: time.sleep(0.01)) for k in range(1, 26)}, **rh)
+            t0 = time.time()
+            r, got = _hook_io(L.lib.lz4mtCompress, data, L.make_sd(6, True, True), rh, wh)
+            assert r == 0 and got == frame, (rings, sorted(wh), L.result_to_string(r))
+            assert time.time() - t0 < 60
+        # decompress: one write() per decoded block
+        for rh, wh in (({}, {1: timed_work}), ({}, {3: timed_work, 14: timed_work}),
+                       ({10: slow_then_work}, {4: timed_work}), ({}, {18: timed_work})):
+            rh = dict({k: (lambda: time.sleep(0.01)) for k in range(2, 75, 3)}, **rh)   # the data reads
+            r, got = _hook_io(L.lib.lz4mtDecompress, frame, L.init_stream_descriptor(), rh, wh)
+            assert r == 0 and got == data, (rings, sorted(wh), L.result_to_string(r))
+    err = capfd.readouterr().err
+    relaunches = err.count("relaunched at block")
+    with capfd.disabled():
+        print(f"write-hook waits (s): {[round(w, 3) for w in waits]}; relaunches: {relaunches}")
+    assert "a write() stalled" in err, err[-2000:]
+    # the hooks that ran while idle waves held the LDS waited for the park
+    assert relaunches >= 8 and sum(w >= 0.045 for w in waits) >= 8, (waits, relaunches)
+
+
+def test_streamed_compress_piped_into_streamed_decompress(monkeypatch):
+    """two streamed calls of one process joined by a pipe on one
+    GPU (compress | decompress), every CU's LDS held by whichever grid runs
+    (8 waves per CU), tiny rings and a pipe far smaller than the data: each
+    grid parks while its write() / read() waits on the other, so the pair
+    completes instead of hanging; bytes exact."""
+    import os
+    import threading
+    from lz4mt_amd import _abi
+    monkeypatch.setenv("LZ4MT_AMD_STREAM_PARK_MS", "50")
+    monkeypatch.setenv("LZ4MT_AMD_STREAM_WAVES_PER_CU", "8")
+    monkeypatch.setenv("LZ4MT_AMD_STREAM_IN", "8")
+    monkeypatch.setenv("LZ4MT_AMD_STREAM_OUT", "8")
+    data = oracle.gen_synthetic(40 << 20, 44)
+    src = ctypes.create_string_buffer(bytes(data), len(data))
+    rfd, wfd = os.pipe()
+    pos = {"c": 0}
+    out = []
+    res = {}
+
+    def c_read(ctx, dst, n):
+        k = min(n, len(data) - pos["c"])
+        ctypes.memmove(dst, ctypes.addressof(src) + pos["c"], k)
+        pos["c"] += k
+        return k
+
+    def c_write(ctx, p, n):
+        b = ctypes.string_at(p, n)
+        while b:
+            b = b[os.write(wfd, b):]
+        return n
+
+    def d_read(ctx, dst, n):
+        got = 0
+        while got < n:
+            b = os.read(rfd, n - got)
+            if not b:
+                break
+            ctypes.memmove(dst + got, b, len(b))
+            got += len(b)
+        return got
+
+    def d_write(ctx, p, n):
+        out.append(ctypes.string_at(p, n))
+        return n
+
+    keep = [_abi.READ_FN(c_read), _abi.WRITE_FN(c_write), _abi.READ_FN(d_read), _abi.WRITE_FN(d_write)]
+
+    def run(kind):
+        ctx = L.init_context()
+        ctx.mode = L.MODE_DEVICE
+        if kind == "c":
+            ctx.read, ctx.write = ctypes.cast(keep[0], ctypes.c_void_p), ctypes.cast(keep[1], ctypes.c_void_p)
+            res["c"] = L.lib.lz4mtCompress(ctypes.byref(ctx), ctypes.byref(L.make_sd(6, True, True)))
+            os.close(wfd)
+        else:
+            ctx.read, ctx.write = ctypes.cast(keep[2], ctypes.c_void_p), ctypes.cast(keep[3], ctypes.c_void_p)
+            res["d"] = L.lib.lz4mtDecompress(ctypes.byref(ctx), ctypes.byref(L.init_stream_descriptor()))
+    th = [threading.Thread(target=run, args=(k,), daemon=True) for k in "cd"]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    alive = any(t.is_alive() for t in th)
+    os.close(rfd)
+    assert not alive, "compress | decompress through a pipe did not finish"
+    assert res == {"c": 0, "d": 0}, res
+    assert b"".join(out) == data
