@@ -302,6 +302,9 @@ class RunGuard:
         self.t0 = time.monotonic()
         self._lock = threading.Lock()
         self._reported = False
+        # the line goes to the process's real stdout even while a group set-up
+        # has file descriptor 1 redirected to stderr (stdout_to_stderr)
+        self._out_fd = os.dup(1)
         key = f"{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}"
         self.dir = os.path.join(tempfile.gettempdir(), f"lz4mt_bench_{key}")
         f = os.environ.get("LZ4MT_BENCH_FAULT", "").split(":")
@@ -383,7 +386,8 @@ class RunGuard:
                 "elapsed_s": round(time.monotonic() - self.t0, 3), "deadline_s": self.deadline_s,
                 "failures": [{k: r.get(k) for k in ("rank", "stage", "transport", "error", "elapsed_s")}
                              for r in recs]}
-        print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        os.write(self._out_fd, (json.dumps(line) + "\n").encode())
         try:
             open(os.path.join(self.dir, "ack"), "w").close()
         except OSError:

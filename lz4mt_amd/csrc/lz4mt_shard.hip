@@ -29,6 +29,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <mutex>
@@ -520,18 +522,34 @@ extern "C" int lz4mtHipIpcAllocKind(uint64_t bytes, void** d_ptr, void* handle64
     if (!d_ptr || !handle64) return -1;
     static_assert(sizeof(hipIpcMemHandle_t) <= 64, "ipc handle");
     const unsigned flags[3] = {0u, hipDeviceMallocFinegrained, hipDeviceMallocUncached};
+    const char* tr = getenv("LZ4MT_AMD_IPC_TRACE");
+    const bool trace = tr && atoi(tr) != 0;
+    const uint64_t n = bytes ? bytes : 1;
     for (int k = std::min(want, 2); k >= 0; --k) {
-        void* p = nullptr;
-        const hipError_t e = k == 0 ? hipMalloc(&p, bytes ? bytes : 1)
-                                    : hipExtMallocWithFlags(&p, bytes ? bytes : 1, flags[k]);
-        if (e != hipSuccess || !p) { (void)hipGetLastError(); continue; }
-        hipIpcMemHandle_t h;
-        if (hipIpcGetMemHandle(&h, p) != hipSuccess) { (void)hipGetLastError(); (void)hipFree(p); continue; }
-        memset(handle64, 0, 64);
-        memcpy(handle64, &h, sizeof(h));
-        *d_ptr = p;
-        if (kind) *kind = k;
-        return 0;
+        // each kind at the size asked for, then rounded up to 2 MiB (whole
+        // large pages of its own, never a sub-allocation of a shared chunk)
+        const uint64_t sizes[2] = {n, (n + (2ull << 20) - 1) & ~((2ull << 20) - 1)};
+        for (const uint64_t sz : sizes) {
+            void* p = nullptr;
+            const hipError_t e = k == 0 ? hipMalloc(&p, sz) : hipExtMallocWithFlags(&p, sz, flags[k]);
+            hipError_t x = hipErrorUnknown;
+            if (e == hipSuccess && p) {
+                hipIpcMemHandle_t h;
+                x = hipIpcGetMemHandle(&h, p);
+                if (x == hipSuccess) {
+                    memset(handle64, 0, 64);
+                    memcpy(handle64, &h, sizeof(h));
+                    *d_ptr = p;
+                    if (kind) *kind = k;
+                    return 0;
+                }
+                (void)hipFree(p);
+            }
+            (void)hipGetLastError();
+            if (trace)
+                fprintf(stderr, "lz4mt_amd: IPC receive buffer kind %d, %llu B: alloc %d, export %d\n", k,
+                        (unsigned long long)sz, (int)e, (int)x);
+        }
     }
     *d_ptr = nullptr;
     return -1;

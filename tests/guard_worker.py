@@ -29,7 +29,10 @@ def main():
         guard.transport = "ipc"
         for stage in ("input", "setup", "step"):
             guard.enter(stage)
-            dist.barrier()
+            # bench.py connects its control group with fd 1 redirected to
+            # stderr: a failure line printed meanwhile must still reach stdout
+            with bench.stdout_to_stderr():
+                dist.barrier()
         guard.enter("step", point="gather")
         t = torch.ones(4)
         dist.all_reduce(t)

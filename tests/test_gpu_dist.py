@@ -21,6 +21,21 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _qget(q, procs, timeout):
+    """q.get that fails at once when a rank process died without answering
+    (instead of waiting out the whole timeout while its peer blocks)."""
+    import queue
+    import time
+    t_end = time.monotonic() + timeout
+    while True:
+        try:
+            return q.get(timeout=2)
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"a rank exited with {dead} before answering"
+            assert time.monotonic() < t_end, "no answer from the ranks"
+
+
 def _bench(*args, timeout=300):
     env = dict(os.environ, LZ4MT_BENCH_BACKEND="gloo")
     env.pop("WORLD_SIZE", None)
@@ -146,7 +161,7 @@ def test_streamed_gather_on_device(n, bid, cap, kind):
     procs = [ctx.Process(target=_streamed_rank, args=(r, 2, port, n, bid, cap, kind, q)) for r in range(2)]
     for p in procs:
         p.start()
-    same, rounds, each = q.get(timeout=300)
+    same, rounds, each = _qget(q, procs, 300)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -211,7 +226,7 @@ def test_nccl_world1_streamed_gather_scatter_verify():
     q = ctx.Queue()
     p = ctx.Process(target=_nccl_world1, args=(q, (40 << 20) + 4099, 7))
     p.start()
-    backend, same, dec_ok, ok, staged = q.get(timeout=240)
+    backend, same, dec_ok, ok, staged = _qget(q, [p], 240)
     p.join(timeout=60)
     assert p.exitcode == 0
     assert backend == "nccl" and same and dec_ok and ok and staged is False
@@ -291,7 +306,7 @@ def _run_two(target, *args, timeout=240):
     procs = [ctx.Process(target=target, args=(r, 2, port, *args, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=timeout) for _ in procs)
+    got = dict(_qget(q, procs, timeout) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

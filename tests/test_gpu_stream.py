@@ -685,7 +685,7 @@ def test_streamed_writer_stall_parks_the_grid(monkeypatch, capfd):
         # -- while the writer stalls, as in a real pipe
         for rh, wh in (({}, {2: timed_work}), ({}, {5: timed_work, 40: timed_work}),
                        ({6: slow_then_work}, {8: timed_work}), ({}, {62: timed_work})):
-            rh = dict({k: (lambda: time.sleep(0.01)) for k in range(1, 26)}, **rh)
+            rh = {**{k: (lambda: time.sleep(0.01)) for k in range(1, 26)}, **rh}
             t0 = time.time()
             r, got = _hook_io(L.lib.lz4mtCompress, data, L.make_sd(6, True, True), rh, wh)
             assert r == 0 and got == frame, (rings, sorted(wh), L.result_to_string(r))
@@ -693,7 +693,7 @@ def test_streamed_writer_stall_parks_the_grid(monkeypatch, capfd):
         # decompress: one write() per decoded block
         for rh, wh in (({}, {1: timed_work}), ({}, {3: timed_work, 14: timed_work}),
                        ({10: slow_then_work}, {4: timed_work}), ({}, {18: timed_work})):
-            rh = dict({k: (lambda: time.sleep(0.01)) for k in range(2, 75, 3)}, **rh)   # the data reads
+            rh = {**{k: (lambda: time.sleep(0.01)) for k in range(2, 75, 3)}, **rh}   # the data reads
             r, got = _hook_io(L.lib.lz4mtDecompress, frame, L.init_stream_descriptor(), rh, wh)
             assert r == 0 and got == data, (rings, sorted(wh), L.result_to_string(r))
     err = capfd.readouterr().err
