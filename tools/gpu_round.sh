@@ -25,6 +25,8 @@
 #   bdref   the -BD reference-bytes tests (tests/test_gpu_bd.py -k reference)
 #   tstream the streamed callback compress tests + the callback-engine config tests
 #   nccl1   the world-size-1 nccl tests (tests/test_gpu_dist.py -k nccl)
+#   interf  k_encode at 8 vs 4 waves per CU (LDS pad) at B7 / B6: what two waves per SIMD cost each other
+#   follow  bench with the block XXH32 beside the encode (LZ4MT_AMD_FOLLOW=1) vs after it
 set -euo pipefail
 tag=$1; shift
 out=gpurun_out/$tag
@@ -185,6 +187,20 @@ for step in "$@"; do
         set -- $spec; name=$1; shift
         timeout -k 10 300 python3 bench.py --no-cpu-baseline "$@" > "$out/$name.json" 2> "$out/$name.err"
         echo "$name $(cut -c1-300 "$out/$name.json")"
+      done ;;
+    interf)  # the encoder's waves interfering on a SIMD: 8 waves per CU (2 per SIMD) vs 4 (LDS padded, 1 per SIMD)
+      for bid in 7 6; do
+        for pad in 0 20480; do
+          LZ4MT_AMD_ENC_LDS_PAD=$pad BID=$bid KTIME_NOCHECK=0 timeout -k 10 200 python3 tools/ktime.py \
+              > "$out/interf_b${bid}_pad$pad.txt" 2>&1 || { tail -5 "$out/interf_b${bid}_pad$pad.txt"; exit 1; }
+          echo "B$bid pad $pad: $(grep encode "$out/interf_b${bid}_pad$pad.txt")"
+        done
+      done ;;
+    follow)  # block XXH32 hashed beside the encode (LZ4MT_AMD_FOLLOW=1) vs after it (the default)
+      for f in 0 1; do
+        LZ4MT_AMD_FOLLOW=$f timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 \
+            > "$out/follow$f.json" 2> "$out/follow$f.err" || { tail -5 "$out/follow$f.err"; exit 1; }
+        echo "follow=$f $(cut -c1-400 "$out/follow$f.json")"
       done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
