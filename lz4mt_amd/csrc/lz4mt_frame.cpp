@@ -621,7 +621,7 @@ bool host_wait(P pred, Q stop) {
 
 // A wave of the streamed grids gives up a wait after LZ4MT_AMD_STREAM_TIMEOUT_S
 // seconds without progress (so a stuck host never pins the GPU); waiting on the
-// user's read() / write() is progress: while any callback runs, a keepalive
+// user's read() / write() is progress: while any callback runs, the monitor
 // thread bumps the liveness word g[5] every 100 ms (a stalled pipe upstream
 // or downstream is not a hang).
 // Parking: a grid holds the LDS of every CU it runs on for as long as it
@@ -633,12 +633,14 @@ bool host_wait(P pred, Q stop) {
 // block is encoded (decoded) but whose output slot is still taken leaves its
 // block in its own HBM buffers with a descriptor in dPend; waves working on
 // a block finish it and then do one of the two.  While parked the reader
-// publishes nothing (publish() below), so every block below the reader's
-// next one was taken.  Other work on the device -- a callback's own GPU
-// calls included -- can then run.  The grid is launched again, at the
-// reader's next block, once no callback is stalled any more: by the reader
-// before it publishes, or by whichever thread's stalled callback returns
-// last; each wave first finishes the block it parked with.
+// publishes nothing (publish() below, under the mutex the park is set
+// under), so every block below the reader's next one was taken.  Other work
+// on the device -- a callback's own GPU calls included -- can then run.
+// Within 10 ms of no callback being stalled any more, the monitor waits for
+// the parked grid to drain and launches it again at the reader's next block;
+// each wave first finishes the block it parked with.  The callbacks
+// themselves only stamp their start and end (atomics): the reader's one
+// publish per block is the only lock on the data path.
 uint64_t stream_wait_ticks() {
     return (uint64_t)env_int("LZ4MT_AMD_STREAM_TIMEOUT_S", 60, 1, 86400) * 100000000ull;   // 100 MHz
 }
@@ -649,40 +651,33 @@ class StreamMonitor {
         : B_(B), g_(g), launch_(launch),
           parkAfter_(std::chrono::milliseconds(env_int("LZ4MT_AMD_STREAM_PARK_MS", 200, 1, 86400000))),
           th_([this] { run(); }) {}
-    ~StreamMonitor() {
+    ~StreamMonitor() { stop(); }
+    // no relaunch after this (the call's blocks are all out, or it stops)
+    void stop() {
         { std::lock_guard<std::mutex> lk(mu_); stop_ = true; }
         cv_.notify_all();
-        th_.join();
+        if (th_.joinable()) th_.join();
     }
-    // one callback in progress for the scope's lifetime; the writer's and the
-    // reader's are timed for parking
+    // one callback in progress for the scope's lifetime (the reader's or the
+    // writer's: each is timed for parking)
     class Scope {
       public:
-        Scope(StreamMonitor& k, bool reader) : k_(k), reader_(reader) {
+        Scope(StreamMonitor& k, bool reader) : k_(k), since_(reader ? k.readSince_ : k.writeSince_) {
             k_.busy_.fetch_add(1, std::memory_order_relaxed);
-            std::lock_guard<std::mutex> lk(k_.mu_);
-            (reader_ ? k_.readSince_ : k_.writeSince_) = std::chrono::steady_clock::now();
-            (reader_ ? k_.reading_ : k_.writing_) = true;
+            since_.store(now_ns(), std::memory_order_release);
         }
-        void leave() {
-            if (done_) return;
-            done_ = true;
-            {
-                std::lock_guard<std::mutex> lk(k_.mu_);
-                (reader_ ? k_.reading_ : k_.writing_) = false;
-            }
+        ~Scope() {
+            since_.store(-1, std::memory_order_release);
             k_.busy_.fetch_sub(1, std::memory_order_relaxed);
         }
-        ~Scope() { leave(); }
 
       private:
         StreamMonitor& k_;
-        bool reader_, done_ = false;
+        std::atomic<int64_t>& since_;
     };
     // The reader publishes block b through fn() -- never while the grid is
-    // parked: then it relaunches the grid at b itself, or, while another
-    // callback is still stalled, waits for that thread to.  false: the call
-    // is stopping (abort, GPU error, failed relaunch).
+    // parked (it waits for the relaunch).  false: the call is stopping
+    // (abort, GPU error, failed relaunch).
     template <class F, class Stop>
     bool publish(uint32_t b, F fn, Stop stop) {
         for (;;) {
@@ -693,37 +688,27 @@ class StreamMonitor {
                     nextPub_ = b + 1;
                     return true;
                 }
-                if (!stalled_locked()) {
-                    if (!relaunch_locked()) return false;
-                    continue;
-                }
             }
-            if (stop()) return false;
+            if (stop() || failed()) return false;
             std::this_thread::sleep_for(std::chrono::microseconds(200));
         }
     }
-    // After a callback returned (and at the end of the input): a parked grid
-    // is launched again unless another callback is still stalled.  false:
-    // the relaunch failed.
-    bool resume() {
-        std::lock_guard<std::mutex> lk(mu_);
-        if (!parked_ || stalled_locked()) return true;
-        return relaunch_locked();
-    }
-    bool parked() {
-        std::lock_guard<std::mutex> lk(mu_);
-        return parked_;
-    }
-    uint32_t parks() const { return parks_.load(std::memory_order_relaxed); }
+    bool failed() const { return failed_.load(std::memory_order_acquire); }
 
   private:
-    bool stalled_locked() const {
-        const auto now = std::chrono::steady_clock::now();
-        return (reading_ && now - readSince_ >= parkAfter_) || (writing_ && now - writeSince_ >= parkAfter_);
+    static int64_t now_ns() {
+        return std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
     }
-    // (mu_ held: nothing is published and nothing parks meanwhile) waits for
-    // the parked grid to drain -- every wave leaves by itself -- and launches
-    // it again at the reader's next block
+    // which callback has run for at least parkAfter_ (nullptr: none)
+    const char* stalled() const {
+        const int64_t t = now_ns(), lim = std::chrono::duration_cast<std::chrono::nanoseconds>(parkAfter_).count();
+        const int64_t r = readSince_.load(std::memory_order_acquire), w = writeSince_.load(std::memory_order_acquire);
+        return (r >= 0 && t - r >= lim) ? "read()" : (w >= 0 && t - w >= lim) ? "write()" : nullptr;
+    }
+    // (mu_ held: nothing is published meanwhile) waits for the parked grid
+    // to drain -- every wave leaves by itself -- and launches it again at the
+    // reader's next block
     bool relaunch_locked() {
         if (hipStreamSynchronize(B_.st) != hipSuccess || __atomic_load_n(g_ + 4, __ATOMIC_ACQUIRE) != 0 ||
             __atomic_load_n(g_ + 1, __ATOMIC_ACQUIRE) != 0) {
@@ -739,7 +724,7 @@ class StreamMonitor {
         }
         if (const char* t = getenv("LZ4MT_AMD_PIPE_TRACE"); t && atoi(t) != 0)   // (read per event: rare)
             fprintf(stderr, "lz4mt_amd: streamed grid parked while a %s stalled; relaunched at block %u\n",
-                    lastWhy_, nextPub_);
+                    why_, nextPub_);
         return true;
     }
     void run() {
@@ -748,12 +733,15 @@ class StreamMonitor {
         for (uint32_t tick = 0; !cv_.wait_for(lk, std::chrono::milliseconds(10), [this] { return stop_; }); ++tick) {
             if (tick % 10 == 0 && busy_.load(std::memory_order_relaxed) > 0)
                 __atomic_store_n(g_ + 5, beat++, __ATOMIC_RELEASE);
-            if (!parked_ && stalled_locked()) {
-                const auto now = std::chrono::steady_clock::now();
-                lastWhy_ = (reading_ && now - readSince_ >= parkAfter_) ? "read()" : "write()";
+            if (failed()) continue;
+            const char* why = stalled();
+            if (!parked_ && why) {
+                why_ = why;
                 __atomic_store_n(g_ + 7, 1u, __ATOMIC_RELEASE);
                 parked_ = true;
-                parks_.fetch_add(1, std::memory_order_relaxed);
+            } else if (parked_ && !why && !relaunch_locked()) {
+                failed_.store(true, std::memory_order_release);
+                __atomic_store_n(g_ + 1, 1u, __ATOMIC_RELEASE);   // abort: the grid, the reader and the writer stop
             }
         }
     }
@@ -762,14 +750,14 @@ class StreamMonitor {
     std::function<hipError_t()> launch_;
     std::chrono::steady_clock::duration parkAfter_;
     std::atomic<int> busy_{0};
-    std::atomic<uint32_t> parks_{0};
+    std::atomic<int64_t> readSince_{-1}, writeSince_{-1};   // start of the running read() / write(), -1: none
+    std::atomic<bool> failed_{false};                        // a relaunch failed
     std::mutex mu_;
     std::condition_variable cv_;
     // (under mu_)
-    bool stop_ = false, reading_ = false, writing_ = false, parked_ = false;
+    bool stop_ = false, parked_ = false;
     uint32_t nextPub_ = 0;
-    const char* lastWhy_ = "read()";
-    std::chrono::steady_clock::time_point readSince_, writeSince_;
+    const char* why_ = "read()";
     std::thread th_;   // last: started once the members above exist
 };
 
@@ -821,7 +809,8 @@ bool compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
         return false;
     }
     std::atomic<uint32_t> total{0xFFFFFFFFu};   // blocks in the stream, once known
-    std::atomic<bool> wfail{false}, relaunchFail{false};
+    std::atomic<bool> wfail{false};
+    bool relaunchFail = false;
     auto gpuFailed = [&] { return ld_acq(g + 4) != 0; };
     auto stopped = [&] { return gpuFailed() || ld_acq(g + 1) != 0; };
     StreamMonitor ka(B, g, launch);
@@ -847,11 +836,6 @@ bool compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
             }
             st_rel(o + 3, b + 1);   // the slot may take block b + Rout
             st_rel(g + 3, b + 1);   // heartbeat
-            if (!ka.resume()) {     // a write() stall parked the grid: back on the device
-                relaunchFail = true;
-                st_rel(g + 1, 1u);
-                return;
-            }
         }
     });
     // the content checksum (FLG.2) is one serial XXH32 chain: a hasher
@@ -902,13 +886,12 @@ bool compress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32& x
     }
     total = b;
     st_rel(g, b);   // waves waiting for a block >= b leave
-    // a grid parked by the last read() holds blocks that still go out
-    if (!stopped() && !ka.resume()) {
-        relaunchFail = true;
-        st_rel(g + 1, 1u);
-    }
+    // (a grid parked by the last read() holds blocks that still go out: the
+    // monitor relaunches it; it stops once the writer is done)
     if (hasher.joinable()) hasher.join();
     writer.join();
+    ka.stop();
+    if (ka.failed()) relaunchFail = true;
     if (wfail || gpuFailed()) st_rel(g + 1, 1u);
     const hipError_t e = hipStreamSynchronize(B.st);
     if (e != hipSuccess || gpuFailed() || ((wfail || relaunchFail) && !s.error())) s.quit(LZ4MT_RESULT_ERROR);
@@ -1147,7 +1130,8 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
         return false;
     }
     std::atomic<uint32_t> total{0xFFFFFFFFu};
-    std::atomic<bool> wfail{false}, relaunchFail{false};
+    std::atomic<bool> wfail{false};
+    bool relaunchFail = false;
     std::atomic<uint32_t> hashed{0};
     auto gpuFailed = [&] { return ld_acq(g + 4) != 0; };
     auto stopped = [&] { return gpuFailed() || ld_acq(g + 1) != 0; };
@@ -1203,11 +1187,6 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
             }
             st_rel(o + 3, b + 1);   // the slot may take block b + Rout
             st_rel(g + 3, b + 1);   // heartbeat
-            if (!ka.resume()) {     // a write() stall parked the grid: back on the device
-                relaunchFail = true;
-                st_rel(g + 1, 1u);
-                return;
-            }
         }
     });
     // the reader: every read on this thread (the batch engine's record checks)
@@ -1245,16 +1224,15 @@ bool decompress_streamed(Session& s, const Lz4MtStreamDescriptor* sd, HostXxh32&
     }
     total = b;
     st_rel(g, b);   // waves waiting for a block >= b leave
-    // a grid parked by the last read() holds blocks that still go out
-    if (!stopped() && !ka.resume()) {
-        relaunchFail = true;
-        st_rel(g + 1, 1u);
-    }
+    // (a grid parked by the last read() holds blocks that still go out: the
+    // monitor relaunches it; it stops once the writer is done)
     writer.join();
     if (hasher.joinable()) {
         if (s.error() || s.quitting() || wfail) st_rel(g + 1, 1u);
         hasher.join();
     }
+    ka.stop();
+    if (ka.failed()) relaunchFail = true;
     if (wfail || gpuFailed()) st_rel(g + 1, 1u);
     const hipError_t e = hipStreamSynchronize(B.st);
     if (e != hipSuccess || gpuFailed() || ((wfail || relaunchFail) && !s.error())) s.quit(LZ4MT_RESULT_ERROR);
