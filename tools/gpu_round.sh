@@ -26,7 +26,6 @@
 #   tstream the streamed callback compress tests + the callback-engine config tests
 #   nccl1   the world-size-1 nccl tests (tests/test_gpu_dist.py -k nccl)
 #   interf  k_encode at 8 vs 4 waves per CU (LDS pad) at B7 / B6: what two waves per SIMD cost each other
-#   follow  bench with the block XXH32 beside the encode (LZ4MT_AMD_FOLLOW=1) vs after it
 set -euo pipefail
 tag=$1; shift
 out=gpurun_out/$tag
@@ -135,7 +134,7 @@ for step in "$@"; do
     ab)
       bash tools/ab.sh > "$out/ab.txt" 2>&1 && bash tools/ab.sh >> "$out/ab.txt" 2>&1
       cat "$out/ab.txt" ;;
-    follow)   # block checksums beside the encode (default) vs after it (LZ4MT_AMD_FOLLOW=0), twice each
+    follow)   # block checksums beside the encode (LZ4MT_AMD_FOLLOW=1) vs after it (the default), twice each
       for k in 1 2; do
         for f in 1 0; do
           LZ4MT_AMD_FOLLOW=$f timeout -k 10 120 python3 -u tools/ktime.py 2>&1 | grep -v amdgpu | sed "s/^/FOLLOW=$f /" \
@@ -195,12 +194,6 @@ for step in "$@"; do
               > "$out/interf_b${bid}_pad$pad.txt" 2>&1 || { tail -5 "$out/interf_b${bid}_pad$pad.txt"; exit 1; }
           echo "B$bid pad $pad: $(grep encode "$out/interf_b${bid}_pad$pad.txt")"
         done
-      done ;;
-    follow)  # block XXH32 hashed beside the encode (LZ4MT_AMD_FOLLOW=1) vs after it (the default)
-      for f in 0 1; do
-        LZ4MT_AMD_FOLLOW=$f timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 \
-            > "$out/follow$f.json" 2> "$out/follow$f.err" || { tail -5 "$out/follow$f.err"; exit 1; }
-        echo "follow=$f $(cut -c1-400 "$out/follow$f.json")"
       done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
