@@ -28,16 +28,17 @@
 #include "../../include/lz4mt_io.h"
 
 namespace {
-constexpr size_t kParMin = 2u << 20;     // smaller transfers stay on the caller
-
-// LZ4MT_AMD_COPY_THREADS / LZ4MT_AMD_COPY_PIECE_KIB: the copy pool's width
-// (caller included) and the smallest piece a transfer is split into
+// LZ4MT_AMD_COPY_THREADS / LZ4MT_AMD_COPY_PIECE_KIB / LZ4MT_AMD_COPY_MIN_KIB:
+// the copy pool's width (caller included), the smallest piece a transfer is
+// split into, and the smallest transfer that is split at all (smaller ones
+// stay on the caller)
 size_t env_size(const char* name, size_t dflt, size_t lo, size_t hi) {
     const char* e = getenv(name);
     const long long v = e ? atoll(e) : (long long)dflt;
     return v < (long long)lo ? lo : ((size_t)v > hi ? hi : (size_t)v);
 }
 const size_t kPiece = env_size("LZ4MT_AMD_COPY_PIECE_KIB", 1024, 64, 1 << 20) << 10;
+const size_t kParMin = env_size("LZ4MT_AMD_COPY_MIN_KIB", 2048, 64, 1 << 20) << 10;
 
 // Persistent helper threads; run(n, f) calls f(0..n-1) on the helpers and
 // the caller and returns when all are done.  Safe for concurrent callers
