@@ -791,19 +791,26 @@ template <bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false> str
 };
 
 // one encoded sequence whose bytes are stored during the next round trip
-// (few loop-carried fields; the layout is derived at store time)
+// (few loop-carried fields; the layout is derived at store time).  The
+// extension lengths come from the window, which computes them for its own
+// output cursor anyway: the layout then needs no division by 255 (two
+// quarter-rate v_mul_hi_u32 and two v_mad_u64_u32 fewer per sequence); with
+// the do-while byte rounds below and the hash input read without an else
+// branch, k_encode 151.1 -> 146.7 ms at 8 GiB B7 (136.3 vs 139.6 at B6;
+// profiles/r06/r06k_trim_ab.txt)
 struct PendSeq {
     uint32_t op, lit, mcf, off, anchor;
+    uint32_t litExt, mlExt;   // ext_len(lit), ext_len(mcf)
 };
 struct SeqLayout {
     uint32_t total, a1, a2, token, litRem, mlRem, off;
     __device__ __forceinline__ explicit SeqLayout(const PendSeq& e) {
-        a1 = 1 + ext_len(e.lit);
+        a1 = 1 + e.litExt;
         a2 = a1 + e.lit;
-        total = a2 + 2 + ext_len(e.mcf);
+        total = a2 + 2 + e.mlExt;
         token = ((e.lit < 15 ? e.lit : 15) << 4) | (e.mcf < 15 ? e.mcf : 15);
-        litRem = e.lit + 240 - 255 * (a1 - 1);   // (lit - 15) % 255 when an extension exists
-        mlRem = e.mcf + 240 - 255 * ext_len(e.mcf);
+        litRem = e.lit + 240 - __umul24(255u, e.litExt);   // (lit - 15) % 255 when an extension exists
+        mlRem = e.mcf + 240 - __umul24(255u, e.mlExt);
         off = e.off;
     }
 };
@@ -829,11 +836,14 @@ __device__ __forceinline__ void store_pend(const PendSeq& p, const SrcRing& V, g
     // the layout in VALU (uniform values in VGPRs): the scalar unit is the
     // CU's busiest port in the encoder window, the vector ALU is not
     PendSeq q = p;
-    asm volatile("" : "+v"(q.lit), "+v"(q.mcf), "+v"(q.off));
+    asm volatile("" : "+v"(q.lit), "+v"(q.mcf), "+v"(q.off), "+v"(q.litExt), "+v"(q.mlExt));
     const SeqLayout e(q);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane((int)e.total);
+    // a sequence is at least 5 bytes: the first round always runs (no
+    // zero-trip test before the loop)
     if (p.anchor >= V.B && p.anchor + p.lit <= V.B + kSR) {
-        for (uint32_t base = 0; base < total; base += 64) {
+        uint32_t base = 0;
+        do {
             const uint32_t x = min(base + L, e.total - 1);   // lanes past the end repeat the last byte
             uint32_t lv = V.r[(p.anchor + x - e.a1) & (kSR - 1)];
             asm volatile("" : "+v"(lv));
@@ -841,14 +851,17 @@ __device__ __forceinline__ void store_pend(const PendSeq& p, const SrcRing& V, g
             // reach HBM uncombined, profiles/r03s_enc_nt_ab.txt; with no
             // stores at all the encoder is only 1.4 % faster)
             d[p.op + x] = (uint8_t)pend_byte(e, x, lv);
-        }
+            base += 64;
+        } while (base < total);
     } else {   // literals no longer (or not yet) in the ring: global bytes
-        for (uint32_t base = 0; base < total; base += 64) {
+        uint32_t base = 0;
+        do {
             const uint32_t x = min(base + L, e.total - 1);
             uint32_t lv = s[(x >= e.a1 && x < e.a2) ? p.anchor + x - e.a1 : p.anchor];
             asm volatile("" : "+v"(lv));
             d[p.op + x] = (uint8_t)pend_byte(e, x, lv);
-        }
+            base += 64;
+        } while (base < total);
     }
 }
 
@@ -1011,10 +1024,13 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         const uint32_t lo = insOn ? insPos : sBase;
         const uint32_t hi = (sHi < mflimitP1 ? sHi : mflimitP1) + 8;
         uint64_t v8;
-        if (hi - lo <= 1024) {
-            V.cover(hi);
-            v8 = V.rd8(p);
-        } else {   // wide window (long searches): hash inputs straight from global
+        // two if-regions and no else: the ring read is issued on both paths
+        // (wasted, harmless, in the rare wide case), so the common path
+        // carries no structurizer flow variable
+        const bool wide = hi - lo > 1024;
+        if (!wide) V.cover(hi);
+        v8 = V.rd8(p);
+        if (wide) {   // wide window (long searches): hash inputs straight from global
             if (ST) acc[13] += 1;
             v8 = gld8u(s + (p < n - 8 ? p : n - 8));
             uint32_t a = (uint32_t)v8, b = (uint32_t)(v8 >> 32);
@@ -1242,6 +1258,8 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             pe.anchor = anchor;
             {
                 const uint32_t litExt = ext_len(lit), mlExt = ext_len(mcf);
+                pe.litExt = litExt;
+                pe.mlExt = mlExt;
                 // 1.9.3's limitedOutput margins; both hold whenever
                 // op + 2 (lit + mcf) + 16 <= cap, so the exact test runs rarely
                 if (op + 2 * (lit + mcf) + 16 > capL) {
