@@ -116,10 +116,15 @@ public:
 
 int pieces(size_t n) { return (int)std::min<size_t>((size_t)CopyPool::get().width(), n / kPiece); }
 
+// a piece of n split k ways, page-aligned: ceil(n / k) rounded up to 4 KiB
+// (rounding floor(n / k) up dropped the last n % k bytes whenever n / k was
+// already a multiple of 4 KiB, e.g. n = 4 MiB + 3 over 4 pieces)
+size_t piece_len(size_t n, int k) { return ((n + (size_t)k - 1) / (size_t)k + 4095) & ~(size_t)4095; }
+
 void par_copy(void* dst, const void* src, size_t n) {
     if (n < kParMin) { memcpy(dst, src, n); return; }
     const int k = pieces(n);
-    const size_t per = (n / (size_t)k + 4095) & ~(size_t)4095;
+    const size_t per = piece_len(n, k);
     CopyPool::get().run(k, [=](int i) {
         const size_t o = (size_t)i * per;
         if (o < n) memcpy(static_cast<char*>(dst) + o, static_cast<const char*>(src) + o, std::min(per, n - o));
@@ -130,7 +135,7 @@ void par_copy(void* dst, const void* src, size_t n) {
 // from the start (stops at the first short piece, like one big call)
 size_t par_pio(int fd, void* buf, size_t n, off_t off, bool wr) {
     const int k = pieces(n);
-    const size_t per = (n / (size_t)k + 4095) & ~(size_t)4095;
+    const size_t per = piece_len(n, k);
     std::vector<size_t> got((size_t)k, 0);
     CopyPool::get().run(k, [&](int i) {
         const size_t o = (size_t)i * per;

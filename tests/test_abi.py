@@ -234,6 +234,44 @@ def test_large_transfers_through_io_bindings(tmp_path):
     assert outb.raw[:len(data)] == data
 
 
+def test_copy_pool_split_keeps_the_last_bytes(tmp_path):
+    """Transfers whose size over the piece count is a whole number of pages
+    plus a remainder (2 MiB + 1 over 2 pieces, 3 MiB + 2 over 3, 4 MiB + 3
+    over 4): every byte lands, by the memory and the cstdio bindings."""
+    import random
+    sizes = [(2 << 20) + 1, (3 << 20) + 2, (4 << 20) + 3, (8 << 20) + 7, (2 << 20) + 4097]
+    rnd = random.Random(11)
+    data = rnd.randbytes(sum(sizes))
+    inb = ctypes.create_string_buffer(data, len(data))
+    outb = ctypes.create_string_buffer(len(data))
+    io = _abi.Lz4MtMemIo(ctypes.cast(inb, ctypes.c_void_p).value, len(data), 0, 0,
+                         ctypes.cast(outb, ctypes.c_void_p).value, len(data), 0)
+    ctx = L.init_context()
+    L.lib.lz4mtMemBind(ctypes.byref(ctx), ctypes.byref(io))
+    rd, wr = _abi.READ_FN(ctx.read), _abi.WRITE_FN(ctx.write)
+    pos = 0
+    for size in sizes:
+        buf = ctypes.create_string_buffer(size)
+        assert rd(ctypes.byref(ctx), ctypes.cast(buf, ctypes.c_void_p), size) == size
+        assert buf.raw == data[pos:pos + size], size
+        assert wr(ctypes.byref(ctx), ctypes.cast(buf, ctypes.c_void_p), size) == size
+        pos += size
+    assert outb.raw == data
+
+    src = tmp_path / "in.bin"
+    src.write_bytes(data)
+    ctx = L.init_context()
+    L.lib.lz4mtIoBindCstdio(ctypes.byref(ctx))
+    assert L.lib.lz4mtIoOpenIstream(ctypes.byref(ctx), str(src).encode())
+    pos = 0
+    for size in sizes:
+        buf = ctypes.create_string_buffer(size)
+        assert L.lib.lz4mtIoRead(ctypes.byref(ctx), buf, size) == size
+        assert buf.raw == data[pos:pos + size], size
+        pos += size
+    L.lib.lz4mtIoCloseIstream(ctypes.byref(ctx))
+
+
 @pytest.mark.parametrize("mode", [L.MODE_SEQUENTIAL, L.MODE_PARALLEL])
 def test_host_engine_stream_size_field(golden_inputs, cpu_codec, mode):
     """FLG.3 (content size): header written as the reference does, frame
