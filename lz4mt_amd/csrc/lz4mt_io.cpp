@@ -31,14 +31,16 @@ namespace {
 // LZ4MT_AMD_COPY_THREADS / LZ4MT_AMD_COPY_PIECE_KIB / LZ4MT_AMD_COPY_MIN_KIB:
 // the copy pool's width (caller included), the smallest piece a transfer is
 // split into, and the smallest transfer that is split at all (smaller ones
-// stay on the caller)
+// stay on the caller).  512 KiB / 256 KiB: 1 MiB-block records split 4-8
+// ways (e2e B6 decompress 27-31 GiB/s vs 18-23 at 2 MiB / 1 MiB, B7 35 vs
+// 31-33); 256 KiB / 128 KiB costs B5 a quarter (profiles/r06/r06n_copy_split_ab.txt)
 size_t env_size(const char* name, size_t dflt, size_t lo, size_t hi) {
     const char* e = getenv(name);
     const long long v = e ? atoll(e) : (long long)dflt;
     return v < (long long)lo ? lo : ((size_t)v > hi ? hi : (size_t)v);
 }
-const size_t kPiece = env_size("LZ4MT_AMD_COPY_PIECE_KIB", 1024, 64, 1 << 20) << 10;
-const size_t kParMin = env_size("LZ4MT_AMD_COPY_MIN_KIB", 2048, 64, 1 << 20) << 10;
+const size_t kPiece = env_size("LZ4MT_AMD_COPY_PIECE_KIB", 256, 64, 1 << 20) << 10;
+const size_t kParMin = env_size("LZ4MT_AMD_COPY_MIN_KIB", 512, 64, 1 << 20) << 10;
 
 // Persistent helper threads; run(n, f) calls f(0..n-1) on the helpers and
 // the caller and returns when all are done.  Safe for concurrent callers

@@ -193,7 +193,7 @@ def test_cstdio_adapters(tmp_path, golden_inputs, cpu_codec):
 
 
 def test_large_transfers_through_io_bindings(tmp_path):
-    """Reads/writes >= 2 MiB go through the copy pool (parallel memcpy /
+    """Large reads/writes go through the copy pool (parallel memcpy /
     pread / pwrite); bytes, positions and fread/feof semantics must not change."""
     import random
     rnd = random.Random(7)
@@ -236,10 +236,10 @@ def test_large_transfers_through_io_bindings(tmp_path):
 
 def test_copy_pool_split_keeps_the_last_bytes(tmp_path):
     """Transfers whose size over the piece count is a whole number of pages
-    plus a remainder (2 MiB + 1 over 2 pieces, 3 MiB + 2 over 3, 4 MiB + 3
-    over 4): every byte lands, by the memory and the cstdio bindings."""
+    plus a remainder (with 8 pieces: 1 MiB + 1, 2 MiB + 1, 3 MiB + 2, ...):
+    every byte lands, by the memory and the cstdio bindings."""
     import random
-    sizes = [(2 << 20) + 1, (3 << 20) + 2, (4 << 20) + 3, (8 << 20) + 7, (2 << 20) + 4097]
+    sizes = [(1 << 20) + 1, (2 << 20) + 1, (3 << 20) + 2, (4 << 20) + 3, (8 << 20) + 7, (2 << 20) + 4097]
     rnd = random.Random(11)
     data = rnd.randbytes(sum(sizes))
     inb = ctypes.create_string_buffer(data, len(data))
