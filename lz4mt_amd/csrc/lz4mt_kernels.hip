@@ -802,21 +802,27 @@ struct PendSeq {
     uint32_t op, lit, mcf, off, anchor;
     uint32_t litExt, mlExt;   // ext_len(lit), ext_len(mcf)
 };
-struct SeqLayout {
+template <bool R8> struct SeqLayout {
     uint32_t total, a1, a2, token, litRem, mlRem, off;
     __device__ __forceinline__ explicit SeqLayout(const PendSeq& e) {
         a1 = 1 + e.litExt;
         a2 = a1 + e.lit;
         total = a2 + 2 + e.mlExt;
         token = ((e.lit < 15 ? e.lit : 15) << 4) | (e.mcf < 15 ? e.mcf : 15);
-        litRem = e.lit + 240 - __umul24(255u, e.litExt);   // (lit - 15) % 255 when an extension exists
-        mlRem = e.mcf + 240 - __umul24(255u, e.mlExt);
+        if (R8) {   // (lit - 15) % 255 mod 256, as it is stored (-255 = 1 mod 256): no multiply
+            litRem = e.lit + 240 + e.litExt;
+            mlRem = e.mcf + 240 + e.mlExt;
+        } else {    // (lit - 15) % 255 when an extension exists
+            litRem = e.lit + 240 - __umul24(255u, e.litExt);
+            mlRem = e.mcf + 240 - __umul24(255u, e.mlExt);
+        }
         off = e.off;
     }
 };
 // byte x of a sequence: token | literal-length ext | literals | offset | match-length ext
 // (flat selects: a nested ?: here is turned into an EXEC-mask branch)
-__device__ __forceinline__ uint32_t pend_byte(const SeqLayout& e, uint32_t x, uint32_t litByte) {
+template <bool R8>
+__device__ __forceinline__ uint32_t pend_byte(const SeqLayout<R8>& e, uint32_t x, uint32_t litByte) {
     const uint32_t vM = x + 1 < e.total ? 255u : e.mlRem;
     const uint32_t vL = x + 1 < e.a1 ? 255u : e.litRem;
     const uint32_t vO = x == e.a2 ? e.off & 255u : e.off >> 8;
@@ -830,6 +836,7 @@ __device__ __forceinline__ uint32_t pend_byte(const SeqLayout& e, uint32_t x, ui
 // stays selects (no load sunk into a branch) and the store waits only on the
 // counter of its own load: LDS (ring, the common case) never waits on the
 // round-trip loads in flight.
+template <bool R8>
 __device__ __forceinline__ void store_pend(const PendSeq& p, const SrcRing& V, g_cu8* __restrict__ s,
                                            g_u8* __restrict__ d) {
     const uint32_t L = laneid();
@@ -837,7 +844,7 @@ __device__ __forceinline__ void store_pend(const PendSeq& p, const SrcRing& V, g
     // CU's busiest port in the encoder window, the vector ALU is not
     PendSeq q = p;
     asm volatile("" : "+v"(q.lit), "+v"(q.mcf), "+v"(q.off), "+v"(q.litExt), "+v"(q.mlExt));
-    const SeqLayout e(q);
+    const SeqLayout<R8> e(q);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane((int)e.total);
     // a sequence is at least 5 bytes: the first round always runs (no
     // zero-trip test before the loop)
@@ -971,7 +978,13 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     // (the layout is settled right after the count: deferring it into the
     // next round trip's shadow cost 3.2 ms, profiles/r04late_encoder_layout_ab.txt)
     auto store_pending = [&]() {
-        store_pend(pe, V, s, d);
+        // remainders mod 256 without a multiply: B4 -2.6 %, B5 -1.4 %; on the
+        // byU32 encoder +0.5 % (profiles/r06/r06pq_quarter_rate_ab.txt)
+#ifndef LZ4MT_EXP_R8ALL
+        store_pend<U16 || P17>(pe, V, s, d);
+#else
+        store_pend<LZ4MT_EXP_R8ALL != 0>(pe, V, s, d);
+#endif
         havePe = false;
     };
     // window: lane 0 INSERT insPos, lane 1 TEST testPos, lane L >= 2 SEARCH

@@ -1,5 +1,6 @@
 """Quick parity screen of an A/B build (LZ4MT_AMD_LIB=exp_libs/<v>.so): frames
-of App. F text and a collision-heavy mixed input at block ids 4..7 against
+of App. F text, a collision-heavy mixed input, random bytes and words of a
+small random vocabulary at block ids 4..7 against
 the CPU oracle, plus the 256 MiB B7 -Sx -BX known answer.  Prints one line;
 exit 1 on a mismatch.  (The full parity suite runs on the build that is
 kept: tools/gpu_round.sh abtest / tests.)"""
@@ -22,8 +23,15 @@ def main():
     for s in range(0, len(mixed), 1 << 20):   # 3-letter stretches: many same-bucket collisions
         for i in range(s, s + 200_000):
             mixed[i] = 97 + rnd.randrange(3)
+    # every byte value in every hash-input position: random bytes, and words
+    # drawn from a small random vocabulary (many matches, varied 5-byte keys)
+    rand = rnd.randbytes(6 << 20)
+    vocab = [rnd.randbytes(rnd.randrange(3, 12)) for _ in range(4000)]
+    words = bytearray()
+    while len(words) < (6 << 20):
+        words += vocab[rnd.randrange(len(vocab))]
     bad = []
-    for label, data in (("appf", syn), ("mixed", bytes(mixed))):
+    for label, data in (("appf", syn), ("mixed", bytes(mixed)), ("random", rand), ("vocab", bytes(words[:6 << 20]))):
         src = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
         for bid in (4, 5, 6, 7):
             for sck, bck in ((False, True), (True, False)):
