@@ -225,6 +225,10 @@ uint64_t lz4mtHipShardBodyBytes(uint64_t n, const Lz4MtStreamDescriptor* sd, voi
  * / batch dependent copies, batch group + far copies, batches, total,
  * matches, far matches, batch sequences, serial-path sequences, -...]. */
 int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* stats16, void* stream);
+/* The same counters per block, unsummed: perBlock16 holds ceil(n /
+ * blockSize) x 16 words (block b at 16 b).  0, or -1. */
+int lz4mtHipDebugEncodeBlockStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* perBlock16,
+                                  void* stream);
 /* The frame path's block encoder alone over blocks of any size 65 547 B ..
  * 4 MiB (frames use 64 KiB .. 4 MiB by 4x steps; the others are timing
  * points of a split parse, tools/occ_sweep.py).  d_slots: nb x blockSize +

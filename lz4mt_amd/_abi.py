@@ -135,6 +135,7 @@ PROTOTYPES = {
     "lz4mtHipCopyAsync": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     "lz4mtHipShardBodyBytes": (c_uint64, [c_uint64, SD_P, c_void_p, c_uint64, c_void_p]),
     "lz4mtHipDebugEncodeStats": (c_int, [c_void_p, c_uint64, c_uint32, ctypes.POINTER(c_uint64), c_void_p]),
+    "lz4mtHipDebugEncodeBlockStats": (c_int, [c_void_p, c_uint64, c_uint32, ctypes.POINTER(c_uint64), c_void_p]),
     "lz4mtHipDebugEncode": (c_int, [c_void_p, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p]),
     "lz4mtHipCheckEncoderOrder": (c_int, []),
     "lz4mtHipEncoderProbe": (c_int, []),

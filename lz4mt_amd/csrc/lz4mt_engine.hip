@@ -1234,8 +1234,11 @@ extern "C" int lz4mtHipDebugEncodeOverlap(const void* d_src, uint64_t n, uint32_
                ? 0 : -1;
 }
 
-extern "C" int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* stats16,
-                                        void* stream) {
+namespace {
+// k_encode_stats over [d_src, d_src + n); per-block counters (16 words per
+// block) into perBlock when given, their sums into stats16 when given
+int encode_stats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* stats16, uint64_t* perBlock,
+                 void* stream) {
     if (!have_device() || blockSize == 0) return -1;
     const hipStream_t st = static_cast<hipStream_t>(stream);
     const uint64_t nb = (n + blockSize - 1) / blockSize;
@@ -1251,14 +1254,28 @@ extern "C" int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t 
         std::vector<uint64_t> h(nb * 16);
         if (hipMemcpyAsync(h.data(), dst, nb * 128, hipMemcpyDeviceToHost, st) == hipSuccess &&
             hipStreamSynchronize(st) == hipSuccess) {
-            for (int i = 0; i < 16; ++i) stats16[i] = 0;
-            for (uint64_t b = 0; b < nb; ++b)
-                for (int i = 0; i < 16; ++i) stats16[i] += h[b * 16 + i];
+            if (stats16) {
+                for (int i = 0; i < 16; ++i) stats16[i] = 0;
+                for (uint64_t b = 0; b < nb; ++b)
+                    for (int i = 0; i < 16; ++i) stats16[i] += h[b * 16 + i];
+            }
+            if (perBlock) std::copy(h.begin(), h.end(), perBlock);
             rc = 0;
         }
     }
     hipFree(slots); hipFree(cs); hipFree(dst);
     return rc;
+}
+}  // namespace
+
+extern "C" int lz4mtHipDebugEncodeStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* stats16,
+                                        void* stream) {
+    return encode_stats(d_src, n, blockSize, stats16, nullptr, stream);
+}
+
+extern "C" int lz4mtHipDebugEncodeBlockStats(const void* d_src, uint64_t n, uint32_t blockSize, uint64_t* perBlock16,
+                                             void* stream) {
+    return perBlock16 ? encode_stats(d_src, n, blockSize, nullptr, perBlock16, stream) : -1;
 }
 
 extern "C" int lz4mtHipDebugDecodeStats(const void* d_frame, uint64_t frameSize, uint64_t* stats16, void* stream) {

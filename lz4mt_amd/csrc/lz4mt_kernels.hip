@@ -913,6 +913,57 @@ __device__ __forceinline__ void publish_progress(uint32_t* pub, uint32_t v) {
 // check fails (or LZ4MT_AMD_ENC_PROBE=readback forces it).
 // DUP: no effect on the code; a separate instantiation for a kernel that
 // must not share (and so outline) another kernel's one (k_encode_stream).
+// SIMD-mate priority (encode_block_v5, byU32 blocks >= 1 MiB).  The waves
+// sharing a SIMD issue oldest first, so with one generation of 2048 blocks
+// (8 GiB of 4 MiB blocks, 8 waves per CU) the younger wave of each pair is
+// starved while both run: slot-0 blocks ended at 118.6 ms on average,
+// slot-1 blocks at 137.9, and the kernel at 146.3 (per-block wall clocks of
+// the product kernel, profiles/r06/r06t_tail.txt).  Each wave publishes
+// its projected finish time (a 100 MHz wall clock, linear in its input
+// progress) every 1/128 of its block and takes the SIMD's issue priority
+// (s_setprio by rank) while it is projected to finish after its SIMD-mates,
+// so pairs end together: k_encode 146.0 -> 139.8 ms at B7, 136.2 -> 132.5
+// at B6; at B5 / B4 (many generations, 2-3 and 1-2 waves per SIMD) it cost
+// 2-5 %, so it is not used there (profiles/r06/r06tu_simd_priority_ab.txt).
+// Slots: [SIMD key: XCC, SE, SH, CU, SIMD] x 16 wave slots.  A finished wave
+// clears its slot; a slot whose projected finish is already past (a previous
+// launch) is not a live SIMD-mate, so no reset between launches is needed.
+constexpr uint32_t kPrioSimds = 8 * 8 * 2 * 16 * 4;
+__device__ uint32_t g_simdFinish[kPrioSimds * 16];
+struct SimdPrio {
+    uint32_t base, slot;   // this SIMD's 16 slots, this wave's slot
+    uint64_t t0;
+    __device__ __forceinline__ void start() {
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
+        const uint32_t key = ((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15)) * 4 +
+                             ((hw >> 4) & 3);
+        base = key * 16;
+        slot = hw & 15;
+        t0 = __builtin_amdgcn_s_memrealtime();
+    }
+    // done / total of this wave's bytes are parsed
+    __device__ __forceinline__ void tick(uint32_t done, uint32_t total) const {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        const float frac = (float)done / (float)total;
+        const uint32_t fin = (uint32_t)t0 + (uint32_t)((float)(uint32_t)(now - t0) / (frac > 1e-3f ? frac : 1e-3f));
+        const uint32_t L = laneid();
+        if (L == 0) __hip_atomic_store(g_simdFinish + base + slot, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t e = L < 16 ? __hip_atomic_load(g_simdFinish + base + L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0u;
+        // live SIMD-mates projected to finish before this wave
+        const bool live = L < 16 && L != slot && (int32_t)(e - (uint32_t)now) > 0;
+        const uint32_t rank = (uint32_t)__builtin_popcountll(bal(live && (int32_t)(e - fin) < 0));
+        if (rank >= 3) __builtin_amdgcn_s_setprio(3);
+        else if (rank == 2) __builtin_amdgcn_s_setprio(2);
+        else if (rank == 1) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+    }
+    __device__ __forceinline__ void done() const {
+        if (laneid() == 0) __hip_atomic_store(g_simdFinish + base + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_setprio(0);
+    }
+};
 template <bool ST, bool U16, bool SPLIT = false, bool LINK = false, bool P17 = false, bool PUB = false,
           bool XH = false, bool XCHG = true, bool DUP = false>
 __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __restrict__ d, uint32_t cap,
@@ -966,6 +1017,20 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     }
     SrcRing V{s, n, R, 0, 0, 0};
     V.init(o0);
+    // SIMD-mate priority: the byU32 encoder on blocks of 1 MiB and more
+    // (LZ4MT_NO_SIMD_PRIO: off, for A/B builds)
+#ifndef LZ4MT_NO_SIMD_PRIO
+    constexpr bool kPrioT = !ST && !U16 && !SPLIT && !LINK && !P17 && !XH;
+#else
+    constexpr bool kPrioT = false;
+#endif
+    const bool prioOn = kPrioT && blen >= (1u << 20);
+    SimdPrio prio{};
+    uint32_t tickShift = 31;
+    if (prioOn) {
+        prio.start();
+        tickShift = (31 - __builtin_clz(blen)) - 7;   // a check every 1/128 of the block
+    }
     const uint32_t capL = limited ? cap : 0xFFFFFFFFu;   // one SGPR for the per-sequence margin test
     const uint32_t mflimitP1 = n - kMfLimit + 1;
     const uint32_t matchlimit = n - kLastLiterals;
@@ -1041,7 +1106,15 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
         // (wasted, harmless, in the rare wide case), so the common path
         // carries no structurizer flow variable
         const bool wide = hi - lo > 1024;
-        if (!wide) V.cover(hi);
+        if constexpr (kPrioT) {   // the check rides on the ring's advance (every 512 B of input or more)
+            if (!wide && hi > V.B + kSR) {
+                const uint32_t oldB = V.B;
+                V.cover(hi);
+                if (prioOn && ((oldB ^ V.B) >> tickShift)) prio.tick(V.B - o0, blen);
+            }
+        } else {
+            if (!wide) V.cover(hi);
+        }
         v8 = V.rd8(p);
         if (wide) {   // wide window (long searches): hash inputs straight from global
             if (ST) acc[13] += 1;
@@ -1298,6 +1371,7 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
             STAMP_ADD(4, ts);
         }
     }
+    if (prioOn) prio.done();
     if (fail) return 0;
     if (havePe) store_pending();
     // ---- last literals
@@ -1329,6 +1403,10 @@ static_assert(kSR + kSRMirror <= 3072, "ring exceeds the shared scratch");
 static_assert(kDedup == 1024, "scratch layout");
 
 #if LZ4MT_PART != 2
+#if LZ4MT_EXP_BLKTIME
+constexpr uint32_t kExpBlkMax = 16384;
+__device__ uint64_t g_expBlk[3 * kExpBlkMax];
+#endif
 // XC: the exchange probe (true, the product) or the read-back probe (false,
 // the fallback when k_xchg_order fails); see encode_block_v5
 template <bool XC>
@@ -1345,6 +1423,9 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
     l_u32* Tl = (l_u32*)T;
     l_u8* Sl = (l_u8*)S;
     l_u8* Xl = (l_u8*)X;
+#if LZ4MT_EXP_BLKTIME
+    const uint64_t t0 = wall_clock64();
+#endif
     int32_t r;
     if (n < (uint32_t)kLimit64K)
         r = encode_block<true, false, false>(s, n, d, cap, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
@@ -1354,7 +1435,22 @@ __global__ void __launch_bounds__(64) k_encode(const uint8_t* __restrict__ src, 
     else
         r = encode_block<false, false, false>(s, n, d, cap, Tl, Sl, (l_u32*)Xl, Xl + kRingE, nullptr);
     if (laneid() == 0) csize[b] = r;
+#if LZ4MT_EXP_BLKTIME
+    if (laneid() == 0 && b < kExpBlkMax) {   // experiment builds only: per-block start / end / placement
+        g_expBlk[3 * b] = t0;
+        g_expBlk[3 * b + 1] = wall_clock64();
+        g_expBlk[3 * b + 2] = ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32) |
+                              (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    }
+#endif
 }
+#if LZ4MT_EXP_BLKTIME
+// (tools/blocktimes.py reads it through lz4mtHipExpBlockTimes)
+extern "C" int lz4mtHipExpBlockTimes(uint64_t* out, uint32_t nb) {
+    if (nb > kExpBlkMax) nb = kExpBlkMax;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_expBlk), (size_t)nb * 24) == hipSuccess ? (int)nb : -1;
+}
+#endif
 
 // k_encode with progress publishing (the block checksums' follower, the
 // block-sharded streamed gather): the same parse and bytes; pub[b] = bytes
