@@ -949,11 +949,18 @@ struct SimdPrio {
         const uint32_t fin = (uint32_t)t0 + (uint32_t)((float)(uint32_t)(now - t0) / (frac > 1e-3f ? frac : 1e-3f));
         const uint32_t L = laneid();
         if (L == 0) __hip_atomic_store(g_simdFinish + base + slot, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if LZ4MT_EXP_CUPRIO   // rank among the CU's waves (4 SIMDs x 16 slots), priority = rank / 2
+        const uint32_t cb = base & ~63u;
+        const uint32_t e = __hip_atomic_load(g_simdFinish + cb + L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool live = cb + L != base + slot && (int32_t)(e - (uint32_t)now) > 0;
+        const uint32_t rank = (uint32_t)__builtin_popcountll(bal(live && (int32_t)(e - fin) < 0)) >> 1;
+#else
         const uint32_t e = L < 16 ? __hip_atomic_load(g_simdFinish + base + L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                   : 0u;
         // live SIMD-mates projected to finish before this wave
         const bool live = L < 16 && L != slot && (int32_t)(e - (uint32_t)now) > 0;
         const uint32_t rank = (uint32_t)__builtin_popcountll(bal(live && (int32_t)(e - fin) < 0));
+#endif
         if (rank >= 3) __builtin_amdgcn_s_setprio(3);
         else if (rank == 2) __builtin_amdgcn_s_setprio(2);
         else if (rank == 1) __builtin_amdgcn_s_setprio(1);
@@ -1029,7 +1036,10 @@ __device__ int32_t encode_block_v5(g_cu8* __restrict__ s, uint32_t n, g_u8* __re
     uint32_t tickShift = 31;
     if (prioOn) {
         prio.start();
-        tickShift = (31 - __builtin_clz(blen)) - 7;   // a check every 1/128 of the block
+#ifndef LZ4MT_EXP_PRIO_SHIFT
+#define LZ4MT_EXP_PRIO_SHIFT 7
+#endif
+        tickShift = (31 - __builtin_clz(blen)) - LZ4MT_EXP_PRIO_SHIFT;   // a check every 1/128 of the block
     }
     const uint32_t capL = limited ? cap : 0xFFFFFFFFu;   // one SGPR for the per-sequence margin test
     const uint32_t mflimitP1 = n - kMfLimit + 1;
@@ -2692,9 +2702,29 @@ __device__ int32_t decode_block(Dec<ST>& D, int64_t cap) {
 #define PHYS_CHECK(end_) \
     if ((end_) > D.physcap) return kDecodeOutputTooSmall;
 
+    // SIMD-mate priority as in the encoder (SimdPrio), on output progress,
+    // blocks of 1 MiB and more (a finished wave's last projection is its
+    // finish time, past at once, so no clearing is needed)
+#ifndef LZ4MT_NO_DEC_PRIO
+    const bool prioOn = !ST && cap >= (1 << 20);
+#else
+    const bool prioOn = false;
+#endif
+    SimdPrio prio{};
+    uint32_t tickShift = 31, opTick = 0;
+    if (prioOn) {
+        prio.start();
+        tickShift = (31 - __builtin_clz((uint32_t)cap)) - 7;   // a check every 1/128 of the block
+    }
     if (oend - op < 64) goto safe_decode;
     for (;;) {
-        if (D.decode_batch(ip, op, iend, oend)) continue;
+        if (D.decode_batch(ip, op, iend, oend)) {
+            if (prioOn && ((opTick ^ (uint32_t)op) >> tickShift)) {
+                opTick = (uint32_t)op;
+                prio.tick(opTick, (uint32_t)cap);
+            }
+            continue;
+        }
         if (ST) D.acc[9] += 1;
         token = D.in8(ip++);
         length = token >> 4;
@@ -2823,6 +2853,10 @@ __device__ void copy_raw(g_cu8* src, g_u8* dst, int64_t n) {
 }
 
 #if LZ4MT_PART != 1
+#if LZ4MT_EXP_BLKTIME
+constexpr uint32_t kExpDecMax = 16384;
+__device__ uint64_t g_expDec[3 * kExpDecMax];
+#endif
 __global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ frame, const BlockRec* __restrict__ recs,
                                                uint32_t blockMax, uint8_t* __restrict__ out, uint64_t outCap,
                                                int32_t* __restrict__ dsize) {
@@ -2853,10 +2887,27 @@ __global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ frame
         D.flushed = 0;
         D.completed = 0;
         D.lowP = 0;
+#if LZ4MT_EXP_BLKTIME
+        const uint64_t t0 = wall_clock64();
+#endif
         res = decode_block(D, (int64_t)blockMax);
+#if LZ4MT_EXP_BLKTIME
+        if (laneid() == 0 && b < kExpDecMax) {
+            g_expDec[3 * b] = t0;
+            g_expDec[3 * b + 1] = wall_clock64();
+            g_expDec[3 * b + 2] = ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32) |
+                                  (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        }
+#endif
     }
     if (laneid() == 0) dsize[b] = res;
 }
+#if LZ4MT_EXP_BLKTIME
+extern "C" int lz4mtHipExpDecBlockTimes(uint64_t* out, uint32_t nb) {
+    if (nb > kExpDecMax) nb = kExpDecMax;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_expDec), (size_t)nb * 24) == hipSuccess ? (int)nb : -1;
+}
+#endif
 
 __global__ void __launch_bounds__(64) k_decode_stats(const uint8_t* __restrict__ frame,
                                                      const BlockRec* __restrict__ recs, uint32_t blockMax,

@@ -2,7 +2,8 @@
 LZ4MT_EXP_BLKTIME: wall clock at 100 MHz, and each wave's HW_ID / XCC_ID):
 how long the kernel runs after the average block is done, and whether the
 late blocks share SIMDs / CUs / XCDs.
-usage: LZ4MT_AMD_LIB=exp_libs/blktime.so python tools/blocktimes.py [block_id] [--sorted]"""
+usage: LZ4MT_AMD_LIB=exp_libs/blktime.so python tools/blocktimes.py [block_id] [--sorted] [--decode]
+(--decode: the same for k_decode, decompressing the frame)"""
 import ctypes
 import os
 import sys
@@ -28,18 +29,28 @@ raw.lz4mtHipExpBlockTimes.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
 sd = L.make_sd(bid, False, True)
 L.lib.lz4mtHipSetTiming(1)
 ms = (ctypes.c_float * 4)()
+dec = "--decode" in sys.argv
+raw.lz4mtHipExpDecBlockTimes.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+frame = L.compress_frame(src, sd) if dec else None
 for rep in range(3):
-    fr = L.compress_frame(src, sd)
-    torch.cuda.synchronize()
-    L.lib.lz4mtHipGetTimings(ms)
+    if dec:
+        fr, r = L.decompress_frame(frame)
+        torch.cuda.synchronize()
+        assert r == 0
+        L.lib.lz4mtHipGetTimings(ms)
+        ms[0] = ms[1]   # the decode kernel's time
+    else:
+        fr = L.compress_frame(src, sd)
+        torch.cuda.synchronize()
+        L.lib.lz4mtHipGetTimings(ms)
     out = np.zeros(nb * 3, dtype=np.uint64)
-    assert raw.lz4mtHipExpBlockTimes(out.ctypes.data, nb) == nb
+    assert (raw.lz4mtHipExpDecBlockTimes if dec else raw.lz4mtHipExpBlockTimes)(out.ctypes.data, nb) == nb
     t = out.reshape(nb, 3)
     t0, t1, hw = t[:, 0].astype(np.int64), t[:, 1].astype(np.int64), t[:, 2]
     start = (t0 - t0.min()) / 1e5   # ms (100 MHz)
     end = (t1 - t0.min()) / 1e5
     dur = end - start
-    print(f"B{bid} pass {rep}: k_encode {ms[0]:.2f} ms; block end mean {end.mean():.2f} ms, p50 {np.median(end):.2f}, "
+    print(f"B{bid} pass {rep}: {'k_decode' if dec else 'k_encode'} {ms[0]:.2f} ms; block end mean {end.mean():.2f} ms, p50 {np.median(end):.2f}, "
           f"p90 {np.percentile(end, 90):.2f}, max {end.max():.2f}; start spread {start.max():.2f} ms; "
           f"duration min {dur.min():.2f} mean {dur.mean():.2f} max {dur.max():.2f}")
     del fr
@@ -62,7 +73,7 @@ for sl in np.unique(slot):
 out_dir = os.environ.get("BT_OUT")
 if out_dir:
     tag = os.path.basename(os.environ["LZ4MT_AMD_LIB"]).split(".")[0]
-    np.savez(os.path.join(out_dir, f"bt_{tag}_b{bid}{'_sorted' if '--sorted' in sys.argv else ''}.npz"),
+    np.savez(os.path.join(out_dir, f"bt_{tag}_b{bid}{'_sorted' if '--sorted' in sys.argv else ''}{'_dec' if dec else ''}.npz"),
              start=start, end=end, xcc=xcc, se=se, sh=sh, cu=cu, simd=simd, slot=slot)
 simdkey = key * 4 + simd
 _, inv, cnt = np.unique(simdkey, return_inverse=True, return_counts=True)
