@@ -95,6 +95,18 @@ hipError_t launch_encode_pub(const uint8_t* src, uint64_t srcSize, uint32_t bloc
                              uint8_t* slots, int32_t* csize, uint32_t* pub, hipStream_t st);
 hipError_t launch_decode(const uint8_t* frame, const BlockRec* recs, uint32_t nBlocks, uint32_t blockMax,
                          uint8_t* out, uint64_t outCap, int32_t* dsize, hipStream_t st);
+// the serial frame walk fused with the decode (k_decode_walk): records are
+// decoded as the walk publishes them.  ctl: 8 zeroed device words.
+hipError_t launch_decode_walk(const uint8_t* frame, uint64_t frameSize, uint64_t bodyPos, uint32_t blockMax,
+                              int blockChecksum, uint32_t maxBlocks, BlockRec* recs, WalkInfo* info, uint32_t* ctl,
+                              uint8_t* out, uint64_t outCap, int32_t* dsize, uint32_t waves, hipStream_t st);
+// beside it: the block checksums as the walk publishes them, and the verify
+// with the walk's block count read on the device
+hipError_t launch_xxh32_walked(const uint8_t* frame, const BlockRec* recs, uint32_t* ctl, uint32_t* digest,
+                               uint32_t waves, hipStream_t st);
+hipError_t launch_block_verify_walked(const BlockRec* recs, const WalkInfo* info, const uint32_t* digest,
+                                      const int32_t* dsize, int blockChecksum, int32_t* status, uint32_t maxBlocks,
+                                      hipStream_t st);
 // the streamed compress's persistent encoder (lz4mt_kernels.hip, k_encode_stream);
 // ticks: a wait's limit without progress (s_memrealtime, 100 MHz); pend:
 // 4 words per wave, a block parked on its output slot (zeroed before the

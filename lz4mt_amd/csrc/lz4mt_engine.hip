@@ -16,6 +16,7 @@
 #include <cstring>
 #include <algorithm>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/lz4mt_hip.h"
@@ -735,13 +736,36 @@ struct DecodeBuffers {
     int32_t* status = nullptr;
     WalkInfo* info = nullptr;
     uint32_t* ssum = nullptr;
+    uint32_t* ctl = nullptr;   // k_decode_walk's published / ended / next words
     uint64_t cap = 0;
-    ~DecodeBuffers() { release(); }
+    ~DecodeBuffers() {
+        release();
+        if (ctl) hipFree(ctl);
+    }
+    // k_decode_walk's control words live in UNCACHED device memory: the
+    // waves poll them from every XCD, and an sc1 load is served by the
+    // reader's own L2, which is not coherent with the other XCDs' -- with
+    // cached memory a poller read a stale copy of the walk's progress until
+    // its 30 s bound (per-XCD L2s, MI355X_MICROARCH.md).  Some runtimes grant
+    // the kind only in 2 MiB units.  False: the fused walk is not used.
+    bool ensure_ctl() {
+        if (ctl) return true;
+        for (size_t sz : {size_t(32), size_t(2) << 20}) {
+            void* p = nullptr;
+            if (hipExtMallocWithFlags(&p, sz, hipDeviceMallocUncached) == hipSuccess && p) {
+                ctl = static_cast<uint32_t*>(p);
+                return true;
+            }
+            (void)hipGetLastError();
+        }
+        return false;
+    }
     WalkScratch ws{};
     uint64_t wsChunks = 0, wsCap = 0, wsNodes = 0;
     void release() {
         hipFree(recs); hipFree(digest); hipFree(dsize); hipFree(status); hipFree(info); hipFree(ssum);
-        recs = nullptr; digest = nullptr; dsize = nullptr; status = nullptr; info = nullptr; ssum = nullptr; cap = 0;
+        recs = nullptr; digest = nullptr; dsize = nullptr; status = nullptr; info = nullptr; ssum = nullptr;
+        cap = 0;
         release_walk();
     }
     void release_walk() {
@@ -840,6 +864,82 @@ Lz4MtResult walk_frame(const uint8_t* frame, uint64_t frameSize, uint64_t bodyPo
         guess = (frameSize - bodyPos) / 4 + 1;
     }
     return LZ4MT_RESULT_OK;
+}
+
+// LZ4MT_AMD_WALK: fused (the serial walk inside the decode kernel, opt-in),
+// serial (the separate serial walk kernel), parallel (the candidate walk, the
+// default for blocks <= 1 MiB over 64 MiB)
+bool fused_walk(uint32_t, uint64_t) {   // opt-in while its stall is open
+    const char* fe = getenv("LZ4MT_AMD_WALK");
+    return fe && strcmp(fe, "fused") == 0;
+}
+
+// The fused walk + decode of an independent-block frame body into target
+// (k_decode_walk), with the block checksums (k_xxh32_walked, on the aux
+// stream) and the verify launched behind it: nothing waits on the host
+// until the walk's info is read back at the end.  Returns false, with
+// nothing to undo, when the record table overflowed (the caller then walks
+// separately with a larger one); otherwise wi is the walk's result and
+// dsize / status hold the blocks [0, wi.nBlocks).
+bool decode_walk_fused(const uint8_t* f, uint64_t frameSize, uint64_t bodyPos, uint32_t bm, int bck, uint8_t* target,
+                       uint64_t targetCap, DecodeBuffers& B, AuxStream& aux, WalkInfo& wi, Lz4MtResult& result,
+                       hipStream_t st) {
+    static const uint32_t kCus = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return (uint32_t)cus;
+    }();
+    const uint64_t guess = std::min<uint64_t>((frameSize - bodyPos) / 4 + 1, (frameSize - bodyPos) / 1024 + 4096);
+    result = LZ4MT_RESULT_OK;
+    if (!B.ensure(guess)) { result = LZ4MT_RESULT_ERROR; return true; }
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(B.cap, 0xFFFFFFFFu);
+    const bool side = bck && aux.ensure();
+    bool ok = hipMemsetAsync(B.ctl, 0, 32, st) == hipSuccess;
+    if (ok && side) ok = hipEventRecord(aux.evIn, st) == hipSuccess && hipStreamWaitEvent(aux.st, aux.evIn, 0) == hipSuccess;
+    static const bool trace = getenv("LZ4MT_AMD_WALK_TRACE") != nullptr;
+    static hipEvent_t ev[6] = {};
+    if (trace && !ev[0])
+        for (auto& e : ev) hipEventCreate(&e);
+    if (trace) hipEventRecord(ev[0], st);
+    // k_decode's LDS allows 8 resident waves per CU: one generation, fed by the walk
+    ok = ok && launch_decode_walk(f, frameSize, bodyPos, bm, bck, cap, B.recs, B.info, B.ctl, target, targetCap, B.dsize,
+                                  std::min<uint32_t>(kCus * 8, cap + 1), st) == hipSuccess;
+    if (trace) hipEventRecord(ev[1], st);
+    if (ok && bck) {   // 16 blocks per wave, as k_xxh32_frame_blocks; at most 2 waves per CU
+        const uint32_t xw = std::min<uint32_t>(kCus * 2, (cap + 15) / 16);
+        if (trace) hipEventRecord(ev[2], side ? aux.st : st);
+        ok = launch_xxh32_walked(f, B.recs, B.ctl, B.digest, xw, side ? aux.st : st) == hipSuccess;
+        if (trace) hipEventRecord(ev[3], side ? aux.st : st);
+        if (ok && side) ok = hipEventRecord(aux.evOut, aux.st) == hipSuccess && hipStreamWaitEvent(st, aux.evOut, 0) == hipSuccess;
+    }
+    ok = ok && launch_block_verify_walked(B.recs, B.info, B.digest, B.dsize, bck, B.status, cap, st) == hipSuccess &&
+         hipMemcpyAsync(&wi, B.info, sizeof(wi), hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipStreamSynchronize(st) == hipSuccess;
+    if (trace) {
+        float a = -1, b = -1, c = -1;
+        hipEventSynchronize(ev[1]);
+        hipEventElapsedTime(&a, ev[0], ev[1]);
+        if (bck) {
+            hipEventSynchronize(ev[3]);
+            hipEventElapsedTime(&b, ev[2], ev[3]);
+            hipEventElapsedTime(&c, ev[0], ev[2]);
+        }
+        fprintf(stderr, "fused walk: k_decode_walk %.3f ms, k_xxh32_walked %.3f ms (starting %.3f ms after the decode "
+                "kernel's start)\n", a, b, c);
+    }
+    if (!ok) { result = LZ4MT_RESULT_ERROR; return true; }
+#if LZ4MT_WALK_DIAG
+    {
+        uint32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        hipMemcpy(c, B.ctl, 32, hipMemcpyDeviceToHost);
+        fprintf(stderr, "fused walk diag: ctl %08x next %u groups %u; timeouts %u (last: need %u saw %08x)\n", c[0],
+                c[2], c[3], c[5], c[6], c[7]);
+    }
+#endif
+    if (wi.result == 1 && wi.nBlocks == cap) return false;   // record table full: walk separately, larger
+    return true;
 }
 
 }  // namespace
@@ -1020,11 +1120,12 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
         const int bck = sd->flg.blockChecksum, sck = sd->flg.streamChecksum;
         WalkInfo wi{};
         g_timing.mark(0, st);
-        result = walk_frame(f, frameSize, pos + 4 + hb, bm, bck, B, wi, st);
-        if (result != LZ4MT_RESULT_OK) break;
-        const uint64_t nb = wi.nBlocks;
+        const uint64_t bodyPos = pos + 4 + hb;
         uint64_t produced = 0;
         if (!sd->flg.blockIndependence) {
+            result = walk_frame(f, frameSize, bodyPos, bm, bck, B, wi, st);
+            if (result != LZ4MT_RESULT_OK) break;
+            const uint64_t nb = wi.nBlocks;
             // block-dependent frame (decompressBlockDependency, src/lz4mt.cpp:
             // 737-845): one wave decodes the blocks in order, each against the
             // 64 KiB before it (zeros before the frame's first byte)
@@ -1061,28 +1162,47 @@ extern "C" Lz4MtResult lz4mtHipDecompressFrame(const void* d_frame, uint64_t fra
         const uint64_t room = outCap > opos ? outCap - opos : 0;
         uint8_t* target = out + opos;
         uint64_t targetCap = room;
-        if (!aligned) {
-            if (!tmp.ensure(nb * bm)) { result = LZ4MT_RESULT_ERROR; break; }
-            target = tmp.p;
-            targetCap = std::min<uint64_t>(room, nb * bm);
-        }
         // The block checksums run on a side stream beside the decode: the
         // checksum kernel uses no LDS (16 blocks per wave), so its waves do
         // not take a slot from the decode's eight 20 KiB waves per CU.
-        const bool side = bck && nb && aux.ensure();
-        if (side) {
-            HIPCHK(hipEventRecord(aux.evIn, st));
-            HIPCHK(hipStreamWaitEvent(aux.st, aux.evIn, 0));
-            HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, aux.st));
-            HIPCHK(hipEventRecord(aux.evOut, aux.st));
+        bool side = false, fused = false;
+        if (aligned && fused_walk(bm, frameSize - bodyPos) && B.ensure_ctl()) {   // walk inside the decode (k_decode_walk)
+            g_timing.mark(1, st);
+            fused = decode_walk_fused(f, frameSize, bodyPos, bm, bck, target, targetCap, B, aux, wi, result, st);
+            if (fused && result != LZ4MT_RESULT_OK) break;
+            if (fused) {
+                g_timing.mark(2, st);
+                g_timing.mark(3, st);
+            }
         }
-        g_timing.mark(1, st);
-        HIPCHK(launch_decode(f, B.recs, (uint32_t)nb, bm, target, targetCap, B.dsize, st));
-        g_timing.mark(2, st);
-        if (side) HIPCHK(hipStreamWaitEvent(st, aux.evOut, 0));
-        else if (bck) HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, st));
-        HIPCHK(launch_block_verify(B.recs, (uint32_t)nb, B.digest, B.dsize, bm, bck, B.status, st));
-        g_timing.mark(3, st);
+        if (!fused) {
+            result = walk_frame(f, frameSize, bodyPos, bm, bck, B, wi, st);
+            if (result != LZ4MT_RESULT_OK) break;
+        }
+        const uint64_t nb = wi.nBlocks;
+        if (!fused) {
+            if (!aligned) {
+                if (!tmp.ensure(nb * bm)) { result = LZ4MT_RESULT_ERROR; break; }
+                target = tmp.p;
+                targetCap = std::min<uint64_t>(room, nb * bm);
+            }
+            side = bck && nb && aux.ensure();
+            if (side) {
+                HIPCHK(hipEventRecord(aux.evIn, st));
+                HIPCHK(hipStreamWaitEvent(aux.st, aux.evIn, 0));
+                HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, aux.st));
+                HIPCHK(hipEventRecord(aux.evOut, aux.st));
+            }
+            g_timing.mark(1, st);
+            HIPCHK(launch_decode(f, B.recs, (uint32_t)nb, bm, target, targetCap, B.dsize, st));
+            g_timing.mark(2, st);
+            if (side) HIPCHK(hipStreamWaitEvent(st, aux.evOut, 0));
+            else if (bck) HIPCHK(launch_xxh32_frame_blocks(f, B.recs, (uint32_t)nb, B.digest, st));
+        }
+        if (!fused) {
+            HIPCHK(launch_block_verify(B.recs, (uint32_t)nb, B.digest, B.dsize, bm, bck, B.status, st));
+            g_timing.mark(3, st);
+        }
         std::vector<int32_t> ds(nb), stv(nb);
         if (nb) {
             HIPCHK(hipMemcpyAsync(ds.data(), B.dsize, nb * 4, hipMemcpyDeviceToHost, st));

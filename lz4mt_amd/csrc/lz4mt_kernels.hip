@@ -913,6 +913,46 @@ __device__ __forceinline__ void publish_progress(uint32_t* pub, uint32_t v) {
 // check fails (or LZ4MT_AMD_ENC_PROBE=readback forces it).
 // DUP: no effect on the code; a separate instantiation for a kernel that
 // must not share (and so outline) another kernel's one (k_encode_stream).
+// (k_decode_walk, k_xxh32_walked; ctl words described at k_decode_walk)
+// waits until records [0, need) are published or the walk ended; returns the
+// published count (0 after 30 s, which the caller treats as the end).  The
+// walker publishes ctl[0] = count (| kWalkEnded at the end) with agent-scope
+// atomics behind a release fence; this polls it with relaxed agent loads and
+// takes ONE agent acquire once it matches.  ctl is uncached device memory
+// (DecodeBuffers::ensure_ctl): a poll is served by the reader's own XCD L2,
+// and with cached memory that copy stayed stale until the 30 s bound.
+constexpr uint32_t kWalkEnded = 0x80000000u;
+__device__ __forceinline__ uint32_t walked_wait(uint32_t* ctl, uint32_t need) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        uint32_t v = 0;
+        if (laneid() == 0) v = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v = (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+        if ((v & ~kWalkEnded) >= need || (v & kWalkEnded)) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every lane: the records as published
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            return v & ~kWalkEnded;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {
+#if LZ4MT_WALK_DIAG
+            if (laneid() == 0) {
+                __hip_atomic_fetch_add(ctl + 5, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(ctl + 6, need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(ctl + 7, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#endif
+            return 0;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+// the walker's publication: its record stores written back, then the word
+__device__ __forceinline__ void walk_publish(uint32_t* ctl, uint32_t v) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    (void)__hip_atomic_exchange(ctl, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // SIMD-mate priority (encode_block_v5, byU32 blocks >= 1 MiB).  The waves
 // sharing a SIMD issue oldest first, so with one generation of 2048 blocks
 // (8 GiB of 4 MiB blocks, 8 waves per CU) the younger wave of each pair is
@@ -2857,13 +2897,11 @@ __device__ void copy_raw(g_cu8* src, g_u8* dst, int64_t n) {
 constexpr uint32_t kExpDecMax = 16384;
 __device__ uint64_t g_expDec[3 * kExpDecMax];
 #endif
-__global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ frame, const BlockRec* __restrict__ recs,
-                                               uint32_t blockMax, uint8_t* __restrict__ out, uint64_t outCap,
-                                               int32_t* __restrict__ dsize) {
-    __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
-    __shared__ __attribute__((aligned(16))) uint8_t win[kWinAlloc];   /* + dummy write area + hop table */
-    const uint32_t b = blockIdx.x;
-    const BlockRec r = recs[b];
+// one block of an independent-block frame into its output slot (k_decode,
+// k_decode_walk): the reference's decompressBlockIndependent body
+__device__ __forceinline__ int32_t decode_one(const uint8_t* __restrict__ frame, const BlockRec& r, uint32_t b,
+                                              uint32_t blockMax, uint8_t* __restrict__ out, uint64_t outCap,
+                                              l_u8* ring, l_u8* win) {
     const uint64_t slot = (uint64_t)b * blockMax;
     const int64_t physcap = outCap > slot ? (int64_t)min<uint64_t>(blockMax, outCap - slot) : 0;
     const int64_t len = r.bits & 0x7FFFFFFFu;
@@ -2879,8 +2917,8 @@ __global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ frame
         D.len = len;
         D.dst = gptr(out) + slot;
         D.physcap = physcap;
-        D.ring = (l_u8*)ring;
-        D.win = (l_u8*)win;
+        D.ring = ring;
+        D.win = win;
         D.wlo = INT64_MIN / 4;
         D.labase = INT64_MIN / 4;
         D.la = 0;
@@ -2900,7 +2938,91 @@ __global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ frame
         }
 #endif
     }
+    return res;
+}
+
+__global__ void __launch_bounds__(64) k_decode(const uint8_t* __restrict__ frame, const BlockRec* __restrict__ recs,
+                                               uint32_t blockMax, uint8_t* __restrict__ out, uint64_t outCap,
+                                               int32_t* __restrict__ dsize) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kWinAlloc];   /* + dummy write area + hop table */
+    const uint32_t b = blockIdx.x;
+    const int32_t res = decode_one(frame, recs[b], b, blockMax, out, outCap, (l_u8*)ring, (l_u8*)win);
     if (laneid() == 0) dsize[b] = res;
+}
+
+// The serial frame walk fused with the decode (wherever the walk is serial,
+// §4.6): workgroup 0's lane 0 follows the size words as k_frame_walk does,
+// publishing the records found so far every kWalkPub blocks (agent-scope
+// release of ctl[0]); every other wave takes block numbers from ctl[2] and
+// decodes each one as soon as its record is published.  k_xxh32_walked hashes the blocks on a side stream the same
+// way.  Waves wait only on the walker, a resident wave of this grid
+// (workgroup 0 is dispatched first), so every wait ends; a 30 s bound keeps
+// even a broken invariant from spinning for ever.
+// ctl: [0] records published (| kWalkEnded once the walk ended), [2] next
+// block to decode, [3] next block group to hash (k_xxh32_walked).
+constexpr uint32_t kWalkPub = 8;
+__global__ void __launch_bounds__(64) k_decode_walk(const uint8_t* __restrict__ frame, uint64_t frameSize,
+                                                    uint64_t bodyPos, uint32_t blockMax, int blockChecksum,
+                                                    uint32_t maxBlocks, BlockRec* __restrict__ recs,
+                                                    WalkInfo* __restrict__ info, uint32_t* __restrict__ ctl,
+                                                    uint8_t* __restrict__ out, uint64_t outCap,
+                                                    int32_t* __restrict__ dsize) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kWinAlloc];
+    const uint32_t L = laneid();
+    if (blockIdx.x == 0 && L == 0) {
+        auto rd32 = [&](uint64_t p) -> uint32_t {
+            return (uint32_t)frame[p] | ((uint32_t)frame[p + 1] << 8) | ((uint32_t)frame[p + 2] << 16) |
+                   ((uint32_t)frame[p + 3] << 24);
+        };
+        uint64_t pos = bodyPos;
+        uint32_t nb = 0;
+        int32_t result = 0;
+        for (;;) {   // result codes: src/lz4mt.cpp:685-727 (as k_frame_walk)
+            if (pos + 4 > frameSize) { result = 12; break; }
+            const uint32_t bits = rd32(pos);
+            pos += 4;
+            if (bits == 0) break;
+            const uint32_t sz = bits & 0x7FFFFFFFu;
+            if (sz > blockMax) { result = 20; break; }
+            if (pos + sz > frameSize) { result = 13; pos = frameSize; break; }
+            BlockRec r{pos, bits, 0};
+            pos += sz;
+            if (blockChecksum) {
+                if (pos + 4 > frameSize) { result = 14; break; }
+                r.checksum = rd32(pos);
+                pos += 4;
+            }
+            if (nb >= maxBlocks) { result = 1; break; }
+            recs[nb++] = r;
+            if (nb % kWalkPub == 0) walk_publish(ctl, nb);
+        }
+        const WalkInfo wi{pos, nb, result};
+        *info = wi;
+        walk_publish(ctl, nb | kWalkEnded);
+    }
+    // the walker's wave does not decode: after its lane-0 loop, a wave that
+    // went on into the decode loop waited out the 30 s bound there (its first
+    // poll never matched), so the walk has a wave of its own
+    if (blockIdx.x == 0) return;
+    for (;;) {
+        uint32_t b = 0;
+        if (L == 0) b = __hip_atomic_fetch_add(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+        if (b >= walked_wait(ctl, b + 1)) return;
+        const int32_t res = decode_one(frame, recs[b], b, blockMax, out, outCap, (l_u8*)ring, (l_u8*)win);
+        if (L == 0) dsize[b] = res;
+    }
+}
+
+hipError_t launch_decode_walk(const uint8_t* frame, uint64_t frameSize, uint64_t bodyPos, uint32_t blockMax,
+                              int blockChecksum, uint32_t maxBlocks, BlockRec* recs, WalkInfo* info, uint32_t* ctl,
+                              uint8_t* out, uint64_t outCap, int32_t* dsize, uint32_t waves, hipStream_t st) {
+    if (!waves || !maxBlocks) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_decode_walk, dim3(waves), dim3(64), 0, st, frame, frameSize, bodyPos, blockMax, blockChecksum,
+                       maxBlocks, recs, info, ctl, out, outCap, dsize);
+    return hipGetLastError();
 }
 #if LZ4MT_EXP_BLKTIME
 extern "C" int lz4mtHipExpDecBlockTimes(uint64_t* out, uint32_t nb) {
@@ -3889,6 +4011,34 @@ __global__ void __launch_bounds__(64) k_xxh32_frame_blocks(const uint8_t* __rest
     if (ok && (laneid() & 3u) == 0) digest[b] = h;
 }
 
+// k_xxh32_frame_blocks beside k_decode_walk: 16 blocks per wave (lane
+// quads), groups taken from ctl[3], each group hashed once the walk has
+// published it (or ended short of it)
+__global__ void __launch_bounds__(64) k_xxh32_walked(const uint8_t* __restrict__ frame,
+                                                     const BlockRec* __restrict__ recs, uint32_t* __restrict__ ctl,
+                                                     uint32_t* __restrict__ digest) {
+    const uint32_t L = laneid();
+    for (;;) {
+        uint32_t g = 0;
+        if (L == 0) g = __hip_atomic_fetch_add(ctl + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t first = 16u * (uint32_t)__builtin_amdgcn_readfirstlane((int)g);
+        const uint32_t w = walked_wait(ctl, first + 16);
+        if (first >= w) return;
+        const uint32_t b = first + (L >> 2);
+        const bool ok = b < w;
+        const BlockRec r = recs[ok ? b : first];
+        const uint32_t h = xxh32_quad(gptr(frame) + r.offset, ok ? (r.bits & 0x7FFFFFFFu) : 0u, gptr(frame));
+        if (ok && (L & 3u) == 0) digest[b] = h;
+    }
+}
+
+hipError_t launch_xxh32_walked(const uint8_t* frame, const BlockRec* recs, uint32_t* ctl, uint32_t* digest,
+                               uint32_t waves, hipStream_t st) {
+    if (!waves) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_xxh32_walked, dim3(waves), dim3(64), 0, st, frame, recs, ctl, digest);
+    return hipGetLastError();
+}
+
 // XXH32 of consecutive `chunk`-byte pieces of one range (the last one
 // short), 16 pieces per wave, a lane quad per piece: the parallel "checksum
 // of checksums" the large-config tests and the multi-GPU check compare.
@@ -4482,6 +4632,28 @@ __global__ void k_block_verify(const BlockRec* __restrict__ recs, uint32_t nBloc
     if (dsize[b] < 0) st = (dsize[b] == kDecodeOutputTooSmall) ? 1 : 18;   // ERROR / DECOMPRESS_FAIL
     else if (blockChecksum && digest[b] != recs[b].checksum) st = 16;      // BLOCK_CHECKSUM_MISMATCH
     status[b] = st;
+}
+
+// k_block_verify after k_decode_walk: the block count from the walk's info
+__global__ void k_block_verify_walked(const BlockRec* __restrict__ recs, const WalkInfo* __restrict__ info,
+                                      const uint32_t* __restrict__ digest, const int32_t* __restrict__ dsize,
+                                      int blockChecksum, int32_t* __restrict__ status) {
+    const uint32_t nb = info->nBlocks;
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gridDim.x * blockDim.x) {
+        int32_t st = 0;
+        if (dsize[b] < 0) st = (dsize[b] == kDecodeOutputTooSmall) ? 1 : 18;
+        else if (blockChecksum && digest[b] != recs[b].checksum) st = 16;
+        status[b] = st;
+    }
+}
+
+hipError_t launch_block_verify_walked(const BlockRec* recs, const WalkInfo* info, const uint32_t* digest,
+                                      const int32_t* dsize, int blockChecksum, int32_t* status, uint32_t maxBlocks,
+                                      hipStream_t st) {
+    const uint32_t need = (maxBlocks + 255) / 256 + 1, wg = need < 1024u ? need : 1024u;
+    hipLaunchKernelGGL(k_block_verify_walked, dim3(wg), dim3(256), 0, st, recs, info, digest, dsize, blockChecksum,
+                       status);
+    return hipGetLastError();
 }
 
 hipError_t launch_block_verify(const BlockRec* recs, uint32_t nBlocks, const uint32_t* digest, const int32_t* dsize,

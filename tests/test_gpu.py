@@ -284,9 +284,10 @@ def test_callback_api_on_gpu(golden_inputs, mode):
 
 # ---------------------------------------------------------------------------
 # the parallel frame walk (candidate offsets + pointer doubling) must give the
-# serial walk's records and error codes on every frame, well-formed or not
+# serial walk's records, bytes and error codes on every frame, well-formed or
+# not
 # ---------------------------------------------------------------------------
-def _decode_both(b, cap):
+def _decode_all(b, cap):
     res = []
     for mode in ("serial", "parallel"):
         os.environ["LZ4MT_AMD_WALK"] = mode
@@ -299,12 +300,15 @@ def _decode_both(b, cap):
     return res
 
 
-@pytest.mark.parametrize("bid,sck,bck", [(4, True, True), (4, False, False), (5, False, True)])
-def test_frame_walk_parallel_matches_serial(golden_inputs, bid, sck, bck):
+@pytest.mark.parametrize("bid,sck,bck", [(4, True, True), (4, False, False), (5, False, True), (6, False, True),
+                                         (7, True, True), (7, False, False)])
+def test_frame_walks_match_serial(golden_inputs, bid, sck, bck):
     data = (golden_inputs["syn300k"] + golden_inputs["zeros300k"] + golden_inputs["random100k"]) * 3
+    if bid >= 6:   # several blocks of 1 / 4 MiB
+        data = data * (4 if bid == 7 else 1)
     f = host(L.compress_frame(dev(data), L.make_sd(bid, sck, bck)))
-    cap = len(data) + (1 << 20)
-    (rs, os_), (rp, op_) = _decode_both(f, cap)
+    cap = len(data) + (4 << 20)
+    (rs, os_), (rp, op_) = _decode_all(f, cap)
     assert rs == rp == 0 and os_ == op_ == data
     rng = random.Random(bid * 7 + sck * 3 + bck)
     bodies = [7 + rng.randrange(len(f) - 7) for _ in range(12)]
@@ -316,7 +320,7 @@ def test_frame_walk_parallel_matches_serial(golden_inputs, bid, sck, bck):
     skip = (0x184D2A50).to_bytes(4, "little") + (3).to_bytes(4, "little") + b"abc"
     cases += [f + skip + f, f + f[:-3], f + b"xy"]
     for b in cases:
-        (rs, os_), (rp, op_) = _decode_both(b, 2 * cap)
+        (rs, os_), (rp, op_) = _decode_all(b, 2 * cap)
         assert rs == rp and os_ == op_, (len(b), rs, rp)
 
 
