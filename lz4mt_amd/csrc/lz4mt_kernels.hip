@@ -3012,7 +3012,14 @@ __global__ void __launch_bounds__(64) k_decode_walk(const uint8_t* __restrict__ 
         b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
         if (b >= walked_wait(ctl, b + 1)) return;
         const int32_t res = decode_one(frame, recs[b], b, blockMax, out, outCap, (l_u8*)ring, (l_u8*)win);
-        if (L == 0) dsize[b] = res;
+        // every lane stores the (uniform) result: a lane-0-only store here,
+        // at the end of the loop body, was compiled as a divergent loop exit
+        // that left lane 0 looping alone, and the wave then waited out the
+        // 30 s bound with its other lanes parked
+        dsize[b] = res;
+        // decode_block's SIMD-mate priority is per block: a wave going back
+        // to wait for the walk must not keep it
+        __builtin_amdgcn_s_setprio(0);
     }
 }
 
