@@ -866,12 +866,27 @@ Lz4MtResult walk_frame(const uint8_t* frame, uint64_t frameSize, uint64_t bodyPo
     return LZ4MT_RESULT_OK;
 }
 
-// LZ4MT_AMD_WALK: fused (the serial walk inside the decode kernel, opt-in),
-// serial (the separate serial walk kernel), parallel (the candidate walk, the
+// LZ4MT_AMD_WALK: fused (the serial walk inside the decode kernel), serial
+// (the separate serial walk kernel), parallel (the candidate walk, the
 // default for blocks <= 1 MiB over 64 MiB)
-bool fused_walk(uint32_t, uint64_t) {   // opt-in while its stall is open
+// Fused by default only where the walk is serial and the frame surely spans
+// more than 3 decode generations (8 resident decoders per CU): the walk then
+// overlaps the earlier generations (32 GiB B7: 270.6 -> 273.2 GiB/s), while
+// with one generation the last block's record arrives only at the walk's end
+// (8 GiB B7: 262.4 -> 258.3; profiles/r06/r06ae_fused_walk_ab.txt).
+bool fused_walk(uint32_t bm, uint64_t body) {
     const char* fe = getenv("LZ4MT_AMD_WALK");
-    return fe && strcmp(fe, "fused") == 0;
+    if (fe && strcmp(fe, "fused") == 0) return true;
+    if (fe && (strcmp(fe, "serial") == 0 || strcmp(fe, "parallel") == 0)) return false;
+    static const uint64_t kDecoders = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return (uint64_t)cus * 8;
+    }();
+    const bool serialWalk = !(bm <= (1u << 20) && body >= (64ull << 20));
+    return serialWalk && body / ((uint64_t)bm + 8) > 3 * kDecoders;
 }
 
 // The fused walk + decode of an independent-block frame body into target
@@ -903,9 +918,11 @@ bool decode_walk_fused(const uint8_t* f, uint64_t frameSize, uint64_t bodyPos, u
     if (trace && !ev[0])
         for (auto& e : ev) hipEventCreate(&e);
     if (trace) hipEventRecord(ev[0], st);
-    // k_decode's LDS allows 8 resident waves per CU: one generation, fed by the walk
+    // k_decode's LDS allows 8 resident waves per CU: the walker + 8 decoders per
+    // CU (the last one resident once the walk ends); with one decoder fewer, one
+    // wave decoded two blocks of a one-generation frame back to back
     ok = ok && launch_decode_walk(f, frameSize, bodyPos, bm, bck, cap, B.recs, B.info, B.ctl, target, targetCap, B.dsize,
-                                  std::min<uint32_t>(kCus * 8, cap + 1), st) == hipSuccess;
+                                  std::min<uint32_t>(kCus * 8, cap) + 1, st) == hipSuccess;
     if (trace) hipEventRecord(ev[1], st);
     if (ok && bck) {   // 16 blocks per wave, as k_xxh32_frame_blocks; at most 2 waves per CU
         const uint32_t xw = std::min<uint32_t>(kCus * 2, (cap + 15) / 16);

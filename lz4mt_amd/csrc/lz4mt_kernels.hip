@@ -946,9 +946,11 @@ __device__ __forceinline__ uint32_t walked_wait(uint32_t* ctl, uint32_t need) {
         __builtin_amdgcn_s_sleep(8);
     }
 }
-// the walker's publication: its record stores written back, then the word
+// the walker's publication: its records were stored write-through (sc1), so
+// waiting for them is the whole release -- an agent release fence here
+// (buffer_wbl2) also wrote back every output line the decoders had dirtied
+// in the walker's XCD L2, once per publication: B7 decompress 152 GiB/s
 __device__ __forceinline__ void walk_publish(uint32_t* ctl, uint32_t v) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     (void)__hip_atomic_exchange(ctl, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -2971,6 +2973,7 @@ __global__ void __launch_bounds__(64) k_decode_walk(const uint8_t* __restrict__ 
     __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
     __shared__ __attribute__((aligned(16))) uint8_t win[kWinAlloc];
     const uint32_t L = laneid();
+    if (blockIdx.x == 0) __builtin_amdgcn_s_setprio(3);   // the walk gates every decoder: it issues first
     if (blockIdx.x == 0 && L == 0) {
         auto rd32 = [&](uint64_t p) -> uint32_t {
             return (uint32_t)frame[p] | ((uint32_t)frame[p + 1] << 8) | ((uint32_t)frame[p + 2] << 16) |
@@ -2995,7 +2998,12 @@ __global__ void __launch_bounds__(64) k_decode_walk(const uint8_t* __restrict__ 
                 pos += 4;
             }
             if (nb >= maxBlocks) { result = 1; break; }
-            recs[nb++] = r;
+            // write-through (sc1) stores: see walk_publish
+            __hip_atomic_store(&recs[nb].offset, r.offset, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(&recs[nb].bits),
+                               (uint64_t)r.bits | ((uint64_t)r.checksum << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            ++nb;
             if (nb % kWalkPub == 0) walk_publish(ctl, nb);
         }
         const WalkInfo wi{pos, nb, result};

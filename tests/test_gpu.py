@@ -283,13 +283,14 @@ def test_callback_api_on_gpu(golden_inputs, mode):
 
 
 # ---------------------------------------------------------------------------
-# the parallel frame walk (candidate offsets + pointer doubling) must give the
-# serial walk's records, bytes and error codes on every frame, well-formed or
-# not
+# the parallel frame walk (candidate offsets + pointer doubling) and the walk
+# fused into the decode (k_decode_walk: records decoded as the walk publishes
+# them) must give the serial walk's records, bytes and error codes on every
+# frame, well-formed or not
 # ---------------------------------------------------------------------------
 def _decode_all(b, cap):
     res = []
-    for mode in ("serial", "parallel"):
+    for mode in ("serial", "parallel", "fused"):
         os.environ["LZ4MT_AMD_WALK"] = mode
         try:
             out = torch.empty(cap, dtype=torch.uint8, device="cuda")
@@ -308,8 +309,8 @@ def test_frame_walks_match_serial(golden_inputs, bid, sck, bck):
         data = data * (4 if bid == 7 else 1)
     f = host(L.compress_frame(dev(data), L.make_sd(bid, sck, bck)))
     cap = len(data) + (4 << 20)
-    (rs, os_), (rp, op_) = _decode_all(f, cap)
-    assert rs == rp == 0 and os_ == op_ == data
+    (rs, os_), (rp, op_), (rf, of_) = _decode_all(f, cap)
+    assert rs == rp == rf == 0 and os_ == op_ == of_ == data
     rng = random.Random(bid * 7 + sck * 3 + bck)
     bodies = [7 + rng.randrange(len(f) - 7) for _ in range(12)]
     cases = [f[:k] for k in bodies]                                   # truncations
@@ -320,8 +321,8 @@ def test_frame_walks_match_serial(golden_inputs, bid, sck, bck):
     skip = (0x184D2A50).to_bytes(4, "little") + (3).to_bytes(4, "little") + b"abc"
     cases += [f + skip + f, f + f[:-3], f + b"xy"]
     for b in cases:
-        (rs, os_), (rp, op_) = _decode_all(b, 2 * cap)
-        assert rs == rp and os_ == op_, (len(b), rs, rp)
+        (rs, os_), (rp, op_), (rf, of_) = _decode_all(b, 2 * cap)
+        assert rs == rp == rf and os_ == op_ == of_, (len(b), rs, rp, rf)
 
 
 def test_compress_frame_async_in_hip_graph(golden_inputs):

@@ -1,14 +1,10 @@
 #!/bin/bash
-# round 6: the frame walk fused into the decode (k_decode_walk) -- the
-# diagnostic at every block size, the GPU parity file with every decode forced
-# through it, then configs[2] (32 GiB decompress-only) and configs[1] with the
-# separate serial walk vs fused
+# round 6: fused walk with 8 decoders per CU + the walker: parity (GPU file,
+# fused forced) and configs[2] / configs[1], serial vs fused, two passes
 set -uo pipefail
-out=${OUT:-gpurun_out/r06ac}
+out=gpurun_out/r06ae
 mkdir -p "$out"
 export TMPDIR=/tmp
-timeout -k 10 120 python3 -u tools/walk_diag.py > "$out/diag.txt" 2>&1 || { tail -20 "$out/diag.txt"; exit 1; }
-grep returned "$out/diag.txt"
 LZ4MT_AMD_WALK=fused timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu.py > "$out/test_gpu_fused.txt" 2>&1 || { tail -30 "$out/test_gpu_fused.txt"; exit 1; }
 tail -1 "$out/test_gpu_fused.txt"
 for pass in 1 2; do
