@@ -870,7 +870,8 @@ Lz4MtResult walk_frame(const uint8_t* frame, uint64_t frameSize, uint64_t bodyPo
 // (the separate serial walk kernel), parallel (the candidate walk, the
 // default for blocks <= 1 MiB over 64 MiB)
 // Fused by default only where the walk is serial and the frame surely spans
-// more than 3 decode generations (8 resident decoders per CU): the walk then
+// more than one decode generation (8 resident decoders per CU; body /
+// (bm + 8) is a lower bound on its block count): the walk then
 // overlaps the earlier generations (32 GiB B7: 270.6 -> 273.2 GiB/s), while
 // with one generation the last block's record arrives only at the walk's end
 // (8 GiB B7: 262.4 -> 258.3; profiles/r06/r06ae_fused_walk_ab.txt).
@@ -886,7 +887,7 @@ bool fused_walk(uint32_t bm, uint64_t body) {
         return (uint64_t)cus * 8;
     }();
     const bool serialWalk = !(bm <= (1u << 20) && body >= (64ull << 20));
-    return serialWalk && body / ((uint64_t)bm + 8) > 3 * kDecoders;
+    return serialWalk && body / ((uint64_t)bm + 8) > kDecoders;
 }
 
 // The fused walk + decode of an independent-block frame body into target
